@@ -1,0 +1,52 @@
+"""Build the HIP extension (libffm_amd.so) in-tree for gfx950.
+
+hipcc drives both the device (gfx950) and host code; the library exports
+the C ABI declared in include/ffm_amd.h.  Kernels are compiled with
+-ffp-contract=off (NumPy rounds every product and sum separately) and with
+IEEE float32 division and denormals, which the bit-exact parity relies on.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB_DIR = os.path.join(HERE, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libffm_amd.so")
+SOURCES = ["core_step.hip", "engine.cpp"]
+HEADERS = ["device_common.h", "kernels.h", os.path.join("..", "..", "include", "ffm_amd.h")]
+ARCH = os.environ.get("FFM_OFFLOAD_ARCH", "gfx950")
+FLAGS = [
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-fno-gpu-flush-denormals-to-zero",
+    "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall",
+]
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = SOURCES + HEADERS + [os.path.basename(__file__)]
+    return any(os.path.getmtime(os.path.join(CSRC, s) if not s.endswith("build.py") else __file__) > t
+               for s in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB_PATH
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc, *FLAGS, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

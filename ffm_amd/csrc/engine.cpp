@@ -1,0 +1,385 @@
+// engine.cpp -- C ABI (include/ffm_amd.h) over the HIP kernels.
+//
+// Owns the device state of E independent environments of one model class and
+// drives the fused step kernel.  Mirrors the reference's FloorFieldModel
+// (model/ffm_core.py:6-133): construction validates and uploads the map/SFF/
+// params (:7-21), reset places agents (:23-26), step advances (:36-104),
+// update_dff diffuses (:106-117).
+#include "../../include/ffm_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(FFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+}  // namespace
+
+struct ffm_engine {
+    ffm_engine_desc d{};
+    int HW = 0, F = 0, K = 1, block = 256;
+    bool f64 = false, mt = false;
+    float kS32 = 0, kD32 = 0, c0 = 0, c1 = 0;
+    double kS64 = 0;
+    uint32_t t = 0;
+    uint8_t* d_map = nullptr;
+    void* d_sff = nullptr;
+    uint16_t* d_free = nullptr;
+    uint16_t* d_pos = nullptr;
+    int32_t* d_cnt = nullptr;
+    float* d_dff = nullptr;
+    float* d_tmp = nullptr;
+    int32_t* d_eps = nullptr;
+    unsigned long long* d_ctr = nullptr;
+    uint32_t* d_mt_np = nullptr;
+    uint32_t* d_mt_py = nullptr;
+};
+
+extern "C" {
+
+const char* ffm_last_error(void) { return g_err.c_str(); }
+int ffm_abi_version(void) { return FFM_ABI_VERSION; }
+
+static void release(ffm_engine* e) {
+    if (!e) return;
+    (void)hipFree(e->d_map);
+    (void)hipFree(e->d_sff);
+    (void)hipFree(e->d_free);
+    (void)hipFree(e->d_pos);
+    (void)hipFree(e->d_cnt);
+    (void)hipFree(e->d_dff);
+    (void)hipFree(e->d_tmp);
+    (void)hipFree(e->d_eps);
+    (void)hipFree(e->d_ctr);
+    (void)hipFree(e->d_mt_np);
+    (void)hipFree(e->d_mt_py);
+    delete e;
+}
+
+int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
+    if (!desc || !out) return fail(FFM_E_INVALID, "null argument");
+    *out = nullptr;
+    const ffm_engine_desc& d = *desc;
+    if (d.abi_version != FFM_ABI_VERSION) return fail(FFM_E_INVALID, "abi_version mismatch");
+    if (d.variant != FFM_VARIANT_CORE) return fail(FFM_E_UNSUPPORTED, "only FFM_VARIANT_CORE is built");
+    if (d.H < 3 || d.W < 3 || (long long)d.H * d.W > 65534)
+        return fail(FFM_E_INVALID, "map must be at least 3x3 and at most 65534 cells");
+    if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
+    if (d.neighborhood != 4 && d.neighborhood != 8) return fail(FFM_E_INVALID, "neighborhood must be 4 or 8");
+    if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
+    if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
+    if (d.agent_capacity < 1 || d.agent_capacity > 65534) return fail(FFM_E_INVALID, "agent_capacity");
+    if (d.n_agents < 0 || d.n_agents > d.agent_capacity) return fail(FFM_E_INVALID, "n_agents > agent_capacity");
+    if (d.rng_mode != FFM_RNG_PHILOX && d.rng_mode != FFM_RNG_MT) return fail(FFM_E_INVALID, "rng_mode");
+    const int H = d.H, W = d.W, HW = H * W;
+    // The reference indexes neighbours without bounds checks (model/ffm_core.py:45,52):
+    // agents must never stand on the outer ring, so no border cell may be free.
+    std::vector<uint16_t> fl;
+    for (int i = 0; i < HW; i++) {
+        const int x = i / W, y = i % W;
+        const bool border = x == 0 || y == 0 || x == H - 1 || y == W - 1;
+        if (d.map[i] == 0) {
+            if (border) return fail(FFM_E_INVALID, "free cell on the map border (walls must enclose the room)");
+            fl.push_back((uint16_t)i);
+        }
+    }
+    if (d.n_agents > (int)fl.size())
+        return fail(FFM_E_INVALID, "Cannot take a larger sample than population when 'replace=False'");
+
+    ffm_engine* e = new ffm_engine();
+    e->d = d;
+    e->d.map = nullptr;
+    e->d.sff = nullptr;
+    e->HW = HW;
+    e->F = (int)fl.size();
+    e->f64 = d.sff_dtype == FFM_SFF_F64;
+    e->mt = d.rng_mode == FFM_RNG_MT;
+    // NumPy weak-scalar promotion (NEP 50): python numbers become float32 next
+    // to a float32 array (model/ffm_core.py:77,109,113).
+    e->kS32 = (float)(-d.k_S);
+    e->kD32 = (float)d.k_D;
+    e->kS64 = -d.k_S;
+    e->c0 = (float)((1.0 - d.decay) * (1.0 - d.diffuse));
+    e->c1 = (float)(d.decay * (1.0 - d.diffuse) / (double)d.neighborhood);
+
+    auto cleanup = [&](int rc) {
+        release(e);
+        return rc;
+    };
+    hipError_t he = hipSetDevice(d.device);
+    if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)));
+
+    // Envs per workgroup: fill 256 agent lanes for small envs; LDS-bounded.
+    const int A = d.agent_capacity;
+    e->block = A > 256 ? 512 : 256;
+    int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);
+    if (e->mt) K = 1;
+    while (K > 1 && ffm::core_step_smem_bytes(HW, A, K, e->f64, e->mt) > 64 * 1024) K--;
+    e->K = K;
+    if (ffm::core_step_smem_bytes(HW, A, K, e->f64, e->mt) > 160 * 1024)
+        return cleanup(fail(FFM_E_UNSUPPORTED, "env does not fit in LDS (tiled large-map kernel not built yet)"));
+
+    const size_t E = (size_t)d.n_envs;
+    const size_t sff_bytes = (size_t)HW * (e->f64 ? 8 : 4);
+#define ALLOC(p, n)                                                                                   \
+    do {                                                                                              \
+        he = hipMalloc((void**)&(p), (n));                                                            \
+        if (he != hipSuccess) return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he))); \
+    } while (0)
+    ALLOC(e->d_map, (size_t)HW);
+    ALLOC(e->d_sff, sff_bytes);
+    ALLOC(e->d_free, std::max<size_t>(1, fl.size()) * 2);
+    ALLOC(e->d_pos, E * A * 2);
+    ALLOC(e->d_cnt, E * 4);
+    ALLOC(e->d_dff, E * HW * 4);
+    ALLOC(e->d_eps, E * 4);
+    ALLOC(e->d_ctr, 4 * 8);
+    if (e->mt) {
+        ALLOC(e->d_mt_np, E * 625 * 4);
+        ALLOC(e->d_mt_py, E * 625 * 4);
+    }
+#undef ALLOC
+    he = hipMemcpy(e->d_map, d.map, HW, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemcpy(e->d_sff, d.sff, sff_bytes, hipMemcpyHostToDevice);
+    if (he == hipSuccess && !fl.empty()) he = hipMemcpy(e->d_free, fl.data(), fl.size() * 2, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemset(e->d_pos, 0xFF, E * A * 2);
+    if (he == hipSuccess) he = hipMemset(e->d_cnt, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(e->d_dff, 0, E * HW * 4);
+    if (he == hipSuccess) he = hipMemset(e->d_eps, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(e->d_ctr, 0, 32);
+    if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_np, 0, E * 625 * 4);
+    if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_py, 0, E * 625 * 4);
+    if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("init: ") + hipGetErrorString(he)));
+    *out = e;
+    return FFM_OK;
+}
+
+int ffm_engine_destroy(ffm_engine* e) {
+    if (!e) return FFM_OK;
+    (void)hipSetDevice(e->d.device);
+    (void)hipDeviceSynchronize();
+    release(e);
+    return FFM_OK;
+}
+
+static ffm::CoreStepArgs make_args(ffm_engine* e) {
+    ffm::CoreStepArgs a{};
+    a.H = e->d.H;
+    a.W = e->d.W;
+    a.HW = e->HW;
+    a.A = e->d.agent_capacity;
+    a.K = e->K;
+    a.E = e->d.n_envs;
+    a.env_base = e->d.env_base;
+    a.pos = e->d_pos;
+    a.cnt = e->d_cnt;
+    a.dff = e->d_dff;
+    a.episodes = e->d_eps;
+    a.counters = e->d_ctr;
+    a.map = e->d_map;
+    a.sff = e->d_sff;
+    a.kS32 = e->kS32;
+    a.kD32 = e->kD32;
+    a.kS64 = e->kS64;
+    a.c0 = e->c0;
+    a.c1 = e->c1;
+    a.key0 = (uint32_t)e->d.seed;
+    a.key1 = (uint32_t)(e->d.seed >> 32);
+    a.t = e->t;
+    a.auto_reset = e->d.auto_reset && !e->mt;
+    a.N = e->d.n_agents;
+    a.free_list = e->d_free;
+    a.F = e->F;
+    a.mt_np = e->d_mt_np;
+    a.mt_py = e->d_mt_py;
+    return a;
+}
+
+int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
+    if (!e || n_steps < 0) return fail(FFM_E_INVALID, "bad engine/n_steps");
+    hipStream_t s = (hipStream_t)stream;
+    for (int i = 0; i < n_steps; i++) {
+        ffm::CoreStepArgs a = make_args(e);
+        HIP_TRY(ffm::launch_core_step(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
+        e->t++;
+    }
+    return FFM_OK;
+}
+
+int ffm_engine_reset(ffm_engine* e, void* stream) {
+    if (!e) return fail(FFM_E_INVALID, "null engine");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t E = (size_t)e->d.n_envs;
+    HIP_TRY(hipMemsetAsync(e->d_dff, 0, E * e->HW * 4, s));
+    HIP_TRY(hipMemsetAsync(e->d_cnt, 0, E * 4, s));
+    HIP_TRY(hipMemsetAsync(e->d_pos, 0xFF, E * e->d.agent_capacity * 2, s));
+    if (e->mt) return FFM_OK;  // the caller uploads positions drawn from its own MT stream
+    // Philox placement, same stream as the in-kernel auto-reset (key: current t).
+    HIP_TRY(ffm::launch_core_reset(make_args(e), s));
+    e->t++;
+    return FFM_OK;
+}
+
+int ffm_engine_update_dff(ffm_engine* e, void* stream) {
+    if (!e) return fail(FFM_E_INVALID, "null engine");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n = (size_t)e->d.n_envs * e->HW;
+    if (!e->d_tmp) HIP_TRY(hipMalloc((void**)&e->d_tmp, n * 4));
+    HIP_TRY(ffm::launch_update_dff(e->d_dff, e->d_tmp, e->d.n_envs, e->d.H, e->d.W, e->d.neighborhood, e->c0,
+                                   e->c1, s));
+    HIP_TRY(hipMemcpyAsync(e->d_dff, e->d_tmp, n * 4, hipMemcpyDeviceToDevice, s));
+    return FFM_OK;
+}
+
+static int check_range(ffm_engine* e, int64_t env0, int64_t n) {
+    if (!e) return fail(FFM_E_INVALID, "null engine");
+    if (env0 < 0 || n < 0 || env0 + n > e->d.n_envs) return fail(FFM_E_INVALID, "env range out of bounds");
+    return FFM_OK;
+}
+
+int ffm_engine_set_state(ffm_engine* e, int64_t env0, int64_t n, const uint16_t* positions,
+                         const int32_t* counts, const float* dff, void* stream) {
+    int rc = check_range(e, env0, n);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int A = e->d.agent_capacity;
+    if (counts) {
+        for (int64_t i = 0; i < n; i++)
+            if (counts[i] < 0 || counts[i] > A) return fail(FFM_E_INVALID, "count out of [0, agent_capacity]");
+    }
+    if (positions && counts) {
+        // Positions must be distinct passable, non-exit cells (the reference never
+        // holds an agent on an exit: model/ffm_core.py:101-102).
+        std::vector<uint8_t> map(e->HW);
+        HIP_TRY(hipMemcpy(map.data(), e->d_map, e->HW, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> seen(e->HW, 0);
+        for (int64_t i = 0; i < n; i++) {
+            for (int j = 0; j < counts[i]; j++) {
+                const uint16_t c = positions[i * A + j];
+                if (c >= e->HW || map[c] != 0) return fail(FFM_E_INVALID, "agent on a non-free cell");
+                if (seen[c]) return fail(FFM_E_INVALID, "two agents on one cell");
+                seen[c] = 1;
+            }
+            for (int j = 0; j < counts[i]; j++) seen[positions[i * A + j]] = 0;
+        }
+    }
+    if (positions)
+        HIP_TRY(hipMemcpyAsync(e->d_pos + env0 * A, positions, (size_t)n * A * 2, hipMemcpyHostToDevice, s));
+    if (counts) HIP_TRY(hipMemcpyAsync(e->d_cnt + env0, counts, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    if (dff)
+        HIP_TRY(hipMemcpyAsync(e->d_dff + env0 * e->HW, dff, (size_t)n * e->HW * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_engine_get_state(ffm_engine* e, int64_t env0, int64_t n, uint16_t* positions, int32_t* counts,
+                         float* dff, void* stream) {
+    int rc = check_range(e, env0, n);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int A = e->d.agent_capacity;
+    if (positions)
+        HIP_TRY(hipMemcpyAsync(positions, e->d_pos + env0 * A, (size_t)n * A * 2, hipMemcpyDeviceToHost, s));
+    if (counts) HIP_TRY(hipMemcpyAsync(counts, e->d_cnt + env0, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (dff)
+        HIP_TRY(hipMemcpyAsync(dff, e->d_dff + env0 * e->HW, (size_t)n * e->HW * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_engine_set_mt_state(ffm_engine* e, int64_t env, const uint32_t* np_key, int32_t np_pos,
+                            const uint32_t* py_key, int32_t py_pos, void* stream) {
+    int rc = check_range(e, env, 1);
+    if (rc) return rc;
+    if (!e->mt) return fail(FFM_E_INVALID, "engine is not in MT mode");
+    if (np_pos < 0 || np_pos > 624 || py_pos < 0 || py_pos > 624) return fail(FFM_E_INVALID, "MT position");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t buf[1250];
+    std::memcpy(buf, np_key, 624 * 4);
+    buf[624] = (uint32_t)np_pos;
+    std::memcpy(buf + 625, py_key, 624 * 4);
+    buf[1249] = (uint32_t)py_pos;
+    HIP_TRY(hipMemcpyAsync(e->d_mt_np + env * 625, buf, 625 * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->d_mt_py + env * 625, buf + 625, 625 * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_engine_get_mt_state(ffm_engine* e, int64_t env, uint32_t* np_key, int32_t* np_pos, uint32_t* py_key,
+                            int32_t* py_pos, void* stream) {
+    int rc = check_range(e, env, 1);
+    if (rc) return rc;
+    if (!e->mt) return fail(FFM_E_INVALID, "engine is not in MT mode");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t buf[1250];
+    HIP_TRY(hipMemcpyAsync(buf, e->d_mt_np + env * 625, 625 * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(buf + 625, e->d_mt_py + env * 625, 625 * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(np_key, buf, 624 * 4);
+    *np_pos = (int32_t)buf[624];
+    std::memcpy(py_key, buf + 625, 624 * 4);
+    *py_pos = (int32_t)buf[1249];
+    return FFM_OK;
+}
+
+int ffm_engine_get_counters(ffm_engine* e, uint64_t* counters, void* stream) {
+    if (!e || !counters) return fail(FFM_E_INVALID, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long c[4];
+    HIP_TRY(hipMemcpyAsync(c, e->d_ctr, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int i = 0; i < 4; i++) counters[i] = c[i];
+    return FFM_OK;
+}
+
+int ffm_engine_device_buffers(ffm_engine* e, ffm_device_buffers* out) {
+    if (!e || !out) return fail(FFM_E_INVALID, "null argument");
+    out->positions = e->d_pos;
+    out->counts = e->d_cnt;
+    out->dff = e->d_dff;
+    out->episodes = e->d_eps;
+    out->counters = reinterpret_cast<uint64_t*>(e->d_ctr);
+    out->mt_np = e->d_mt_np;
+    out->mt_py = e->d_mt_py;
+    return FFM_OK;
+}
+
+int ffm_engine_get_step_index(ffm_engine* e, uint32_t* t) {
+    if (!e || !t) return fail(FFM_E_INVALID, "null argument");
+    *t = e->t;
+    return FFM_OK;
+}
+
+int ffm_engine_set_step_index(ffm_engine* e, uint32_t t) {
+    if (!e) return fail(FFM_E_INVALID, "null engine");
+    e->t = t;
+    return FFM_OK;
+}
+
+int ffm_np_expf_device(const float* x, float* y, int64_t n, void* stream) {
+    HIP_TRY(ffm::launch_np_expf(x, y, n, (hipStream_t)stream));
+    return FFM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// kernels.h -- host-side launch interface of the FFM HIP kernels (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ffm {
+
+struct CoreStepArgs {
+    int H, W, HW;          // map shape
+    int A;                 // agent slots per env (stride of pos)
+    int K;                 // envs per workgroup
+    long long E;           // envs on this device
+    long long env_base;    // global id of env 0 (RNG key)
+    uint16_t* pos;         // [E][A] cell indices
+    int* cnt;              // [E]
+    float* dff;            // [E][HW]
+    int* episodes;         // [E] or nullptr
+    unsigned long long* counters;  // [4] agent_steps, exits, resets, steps
+    const uint8_t* map;    // [HW]
+    const void* sff;       // [HW] f32 or f64
+    float kS32, kD32;      // f32(-k_S), f32(k_D)
+    double kS64;           // -k_S (float64 SFF path)
+    float c0, c1;          // f32((1-decay)(1-diffuse)), f32(decay(1-diffuse)/|nb|)
+    uint32_t key0, key1;   // Philox key (seed)
+    uint32_t t;            // step index (Philox counter word 0)
+    int auto_reset, N;     // re-place N agents when an env empties
+    const uint16_t* free_list;  // [F] row-major free cells
+    int F;
+    uint32_t* mt_np;       // [E][625] MT mode
+    uint32_t* mt_py;       // [E][625]
+};
+
+size_t core_step_smem_bytes(int HW, int A, int K, bool f64, bool mt);
+hipError_t launch_core_step(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
+hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
+hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,
+                             float c1, hipStream_t s);
+hipError_t launch_np_expf(const float* x, float* y, long long n, hipStream_t s);
+
+}  // namespace ffm

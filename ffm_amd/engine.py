@@ -1,0 +1,296 @@
+"""Python binding of the C ABI in ``include/ffm_amd.h`` (ctypes).
+
+``Engine`` owns E independent environments of the reference's
+``FloorFieldModel`` (SoraKurihara/FFM ``model/ffm_core.py``) on one MI355X and
+steps all of them with one fused HIP kernel launch per step.  There is no CPU
+fallback: if the HIP library is missing, importing the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import random as _pyrandom
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libffm_amd.so")
+
+ABI_VERSION = 1
+OK, E_INVALID, E_HIP, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -4
+VARIANT_CORE = 0
+RNG_PHILOX, RNG_MT = 0, 1
+SFF_F32, SFF_F64 = 0, 1
+
+EXPORTED = [
+    "ffm_last_error", "ffm_abi_version", "ffm_engine_create", "ffm_engine_destroy",
+    "ffm_engine_reset", "ffm_engine_step", "ffm_engine_update_dff", "ffm_engine_set_state",
+    "ffm_engine_get_state", "ffm_engine_set_mt_state", "ffm_engine_get_mt_state",
+    "ffm_engine_get_counters", "ffm_engine_device_buffers", "ffm_engine_get_step_index",
+    "ffm_engine_set_step_index", "ffm_np_expf_device",
+]
+
+
+class EngineDesc(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("variant", C.c_int32),
+        ("H", C.c_int32), ("W", C.c_int32),
+        ("map", C.c_void_p), ("sff", C.c_void_p), ("sff_dtype", C.c_int32),
+        ("neighborhood", C.c_int32),
+        ("k_S", C.c_double), ("k_D", C.c_double), ("diffuse", C.c_double), ("decay", C.c_double),
+        ("n_envs", C.c_int64), ("agent_capacity", C.c_int32), ("n_agents", C.c_int32),
+        ("rng_mode", C.c_int32), ("auto_reset", C.c_int32), ("seed", C.c_uint64),
+        ("env_base", C.c_int64), ("device", C.c_int32), ("envs_per_block", C.c_int32),
+    ]
+
+
+class DeviceBuffers(C.Structure):
+    _fields_ = [
+        ("positions", C.c_void_p), ("counts", C.c_void_p), ("dff", C.c_void_p),
+        ("episodes", C.c_void_p), ("counters", C.c_void_p),
+        ("mt_np", C.c_void_p), ("mt_py", C.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def load_library():
+    """Load libffm_amd.so.  Raises (never falls back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"ffm_amd HIP library not found at {LIB_PATH}; build it with "
+            "`python -m ffm_amd.build` (hipcc --offload-arch=gfx950)")
+    L = C.CDLL(LIB_PATH)
+    P, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    L.ffm_last_error.restype = C.c_char_p
+    L.ffm_abi_version.restype = C.c_int
+    L.ffm_engine_create.argtypes = [C.POINTER(EngineDesc), C.POINTER(P)]
+    L.ffm_engine_destroy.argtypes = [P]
+    L.ffm_engine_reset.argtypes = [P, P]
+    L.ffm_engine_step.argtypes = [P, i32, P]
+    L.ffm_engine_update_dff.argtypes = [P, P]
+    L.ffm_engine_set_state.argtypes = [P, i64, i64, P, P, P, P]
+    L.ffm_engine_get_state.argtypes = [P, i64, i64, P, P, P, P]
+    L.ffm_engine_set_mt_state.argtypes = [P, i64, P, i32, P, i32, P]
+    L.ffm_engine_get_mt_state.argtypes = [P, i64, P, C.POINTER(i32), P, C.POINTER(i32), P]
+    L.ffm_engine_get_counters.argtypes = [P, P, P]
+    L.ffm_engine_device_buffers.argtypes = [P, C.POINTER(DeviceBuffers)]
+    L.ffm_engine_get_step_index.argtypes = [P, C.POINTER(C.c_uint32)]
+    L.ffm_engine_set_step_index.argtypes = [P, C.c_uint32]
+    L.ffm_np_expf_device.argtypes = [P, P, i64, P]
+    for name in EXPORTED:
+        if name != "ffm_last_error":
+            getattr(L, name).restype = C.c_int
+    if L.ffm_abi_version() != ABI_VERSION:
+        raise ImportError("libffm_amd.so ABI version mismatch; rebuild")
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc == OK:
+        return
+    msg = _lib.ffm_last_error().decode(errors="replace")
+    if rc == E_INVALID:
+        raise ValueError(msg)
+    if rc == E_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    if rc == E_NOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(getattr(stream, "cuda_stream"))
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+DEFAULT_PARAMS = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "moore"}
+
+
+class Engine:
+    """E environments of ``FloorFieldModel`` on one GPU.
+
+    rng="philox": production mode, every draw keyed by (seed, step, env, agent).
+    rng="mt": each env carries its own NumPy-legacy and CPython MT19937 state and
+    consumes it exactly like the reference (bit-exact replay).
+    """
+
+    def __init__(self, map_array, sff, n_envs: int, n_agents: int, agent_capacity: int | None = None,
+                 params: dict | None = None, rng: str = "philox", seed: int = 42,
+                 auto_reset: bool = True, env_base: int = 0, device: int = 0,
+                 envs_per_block: int = 0):
+        L = load_library()
+        p = {**DEFAULT_PARAMS, **(params or {})}
+        self.params = p
+        self.map = np.ascontiguousarray(map_array, dtype=np.uint8)
+        if self.map.ndim != 2:
+            raise ValueError("map must be 2-D")
+        self.H, self.W = self.map.shape
+        sff = np.asarray(sff)
+        if sff.shape != self.map.shape:
+            raise ValueError("sff shape must equal map shape")
+        if sff.dtype == np.float32:
+            self.sff = np.ascontiguousarray(sff)
+            sdt = SFF_F32
+        else:
+            self.sff = np.ascontiguousarray(sff, dtype=np.float64)
+            sdt = SFF_F64
+        nbn = p.get("neighborhood", "moore")
+        self.nb = 4 if nbn == "neumann" else 8
+        self.n_envs = int(n_envs)
+        self.n_agents = int(n_agents)
+        self.A = int(agent_capacity if agent_capacity is not None else max(1, n_agents))
+        self.rng = rng
+        d = EngineDesc()
+        d.abi_version = ABI_VERSION
+        d.variant = VARIANT_CORE
+        d.H, d.W = self.H, self.W
+        d.map = self.map.ctypes.data
+        d.sff = self.sff.ctypes.data
+        d.sff_dtype = sdt
+        d.neighborhood = self.nb
+        d.k_S, d.k_D = float(p["k_S"]), float(p["k_D"])
+        d.diffuse, d.decay = float(p["diffuse"]), float(p["decay"])
+        d.n_envs = self.n_envs
+        d.agent_capacity = self.A
+        d.n_agents = self.n_agents
+        d.rng_mode = {"philox": RNG_PHILOX, "mt": RNG_MT}[rng]
+        d.auto_reset = int(bool(auto_reset))
+        d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        d.env_base = int(env_base)
+        d.device = int(device)
+        d.envs_per_block = int(envs_per_block)
+        h = C.c_void_p()
+        _check(L.ffm_engine_create(C.byref(d), C.byref(h)))
+        self._h = h
+        self._L = L
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ffm_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- the hot path ------------------------------------------------------
+    def reset(self, stream=None):
+        _check(self._L.ffm_engine_reset(self._h, _stream_handle(stream)))
+
+    def step(self, n_steps: int = 1, stream=None):
+        _check(self._L.ffm_engine_step(self._h, int(n_steps), _stream_handle(stream)))
+
+    def update_dff(self, stream=None):
+        _check(self._L.ffm_engine_update_dff(self._h, _stream_handle(stream)))
+
+    # -- state transfer -----------------------------------------------------
+    def get_state(self, env0: int = 0, n: int | None = None, stream=None):
+        n = self.n_envs - env0 if n is None else n
+        pos = np.empty((n, self.A), np.uint16)
+        cnt = np.empty(n, np.int32)
+        dff = np.empty((n, self.H, self.W), np.float32)
+        _check(self._L.ffm_engine_get_state(self._h, env0, n, _ptr(pos), _ptr(cnt), _ptr(dff),
+                                            _stream_handle(stream)))
+        return pos, cnt, dff
+
+    def set_state(self, env0: int = 0, positions=None, counts=None, dff=None, stream=None):
+        n = None
+        arrs = []
+        for a, dt in ((positions, np.uint16), (counts, np.int32), (dff, np.float32)):
+            if a is None:
+                arrs.append(None)
+                continue
+            a = np.ascontiguousarray(a, dtype=dt)
+            n = a.shape[0] if n is None else n
+            if a.shape[0] != n:
+                raise ValueError("inconsistent env counts")
+            arrs.append(a)
+        if n is None:
+            return
+        if arrs[0] is not None and arrs[0].shape[1:] != (self.A,):
+            raise ValueError(f"positions must be [n, {self.A}]")
+        if arrs[2] is not None and arrs[2].reshape(n, -1).shape[1] != self.H * self.W:
+            raise ValueError("dff must be [n, H, W]")
+        _check(self._L.ffm_engine_set_state(self._h, env0, n, _ptr(arrs[0]), _ptr(arrs[1]),
+                                            _ptr(arrs[2]), _stream_handle(stream)))
+
+    def set_mt_state(self, env: int, np_key, np_pos: int, py_key, py_pos: int, stream=None):
+        nk = np.ascontiguousarray(np_key, dtype=np.uint32)
+        pk = np.ascontiguousarray(py_key, dtype=np.uint32)
+        if nk.size != 624 or pk.size != 624:
+            raise ValueError("MT19937 keys must have 624 words")
+        _check(self._L.ffm_engine_set_mt_state(self._h, env, _ptr(nk), int(np_pos), _ptr(pk),
+                                               int(py_pos), _stream_handle(stream)))
+
+    def get_mt_state(self, env: int, stream=None):
+        nk = np.empty(624, np.uint32)
+        pk = np.empty(624, np.uint32)
+        npos, ppos = C.c_int32(), C.c_int32()
+        _check(self._L.ffm_engine_get_mt_state(self._h, env, _ptr(nk), C.byref(npos), _ptr(pk),
+                                               C.byref(ppos), _stream_handle(stream)))
+        return nk, int(npos.value), pk, int(ppos.value)
+
+    # MT helpers bridging the interpreter's generators ------------------------
+    def load_rng_from(self, env: int, np_rs: np.random.RandomState | None = None,
+                      py_r: _pyrandom.Random | None = None):
+        st = (np_rs if np_rs is not None else np.random.mtrand._rand).get_state(legacy=True)
+        ps = (py_r if py_r is not None else _pyrandom._inst).getstate()
+        self.set_mt_state(env, st[1], st[2], np.asarray(ps[1][:624], np.uint32), ps[1][624])
+
+    def store_rng_to(self, env: int, np_rs: np.random.RandomState | None = None,
+                     py_r: _pyrandom.Random | None = None):
+        nk, npos, pk, ppos = self.get_mt_state(env)
+        rs = np_rs if np_rs is not None else np.random.mtrand._rand
+        st = rs.get_state(legacy=True)
+        rs.set_state(("MT19937", nk, npos, st[3], st[4]))
+        r = py_r if py_r is not None else _pyrandom._inst
+        ps = r.getstate()
+        r.setstate((ps[0], tuple(int(w) for w in pk) + (ppos,), ps[2]))
+
+    # -- telemetry -------------------------------------------------------------
+    def counters(self, stream=None) -> dict:
+        c = np.zeros(4, np.uint64)
+        _check(self._L.ffm_engine_get_counters(self._h, _ptr(c), _stream_handle(stream)))
+        return {"agent_steps": int(c[0]), "exits": int(c[1]), "resets": int(c[2]), "steps": int(c[3])}
+
+    def device_buffers(self) -> dict:
+        b = DeviceBuffers()
+        _check(self._L.ffm_engine_device_buffers(self._h, C.byref(b)))
+        return {k: b.__getattribute__(k) for k, _ in DeviceBuffers._fields_}
+
+    @property
+    def step_index(self) -> int:
+        t = C.c_uint32()
+        _check(self._L.ffm_engine_get_step_index(self._h, C.byref(t)))
+        return int(t.value)
+
+    @step_index.setter
+    def step_index(self, t: int):
+        _check(self._L.ffm_engine_set_step_index(self._h, int(t) & 0xFFFFFFFF))
+
+
+def np_expf_device(x_dev_ptr: int, y_dev_ptr: int, n: int, stream=None):
+    L = load_library()
+    _check(L.ffm_np_expf_device(x_dev_ptr, y_dev_ptr, n, _stream_handle(stream)))

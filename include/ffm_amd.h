@@ -1,0 +1,142 @@
+/*
+ * ffm_amd.h -- C ABI of the MI355X-native batched floor-field stepper.
+ *
+ * The reference (SoraKurihara/FFM) has no native boundary: its "plugin" API
+ * is the duck-typed model class consumed by the drivers.  Each entry point
+ * below is what that class's methods bind to when a binding (ctypes stub in
+ * INTEGRATION.md, or ffm_amd/engine.py) replaces the NumPy body:
+ *
+ *   ffm_engine_create      <- FloorFieldModel.__init__      model/ffm_core.py:7-21
+ *   ffm_engine_reset       <- initialize_agents / reset     model/ffm_core.py:23-26
+ *                                                           (reset(): model/ffm_ac_core.py:319-325)
+ *   ffm_engine_step        <- FloorFieldModel.step          model/ffm_core.py:36-104
+ *   ffm_engine_update_dff  <- FloorFieldModel.update_dff    model/ffm_core.py:106-117
+ *   ffm_engine_{get,set}_state    <- .positions / .dff attributes (read by
+ *                                    main.py:44-46, assigned by run_trained_ffm.py:235-236)
+ *   ffm_engine_{get,set}_mt_state <- the process-global np.random / random
+ *                                    streams the reference consumes
+ *                                    (model/ffm_core.py:25,84,95,96)
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Host pointers
+ * unless the name says "device".  Every function returns 0 on success or a
+ * negative FFM_E* code; ffm_last_error() describes the last failure of the
+ * calling thread.  One engine per thread at a time (the engine is not
+ * re-entrant, like the reference's process-global RNG).  Work is
+ * stream-ordered on the hipStream_t passed as `stream` (NULL = null stream);
+ * the get/set functions synchronise that stream.
+ *
+ * Agent positions are cell indices x*W + y stored as uint16 (maps up to
+ * 65,536 cells); positions[e][0..count[e]) are the live agents of env e in
+ * the reference's order (the row order of FloorFieldModel.positions).
+ */
+#ifndef FFM_AMD_H
+#define FFM_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFM_ABI_VERSION 1
+
+enum {
+    FFM_OK = 0,
+    FFM_E_INVALID = -1,   /* bad argument / shape / map (ValueError in the reference) */
+    FFM_E_HIP = -2,       /* HIP runtime failure */
+    FFM_E_NOMEM = -3,
+    FFM_E_UNSUPPORTED = -4
+};
+
+/* Which model class the engine steps. */
+enum {
+    FFM_VARIANT_CORE = 0      /* model/ffm_core.py FloorFieldModel */
+};
+
+/* Where the random draws come from. */
+enum {
+    FFM_RNG_PHILOX = 0,       /* counter-based, keyed (seed, step, env, agent, purpose) */
+    FFM_RNG_MT = 1            /* per-env NumPy-legacy + CPython MT19937 streams:
+                                 reproduces the reference bit for bit */
+};
+
+enum { FFM_SFF_F32 = 0, FFM_SFF_F64 = 1 };
+
+typedef struct {
+    int32_t abi_version;      /* = FFM_ABI_VERSION */
+    int32_t variant;          /* FFM_VARIANT_* */
+    int32_t H, W;             /* map shape; H*W <= 65536 */
+    const uint8_t* map;       /* host [H*W]: 0 free, 2 wall, 3 exit (others: blocked) */
+    const void* sff;          /* host [H*W] static floor field */
+    int32_t sff_dtype;        /* FFM_SFF_F32 / FFM_SFF_F64 (dtype of the .npy, model/ffm_core.py:17) */
+    int32_t neighborhood;     /* 4 = "neumann", 8 = "moore" (model/ffm_core.py:28-34) */
+    double k_S, k_D, diffuse, decay;   /* params, model/ffm_core.py:8-15 */
+    int64_t n_envs;           /* E: independent environments on this device */
+    int32_t agent_capacity;   /* A: slots per env (>= n_agents) */
+    int32_t n_agents;         /* N placed by reset / auto-reset */
+    int32_t rng_mode;         /* FFM_RNG_* */
+    int32_t auto_reset;       /* 1: an env that empties is re-placed at the start of the next step */
+    uint64_t seed;            /* Philox key */
+    int64_t env_base;         /* global id of env 0 (multi-GPU sharding keys RNG by global id) */
+    int32_t device;           /* HIP device ordinal */
+    int32_t envs_per_block;   /* 0 = auto */
+} ffm_engine_desc;
+
+typedef struct {
+    uint16_t* positions;      /* [E][A] */
+    int32_t* counts;          /* [E] */
+    float* dff;               /* [E][H*W] */
+    int32_t* episodes;        /* [E] completed resets */
+    uint64_t* counters;       /* [4]: agent_steps, exits, resets, steps */
+    uint32_t* mt_np;          /* [E][625] (MT mode only, else NULL) */
+    uint32_t* mt_py;          /* [E][625] */
+} ffm_device_buffers;
+
+typedef struct ffm_engine ffm_engine;
+
+const char* ffm_last_error(void);
+int ffm_abi_version(void);
+
+int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out);
+int ffm_engine_destroy(ffm_engine* eng);
+
+/* Place n_agents in every env (Philox mode: keyed by the engine step counter,
+ * which then advances) and zero the DFF.  MT mode places nothing: the caller
+ * draws the placement from its own generator (initialize_agents) and uploads it. */
+int ffm_engine_reset(ffm_engine* eng, void* stream);
+
+/* Advance every env by n_steps steps (model/ffm_core.py:36-104 each). */
+int ffm_engine_step(ffm_engine* eng, int32_t n_steps, void* stream);
+
+/* Only the diffusion/decay of the DFF (model/ffm_core.py:106-117). */
+int ffm_engine_update_dff(ffm_engine* eng, void* stream);
+
+/* Copy envs [env0, env0+n) in/out.  Any pointer may be NULL to skip it.
+ * positions: [n][A] uint16, counts: [n] int32, dff: [n][H*W] float32. */
+int ffm_engine_set_state(ffm_engine* eng, int64_t env0, int64_t n, const uint16_t* positions,
+                         const int32_t* counts, const float* dff, void* stream);
+int ffm_engine_get_state(ffm_engine* eng, int64_t env0, int64_t n, uint16_t* positions,
+                         int32_t* counts, float* dff, void* stream);
+
+/* MT mode: per-env generator states, 624 words + position (NumPy
+ * get_state()[1:3] / CPython getstate()[1]). */
+int ffm_engine_set_mt_state(ffm_engine* eng, int64_t env, const uint32_t* np_key, int32_t np_pos,
+                            const uint32_t* py_key, int32_t py_pos, void* stream);
+int ffm_engine_get_mt_state(ffm_engine* eng, int64_t env, uint32_t* np_key, int32_t* np_pos,
+                            uint32_t* py_key, int32_t* py_pos, void* stream);
+
+/* counters[4] = {agent_steps, exits, resets, steps} accumulated since create. */
+int ffm_engine_get_counters(ffm_engine* eng, uint64_t* counters, void* stream);
+int ffm_engine_device_buffers(ffm_engine* eng, ffm_device_buffers* out);
+/* Step counter (Philox key component); settable for replay. */
+int ffm_engine_get_step_index(ffm_engine* eng, uint32_t* t);
+int ffm_engine_set_step_index(ffm_engine* eng, uint32_t t);
+
+/* ---- numerics probes (used by the parity tests) ---------------------- */
+/* y[i] = NumPy-exact float32 exp(x[i]) computed on the device; device pointers. */
+int ffm_np_expf_device(const float* x, float* y, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FFM_AMD_H */

@@ -1,0 +1,111 @@
+"""CPU-side checks of the C ABI library and the drop-in host logic (no GPU)."""
+import ctypes
+import inspect
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ffm_amd import build as B
+    B.build()
+    from ffm_amd.engine import load_library
+    return load_library()
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "ffm_amd.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(ffm_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol(lib):
+    names = header_functions()
+    assert len(names) >= 15
+    so = ctypes.CDLL(os.path.join(ROOT, "ffm_amd", "_lib", "libffm_amd.so"))
+    for n in names:
+        assert hasattr(so, n), n
+    from ffm_amd.engine import EXPORTED
+    assert sorted(EXPORTED) == names
+
+
+def test_abi_version(lib):
+    assert lib.ffm_abi_version() == 1
+
+
+def test_engine_fails_loudly_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Engine
+    m = make_room(12, 12)
+    with pytest.raises((RuntimeError, MemoryError)):
+        Engine(m, l1_sff(m), n_envs=4, n_agents=8)
+
+
+def test_engine_validation_before_device(lib):
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Engine
+    m = make_room(12, 12)
+    with pytest.raises(ValueError):
+        Engine(m, l1_sff(m), n_envs=1, n_agents=101)
+    bad = m.copy()
+    bad[5, 0] = 0
+    with pytest.raises(ValueError):
+        Engine(bad, l1_sff(m), n_envs=1, n_agents=1)
+    with pytest.raises(ValueError):
+        Engine(m, l1_sff(m)[:5], n_envs=1, n_agents=1)
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    import ffm_amd.engine as E
+    monkeypatch.setattr(E, "_lib", None)
+    monkeypatch.setattr(E, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError):
+        E.load_library()
+
+
+def test_dropin_signature_matches_reference():
+    from ffm_amd.model.ffm_core import FloorFieldModel
+    sig = inspect.signature(FloorFieldModel.__init__)
+    assert list(sig.parameters) == ["self", "map_array", "sff_path", "N", "params"]
+    assert sig.parameters["params"].default is None
+    for meth in ("initialize_agents", "get_neighbors", "step", "update_dff", "run"):
+        assert callable(getattr(FloorFieldModel, meth))
+    assert list(inspect.signature(FloorFieldModel.run).parameters) == ["self", "save_prefix", "save_interval"]
+
+
+def test_dropin_initialization_consumes_rng_like_reference(tmp_path):
+    """initialize_agents (model/ffm_core.py:23-26) against the golden initial placements."""
+    import random
+    from golden_util import load_case
+    from ffm_amd.model.ffm_core import FloorFieldModel
+    case = load_case("neumann_12x12_N8")
+    sff_path = str(tmp_path / "sff.npy")
+    np.save(sff_path, case.sff)
+    W = case.map.shape[1]
+    for ep in case.episodes[:6]:
+        np.random.seed(ep.seed)
+        random.seed(ep.seed)
+        m = FloorFieldModel(case.map, sff_path, case.N, dict(case.params))
+        assert np.array_equal(m.positions[:, 0] * W + m.positions[:, 1], ep.init)
+        assert m.positions.dtype == np.int64
+        assert m.dff.dtype == np.float32 and not m.dff.any()
+        assert m.neighbors == [(-1, 0), (1, 0), (0, -1), (0, 1)]
+    with pytest.raises(ValueError):
+        FloorFieldModel(case.map, sff_path, 101, dict(case.params))
+
+
+def test_room_generator_matches_reference_recipe():
+    from golden_util import GOLDEN_DIR
+    from ffm_amd.data import make_room, l1_sff
+    z = np.load(os.path.join(GOLDEN_DIR, "room_12x12_reference.npz"))
+    assert np.array_equal(make_room(12, 12), z["map"])
+    s = l1_sff(make_room(12, 12))
+    assert s.dtype == z["sff"].dtype == np.float32
+    assert np.array_equal(s, z["sff"])

@@ -1,0 +1,266 @@
+"""GPU parity: the HIP step (through the C ABI) against the reference's golden
+vectors (MT replay) and against the CPU restatement (Philox mode) at scale.
+
+Bars: integer agent positions/counts bit-exact; DFF float32 bit-exact (the
+north star allows 1e-5, the kernel meets 0 ULP); RNG streams left in the same
+state as the reference's.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from golden_util import case_names, dff_hash, load_case
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+
+
+def _engine(**kw):
+    from ffm_amd.engine import Engine
+    return Engine(**kw)
+
+
+# ---------------------------------------------------------------------------
+# NumPy float32 exp on the device, every float32 in [-104, -0]
+# ---------------------------------------------------------------------------
+def test_np_expf_device_exhaustive():
+    from ffm_amd.engine import np_expf_device
+    from oracle import oracle as O
+    lo = int(np.float32(-0.0).view(np.uint32))
+    hi = int(np.float32(-104.0).view(np.uint32))
+    chunk = 1 << 26
+    y = torch.empty(chunk, dtype=torch.float32, device="cuda")
+    for start in range(lo, hi + 1, chunk):
+        n = min(chunk, hi + 1 - start)
+        bits = np.arange(start, start + n, dtype=np.uint32)
+        x_host = bits.view(np.float32)
+        x = torch.from_numpy(bits.view(np.int32)).to("cuda").view(torch.float32)
+        np_expf_device(x.data_ptr(), y.data_ptr(), n)
+        torch.cuda.synchronize()
+        got = y[:n].cpu().numpy().view(np.uint32)
+        want = O.np_expf(x_host, nthreads=16).view(np.uint32)
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, f"{bad.size} mismatches, first x={x_host[bad[0]]!r}"
+
+
+# ---------------------------------------------------------------------------
+# MT replay: every golden episode, all seeds of a case batched as envs
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", case_names())
+def test_engine_replays_reference_goldens(name):
+    case = load_case(name)
+    H, W = case.map.shape
+    E = len(case.episodes)
+    A = case.N
+    eng = _engine(map_array=case.map, sff=case.sff, n_envs=E, n_agents=0, agent_capacity=A,
+                  params=case.params, rng="mt", auto_reset=False)
+    free = np.flatnonzero(case.map.reshape(-1) == 0)
+    pos0 = np.full((E, A), 0xFFFF, np.uint16)
+    for e, ep in enumerate(case.episodes):
+        rs = np.random.RandomState(ep.seed)
+        r = random.Random(ep.seed)
+        init = free[rs.choice(len(free), case.N, replace=False)]
+        assert np.array_equal(init, ep.init)
+        pos0[e, :case.N] = init
+        eng.load_rng_from(e, rs, r)
+    eng.set_state(0, positions=pos0, counts=np.full(E, case.N, np.int32),
+                  dff=np.zeros((E, H, W), np.float32))
+    T = max(len(ep.counts) for ep in case.episodes)
+    for t in range(T):
+        eng.step(1)
+        pos, cnt, dff = eng.get_state()
+        for e, ep in enumerate(case.episodes):
+            if t >= len(ep.counts):
+                continue
+            assert cnt[e] == ep.counts[t], f"seed {ep.seed} step {t}: count"
+            assert np.array_equal(pos[e, :cnt[e]], ep.cells[t]), f"seed {ep.seed} step {t}: positions"
+            assert dff_hash(dff[e]) == int(ep.hashes[t]), f"seed {ep.seed} step {t}: DFF bits"
+            if ep.full:
+                assert np.array_equal(dff[e].view(np.uint32), ep.full[t].view(np.uint32))
+            if t == len(ep.counts) - 1:
+                rs, r = np.random.RandomState(), random.Random()
+                eng.store_rng_to(e, rs, r)
+                assert list(rs._bit_generator.random_raw(4)) == list(ep.np_tail), "np stream"
+                assert [r.getrandbits(32) for _ in range(4)] == list(ep.py_tail), "py stream"
+    eng.close()
+
+
+def test_dropin_model_runs_main_py_config():
+    """ffm_amd.model.ffm_core.FloorFieldModel driven like main.py:17-57."""
+    import os
+    import tempfile
+    from ffm_amd.model.ffm_core import FloorFieldModel
+    case = load_case("main_50x50_N100")
+    ep = case.episodes[0]
+    with tempfile.TemporaryDirectory() as td:
+        sff_path = os.path.join(td, "sff.npy")
+        np.save(sff_path, case.sff)
+        np.random.seed(ep.seed)
+        random.seed(ep.seed)
+        model = FloorFieldModel(case.map.astype(np.int32), sff_path, case.N, dict(case.params))
+        W = case.map.shape[1]
+        assert np.array_equal(model.positions[:, 0] * W + model.positions[:, 1], ep.init)
+        step = 0
+        while model.positions.shape[0] > 0:
+            model.step()
+            p = model.positions
+            assert np.array_equal(p[:, 0] * W + p[:, 1], ep.cells[step]), f"step {step}"
+            assert dff_hash(model.dff) == int(ep.hashes[step]), f"step {step}: DFF"
+            step += 1
+        assert step == len(ep.counts)
+        assert list(np.random.mtrand._rand._bit_generator.random_raw(4)) == list(ep.np_tail)
+        assert [random.getrandbits(32) for _ in range(4)] == list(ep.py_tail)
+
+
+# ---------------------------------------------------------------------------
+# Philox mode: GPU == CPU restatement at scale
+# ---------------------------------------------------------------------------
+def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0, nthreads=16):
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import oracle as O
+    m = make_room(H, W)
+    s = l1_sff(m)
+    eng = _engine(map_array=m, sff=s, n_envs=E, n_agents=N, params=params, rng="philox",
+                  seed=seed, auto_reset=True, env_base=env_base, envs_per_block=envs_per_block)
+    core = O.Core(m, s, params)
+    pos = np.full((E, N), 0xFFFF, np.uint16)
+    cnt = np.zeros(E, np.int32)
+    dff = np.zeros((E, H, W), np.float32)
+    eps = np.zeros(E, np.int32)
+    cpu_steps = 0
+    eng.reset()
+    # engine.reset() used t=0 for placement; mirror it on the CPU
+    for e in range(E):
+        pos[e] = core.reset_philox(N, seed, 0, env_base + e)
+    cnt[:] = N
+    for t in range(1, T + 1):
+        cpu_steps += core.step_philox_batch(pos, cnt, dff, eps, seed, t, True, N, env_base, nthreads)
+    eng.step(T)
+    gpos, gcnt, gdff = eng.get_state()
+    assert np.array_equal(gcnt, cnt), "counts"
+    for e in range(E):
+        assert np.array_equal(gpos[e, :cnt[e]], pos[e, :cnt[e]]), f"env {e} positions"
+    assert np.array_equal(gdff.view(np.uint32), dff.view(np.uint32)), "DFF bits"
+    c = eng.counters()
+    assert c["agent_steps"] == cpu_steps
+    assert c["resets"] == int(eps.sum())
+    assert c["steps"] == T
+    eng.close()
+    return cnt, eps
+
+
+def test_philox_config2_full_size_matches_cpu():
+    """12x12, 32 agents, 65,536 envs (BASELINE config 2) for 150 steps."""
+    cnt, eps = _philox_compare(12, 12, 32, 65536, 150,
+                               {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"})
+    assert eps.sum() > 0  # auto-reset exercised
+
+
+@pytest.mark.parametrize("params", [
+    {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "moore"},
+    {"k_S": 1.5, "k_D": 2.5, "diffuse": 0.3, "decay": 0.1, "neighborhood": "neumann"},
+])
+def test_philox_12x12_param_points(params):
+    _philox_compare(12, 12, 60, 2048, 120, params, seed=7, envs_per_block=3)
+
+
+def test_philox_config3_64x64_matches_cpu():
+    """64x64, 512 agents (BASELINE config 3), 512 envs, 60 steps."""
+    _philox_compare(64, 64, 512, 512, 60,
+                    {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"})
+
+
+def test_sharding_invariance():
+    """Envs keyed by global id: two shards == one engine (the multi-GPU contract)."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"neighborhood": "neumann"}
+    full = _engine(map_array=m, sff=s, n_envs=4096, n_agents=32, params=p, seed=3)
+    a = _engine(map_array=m, sff=s, n_envs=1000, n_agents=32, params=p, seed=3, env_base=0)
+    b = _engine(map_array=m, sff=s, n_envs=3096, n_agents=32, params=p, seed=3, env_base=1000)
+    for eng in (full, a, b):
+        eng.reset()
+        eng.step(90)
+    fp, fc, fd = full.get_state()
+    ap, ac, ad = a.get_state()
+    bp, bc, bd = b.get_state()
+    assert np.array_equal(fc, np.concatenate([ac, bc]))
+    assert np.array_equal(fd, np.concatenate([ad, bd]))
+    for e in range(4096):
+        q = ap[e] if e < 1000 else bp[e - 1000]
+        assert np.array_equal(fp[e, :fc[e]], q[:fc[e]])
+
+
+def test_full_size_invariants_and_determinism():
+    """Size-independent properties at BASELINE config 2 size."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"neighborhood": "neumann"}
+    outs = []
+    for _ in range(2):
+        eng = _engine(map_array=m, sff=s, n_envs=65536, n_agents=32, params=p, seed=11)
+        eng.reset()
+        eng.step(300)
+        outs.append(eng.get_state())
+        c = eng.counters()
+        eng.close()
+    (p1, c1, d1), (p2, c2, d2) = outs
+    assert np.array_equal(c1, c2) and np.array_equal(d1.view(np.uint32), d2.view(np.uint32))
+    assert np.array_equal(p1, p2)
+    assert (c1 >= 0).all() and (c1 <= 32).all()
+    assert (d1 >= 0).all() and np.isfinite(d1).all()
+    flat = m.reshape(-1)
+    for e in range(0, 65536, 97):
+        cells = p1[e, :c1[e]]
+        assert len(set(cells.tolist())) == len(cells)
+        assert (flat[cells] == 0).all()
+    assert c["steps"] == 300 and c["agent_steps"] > 0
+
+
+def test_update_dff_entry_point():
+    """ffm_engine_update_dff == the reference's update_dff expression."""
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import oracle as O
+    m = make_room(9, 13)
+    s = l1_sff(m)
+    rs = np.random.RandomState(5)
+    for nbname in ("neumann", "moore"):
+        p = {"diffuse": 0.3, "decay": 0.15, "neighborhood": nbname}
+        eng = _engine(map_array=m, sff=s, n_envs=3, n_agents=0, agent_capacity=4, params=p, auto_reset=False)
+        d = (rs.exponential(1.0, (3, 9, 13)) * (rs.uniform(size=(3, 9, 13)) < 0.6)).astype(np.float32)
+        eng.set_state(0, dff=d)
+        eng.update_dff()
+        _, _, got = eng.get_state()
+        core = O.Core(m, s, p)
+        for e in range(3):
+            want = d[e].copy()
+            core.update_dff(want)
+            assert np.array_equal(got[e].view(np.uint32), want.view(np.uint32))
+        eng.close()
+
+
+def test_invalid_inputs_raise():
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    with pytest.raises(ValueError):
+        _engine(map_array=m, sff=s, n_envs=1, n_agents=101)  # more agents than free cells
+    bad = m.copy()
+    bad[0, 3] = 0
+    with pytest.raises(ValueError):
+        _engine(map_array=bad, sff=s, n_envs=1, n_agents=4)  # open border
+    eng = _engine(map_array=m, sff=s, n_envs=2, n_agents=4, auto_reset=False)
+    with pytest.raises(ValueError):
+        eng.set_state(0, positions=np.zeros((1, 4), np.uint16), counts=np.array([2], np.int32))  # wall cell
+    eng.close()
