@@ -368,14 +368,13 @@ static int32_t decide_core(const ffo_core_cfg* c, int x, int y, const int32_t* o
     return cand[nc - 1];
 }
 
-void ffo_update_dff(const ffo_core_cfg* c, float* dff) {
+static void update_dff_scratch(const ffo_core_cfg* c, float* dff, float* B) {
     /* model/ffm_core.py:106-117 */
     const int H = c->H, W = c->W, HW = H * W;
     const int (*nb)[2] = nb_table(c);
     const float c0 = (float)((1.0 - c->decay) * (1.0 - c->diffuse));
     const float c1 = (float)(c->decay * (1.0 - c->diffuse) / (double)c->nb);
     const float thr = 1e-4f;
-    float* B = (float*)malloc(sizeof(float) * (size_t)HW);
     for (int i = 0; i < HW; i++) B[i] = c0 * dff[i];
     for (int x = 0; x < H; x++)
         for (int y = 0; y < W; y++) {
@@ -388,17 +387,24 @@ void ffo_update_dff(const ffo_core_cfg* c, float* dff) {
             }
             dff[x * W + y] = (a < thr) ? 0.0f : a;
         }
+}
+
+void ffo_update_dff(const ffo_core_cfg* c, float* dff) {
+    float* B = (float*)malloc(sizeof(float) * (size_t)(c->H * c->W));
+    update_dff_scratch(c, dff, B);
     free(B);
 }
 
-/* One step of one env; pos in/out, n in/out, occ is scratch [H*W] filled -1. */
+/* One step of one env; pos in/out, n in/out, occ is scratch [H*W] filled -1,
+ * work is scratch of 3*n int32 + H*W float. */
 static void core_step(const ffo_core_cfg* c, int32_t* pos, int32_t* n, float* dff,
-                      int32_t* occ, rngctx* r) {
+                      int32_t* occ, int32_t* work, rngctx* r) {
     const int W = c->W;
     const int np_ = *n;
-    int32_t* req = (int32_t*)malloc(sizeof(int32_t) * (size_t)(np_ > 0 ? np_ : 1) * 3);
+    int32_t* req = work;
     int32_t* nxt = req + np_;
     int32_t* tgt_order = nxt + np_;     /* targets in first-request order */
+    float* B = (float*)(tgt_order + np_);
     int ntg = 0;
 
     for (int i = 0; i < np_; i++) occ[pos[i]] = i;
@@ -437,8 +443,7 @@ static void core_step(const ffo_core_cfg* c, int32_t* pos, int32_t* n, float* df
     for (int i = 0; i < np_; i++)
         if (c->map[nxt[i]] != 3) pos[nn++] = nxt[i];
     *n = nn;
-    free(req);
-    ffo_update_dff(c, dff);                             /* :104 */
+    update_dff_scratch(c, dff, B);                      /* :104 */
 }
 
 int ffo_core_step_mt(const ffo_core_cfg* c, int32_t* pos, int32_t* n, float* dff,
@@ -446,8 +451,10 @@ int ffo_core_step_mt(const ffo_core_cfg* c, int32_t* pos, int32_t* n, float* dff
     const int HW = c->H * c->W;
     int32_t* occ = (int32_t*)malloc(sizeof(int32_t) * (size_t)HW);
     for (int i = 0; i < HW; i++) occ[i] = -1;
+    int32_t* work = (int32_t*)malloc(sizeof(int32_t) * (size_t)(3 * (*n) + HW + 1));
     rngctx r = {0, np_rng, py_rng, 0, 0, 0};
-    core_step(c, pos, n, dff, occ, &r);
+    core_step(c, pos, n, dff, occ, work, &r);
+    free(work);
     free(occ);
     return 0;
 }
@@ -515,6 +522,7 @@ void ffo_core_step_philox_batch(const ffo_core_cfg* c, int64_t E, int32_t A_cap,
         int32_t* occ = (int32_t*)malloc(sizeof(int32_t) * (size_t)HW);
         int32_t* p32 = (int32_t*)malloc(sizeof(int32_t) * (size_t)(A_cap > 0 ? A_cap : 1));
         uint16_t* scratch = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)HW);
+        int32_t* work = (int32_t*)malloc(sizeof(int32_t) * (size_t)(3 * (A_cap > N_reset ? A_cap : N_reset) + HW + 1));
         for (int i = 0; i < HW; i++) occ[i] = -1;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
@@ -532,13 +540,14 @@ void ffo_core_step_philox_batch(const ffo_core_cfg* c, int64_t E, int32_t A_cap,
             total += (uint64_t)n;
             for (int i = 0; i < n; i++) p32[i] = pe[i];
             rngctx r = {1, NULL, NULL, seed, t, (uint64_t)(env_base + e)};
-            core_step(c, p32, &n, de, occ, &r);
+            core_step(c, p32, &n, de, occ, work, &r);
             for (int i = 0; i < n; i++) pe[i] = (uint16_t)p32[i];
             counts[e] = n;
         }
         free(occ);
         free(p32);
         free(scratch);
+        free(work);
     }
     free(fl);
     if (agent_steps) *agent_steps = total;
