@@ -1,0 +1,221 @@
+// core_common.h -- per-agent pieces of the ffm_core step shared by the
+// wave-per-env and block-per-env kernels (model/ffm_core.py of SoraKurihara/FFM).
+//
+// Layout convention inside LDS: every per-env grid is PADDED by one cell on
+// each side (row stride PW = W + 2), so neighbour offsets are constants and no
+// bounds checks are needed.  The halo is "blocked" in the grid and 0 in the
+// DFF tile, which is exactly the zero padding of np.pad in update_dff
+// (model/ffm_core.py:111).
+//
+// Grid cell codes: 0 free, 2 blocked (wall or any non-walkable value), 3 exit,
+// AGENT_BIT | i = agent i currently there (model/ffm_ac_core.py:120-122 builds
+// the same "state map").  A cell is a candidate iff its code is 0 or 3
+// (model/ffm_core.py:52-60: walkable AND not occupied by another agent).
+#pragma once
+#include "device_common.h"
+
+namespace ffm {
+
+template <class GT>
+struct GridCodes;
+template <>
+struct GridCodes<uint8_t> {
+    static constexpr uint32_t kAgent = 0x80u, kIdx = 0x7Fu;
+};
+template <>
+struct GridCodes<uint16_t> {
+    static constexpr uint32_t kAgent = 0x8000u, kIdx = 0x7FFFu;
+};
+
+struct DrawPhilox {
+    uint32_t k0, k1, t, env, agent;
+    __device__ double get() const {
+        const uint4 w = philox(make_uint4(t, env, agent, kPurDecide << 28), k0, k1);
+        return u53(w.x, w.y);
+    }
+};
+struct DrawFixed {
+    double u;
+    __device__ double get() const { return u; }
+};
+struct DrawPending {
+    __device__ double get() const { return -1.0; }
+};
+
+// NumPy add.reduce of the candidate exps: left fold below 8 elements, 8-lane
+// pairwise at >= 8 (only reachable with the Moore neighbourhood).
+template <int NB, class T>
+__device__ __forceinline__ T np_sum(const T (&e)[NB + 1], const bool (&v)[NB + 1], int nc) {
+    if (NB == 8 && nc >= 8) {
+        int q = NB + 1;  // slot of the (at most one) invalid neighbour
+#pragma unroll
+        for (int s = NB - 1; s >= 0; s--)
+            if (!v[s]) q = s;
+        T a[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) a[j] = (j < q) ? e[j] : e[j + 1];
+        T res = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+        if (nc == 9) res += e[8];
+        return res;
+    }
+    T res = T(-0.0);
+#pragma unroll
+    for (int s = 0; s <= NB; s++)
+        if (v[s]) res += e[s];
+    return res;
+}
+
+// np.random.choice's comparison fl(cdf_k / cdf_last) > u without a float64
+// division in the common case: q = cdf_k * (1/cdf_last) is within a few ulp
+// of the correctly rounded quotient, so it decides unless it lands within
+// 2^-48 of u; only then is the exact IEEE division evaluated.
+__device__ __forceinline__ bool cdf_gt(double ck, double last, double inv_last, double u) {
+    const double q = ck * inv_last;
+    const double d = q - u;
+    if (d > 0x1p-48) return true;
+    if (d < -0x1p-48) return false;
+    return ck / last > u;
+}
+
+// decide() for one agent at padded cell pp: model/ffm_core.py:41-88.
+// Returns the padded target cell, kNoReq, or kPending (draw needed, MT pass 1).
+template <int NB, bool F64, class GT, class Draw>
+__device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const float* sff32,
+                                           const double* sff64, const float* dff, float kS32, float kD32,
+                                           double kS64, const Draw& draw) {
+    int cell[NB + 1];
+    bool v[NB + 1];
+    int nvalid = 0;
+    int exit_cell = -1;
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        const int c = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
+        cell[s] = c;
+        const uint32_t g = grid[c];
+        const bool ok = g == 0u || g == 3u;                          // :52-60
+        v[s] = ok;
+        nvalid += ok ? 1 : 0;
+        if (g == 3u && exit_cell < 0) exit_cell = c;                 // :66-72 first exit
+    }
+    if (nvalid == 0) return kNoReq;                                  // :63
+    if (exit_cell >= 0) return (uint32_t)exit_cell;
+    cell[NB] = pp;                                                   // :64 stay, last
+    v[NB] = true;
+    const int nc = nvalid + 1;
+
+    double cdf[NB + 1];
+    double last;
+    if (!F64) {
+        float sc[NB + 1], e[NB + 1];
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k <= NB; k++) {
+            if (!v[k]) { sc[k] = 0.0f; continue; }
+            const float a = kS32 * sff32[cell[k]];
+            const float b = kD32 * dff[cell[k]];
+            sc[k] = a + b;                                           // :77
+            mx = sc[k] > mx ? sc[k] : mx;                            // :78
+        }
+#pragma unroll
+        for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(sc[k] - mx) : 0.0f;   // :80
+        const float sum = np_sum<NB, float>(e, v, nc);                             // :81
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k <= NB; k++) {
+            if (v[k]) acc += (double)(e[k] / sum);                   // :83, then cumsum in choice
+            cdf[k] = acc;
+        }
+        last = acc;
+    } else {
+        double sc[NB + 1], e[NB + 1];
+        double mx = -__builtin_inf();
+#pragma unroll
+        for (int k = 0; k <= NB; k++) {
+            if (!v[k]) { sc[k] = 0.0; continue; }
+            const float b = kD32 * dff[cell[k]];
+            sc[k] = kS64 * sff64[cell[k]] + (double)b;
+            mx = sc[k] > mx ? sc[k] : mx;
+        }
+#pragma unroll
+        for (int k = 0; k <= NB; k++) e[k] = v[k] ? exp(sc[k] - mx) : 0.0;
+        const double sum = np_sum<NB, double>(e, v, nc);
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k <= NB; k++) {
+            if (v[k]) acc += e[k] / sum;
+            cdf[k] = acc;
+        }
+        last = acc;
+    }
+    const double u = draw.get();                                     // :84
+    if (u < 0.0) return kPending;
+    // np.random.choice: cdf /= cdf[-1]; idx = searchsorted(cdf, u, side="right")
+    const double inv = 1.0 / last;
+    uint32_t target = (uint32_t)cell[NB];
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        if (v[k] && !found && cdf_gt(cdf[k], last, inv, u)) {
+            found = true;
+            target = (uint32_t)cell[k];
+        }
+    }
+    return target;  // the stay slot has cdf == 1 > u
+}
+
+// The requesters of target r (padded): agents adjacent to r whose request is r.
+// who[s] = agent index at r - off(s) (or 0xFFFF), is[s] = it requests r.
+template <int NB, class GT>
+__device__ __forceinline__ int requesters(int r, int PW, const GT* grid, const uint16_t* sreq,
+                                          uint16_t (&who)[NB], bool (&is)[NB]) {
+    int m = 0;
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        const uint32_t g = grid[r - nb_dx<NB>(s) * PW - nb_dy<NB>(s)];
+        const bool ag = (g & GridCodes<GT>::kAgent) != 0u;
+        const uint16_t j = ag ? (uint16_t)(g & GridCodes<GT>::kIdx) : (uint16_t)0xFFFF;
+        const bool ok = ag && sreq[j] == (uint16_t)r;
+        who[s] = j;
+        is[s] = ok;
+        m += ok ? 1 : 0;
+    }
+    return m;
+}
+
+// Slot (neighbour index) of the k-th smallest requester.
+template <int NB>
+__device__ __forceinline__ int kth_slot(const uint16_t (&who)[NB], const bool (&is)[NB], int k) {
+    int sel = -1;
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        int rank = 0;
+#pragma unroll
+        for (int q = 0; q < NB; q++) rank += (is[q] && who[q] < who[s]) ? 1 : 0;
+        if (is[s] && rank == k) sel = s;
+    }
+    return sel;
+}
+
+// Philox-mode placement key of free-list entry j (see DESIGN.md "Placement").
+__device__ __forceinline__ uint32_t reset_key(uint32_t k0, uint32_t k1, uint32_t t, uint32_t genv, uint32_t j) {
+    return philox(make_uint4(t, genv, j, kPurReset << 28), k0, k1).x;
+}
+
+// Candidate threshold: ~2N of F keys fall below it; exact fallback = all.
+__device__ __forceinline__ uint32_t reset_threshold(int N, int F) {
+    if (N >= F) return 0xFFFFFFFFu;
+    const unsigned long long t = ((unsigned long long)(2 * N + 16) << 32) / (unsigned long long)F;
+    return t >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+__device__ __forceinline__ int unpad(int pp, int PW) {
+    const int x = pp / PW - 1, y = pp - (pp / PW) * PW - 1;
+    return x * (PW - 2) + y;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+}  // namespace ffm

@@ -2,396 +2,550 @@
 //
 // One launch advances every env by one FloorFieldModel.step()
 // (model/ffm_core.py:36-104 of SoraKurihara/FFM):
-//   decide   (:40-88)  lanes = agents; occupancy grid + DFF + SFF + map in LDS
-//   resolve  (:90-98)  lanes = agents; the first requester of a target owns it
-//   exit     (:100-102) order-preserving ballot/popcount compaction
-//   update_dff (:106-117) lanes = cells; 4/8-point stencil over the LDS copy
+//   decide     (:40-88)  lanes = agents; grid (map + occupancy), DFF, SFF in LDS
+//   resolve    (:90-98)  lanes = agents; the first requester of a target owns it
+//   exit       (:100-102) order-preserving ballot/popcount compaction
+//   update_dff (:106-117) lanes = cells; 4/8-point stencil on a zero-halo tile
 //
-// Work mapping: a workgroup holds K consecutive envs entirely in LDS
-// (DFF f32 [K][HW], occupancy u16 [K][HW], positions/requests/next u16 [K][A]),
-// so each env's state makes exactly one HBM round trip per step: positions
-// (2A B) + count (4 B) + DFF (4HW B), read once and written once.  Map and
-// SFF are shared by all envs and stay L2-resident.
+// Two kernels share the per-agent code in core_common.h:
+//
+//  * core_wave_kernel -- small envs (A <= 64): one WAVE owns one or two envs
+//    end to end (lanes 0-31 / 32-63 = the agents of env a / env b), so the
+//    whole step needs no workgroup barrier, only in-order LDS within the wave.
+//    Waves are persistent (grid-stride over env groups).  Used for BASELINE
+//    configs 1, 2 and 4 (12x12, 32 agents).
+//  * core_block_kernel -- larger envs (A up to a few thousand, H*W up to
+//    ~20k cells): a workgroup owns K >= 1 envs, phases separated by
+//    __syncthreads().  Used for config 3 (64x64, 512 agents) and main.py's
+//    50x50 / 100-agent room.
+//
+// Each env's mutable state makes exactly one HBM round trip per step:
+// positions (2A B) + count (4 B) + DFF (4HW B) read once and written once.
+// Map and SFF are shared by all envs (L2-resident, staged once per block).
 //
 // Sequential semantics in parallel:
-//   * agent order: occupancy is built from the CURRENT positions only, so
-//     decisions are independent across agents (the reference also reads only
-//     the current positions at :48-60);
-//   * dict insertion order of targets (:90): the requesters of a target T are
+//   * decisions read only the CURRENT positions (the reference builds its
+//     occupied set from self.positions, :48-60), so agents decide independently;
+//   * dict insertion order of targets (:90): the requesters of target T are
 //     the agents adjacent to T (or T's occupant, for a stay); the requester
-//     with the smallest index owns T and resolves it, which is the order the
-//     dict would visit it in;
+//     with the smallest index owns T and resolves it, which is the position T
+//     has in the dict;
 //   * RNG order: Philox draws are keyed by (t, env, agent | owner, purpose),
-//     so order is irrelevant; MT mode (reference replay) serialises the draws
-//     per env in exactly the reference's order (one lane per env, LDS state).
+//     so order does not matter; MT mode (reference replay) serialises the
+//     draws of each env on one lane in exactly the reference's order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "device_common.h"
+#include "core_common.h"
 #include "kernels.h"
 
 namespace ffm {
 
-// ---------------------------------------------------------------------------
-// decide(): candidate test, exit forcing, softmax and choice for one agent.
-// Candidates are kept in fixed slots (neighbour order, stay last) with a
-// validity mask instead of a compacted list, so every register index is static.
-// ---------------------------------------------------------------------------
-struct DrawPhilox {
-    uint32_t k0, k1, t, env, agent;
-    __device__ double get() const {
-        const uint4 w = philox(make_uint4(t, env, agent, kPurDecide << 28), k0, k1);
-        return u53(w.x, w.y);
-    }
-};
-struct DrawFixed {
-    double u;
-    __device__ double get() const { return u; }
-};
-struct DrawPending {
-    __device__ double get() const { return -1.0; }
-};
-
-template <int NB>
-__device__ __forceinline__ float sum_f32(const float (&e)[NB + 1], const bool (&v)[NB + 1], int nc) {
-    // NumPy add.reduce: left fold below 8 elements, 8-lane pairwise at >= 8.
-    if (NB == 8 && nc >= 8) {
-        int q = NB + 1;  // slot of the (at most one) invalid neighbour
-#pragma unroll
-        for (int s = NB - 1; s >= 0; s--)
-            if (!v[s]) q = s;
-        float a[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) a[j] = (j < q) ? e[j] : e[j + 1];
-        float res = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-        if (nc == 9) res += e[8];
-        return res;
-    }
-    float res = -0.0f;
-#pragma unroll
-    for (int s = 0; s <= NB; s++)
-        if (v[s]) res += e[s];
-    return res;
-}
-
-template <int NB>
-__device__ __forceinline__ double sum_f64(const double (&e)[NB + 1], const bool (&v)[NB + 1], int nc) {
-    if (NB == 8 && nc >= 8) {
-        int q = NB + 1;
-#pragma unroll
-        for (int s = NB - 1; s >= 0; s--)
-            if (!v[s]) q = s;
-        double a[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) a[j] = (j < q) ? e[j] : e[j + 1];
-        double res = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-        if (nc == 9) res += e[8];
-        return res;
-    }
-    double res = -0.0;
-#pragma unroll
-    for (int s = 0; s <= NB; s++)
-        if (v[s]) res += e[s];
-    return res;
-}
-
-template <int NB, bool F64, class Draw>
-__device__ __forceinline__ uint32_t decide(int x, int y, int W, const uint8_t* smap, const float* ssff32,
-                                           const double* ssff64, const float* sdff, const uint16_t* socc,
-                                           float kS32, float kD32, double kS64, const Draw& draw) {
-    int cell[NB + 1];
-    bool v[NB + 1];
-    int nvalid = 0;
-    int exit_cell = -1;
-#pragma unroll
-    for (int s = 0; s < NB; s++) {
-        const int c = (x + nb_dx<NB>(s)) * W + (y + nb_dy<NB>(s));
-        cell[s] = c;
-        const uint8_t m = smap[c];
-        const bool ok = (m == 0 || m == 3) && socc[c] == kEmpty;      // :52-60
-        v[s] = ok;
-        nvalid += ok ? 1 : 0;
-        if (ok && m == 3 && exit_cell < 0) exit_cell = c;           // :66-72
-    }
-    if (nvalid == 0) return kNoReq;                                  // :63
-    if (exit_cell >= 0) return (uint32_t)exit_cell;
-    cell[NB] = x * W + y;                                            // :64 stay
-    v[NB] = true;
-    const int nc = nvalid + 1;
-
-    double cdf[NB + 1];
-    double last;
-    if (!F64) {
-        float s[NB + 1], e[NB + 1];
-        float mx = -__builtin_inff();
-#pragma unroll
-        for (int k = 0; k <= NB; k++) {
-            const float a = kS32 * ssff32[cell[k]];
-            const float b = kD32 * sdff[cell[k]];
-            s[k] = a + b;                                            // :77
-            if (v[k]) mx = s[k] > mx ? s[k] : mx;                    // :78
-        }
-#pragma unroll
-        for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(s[k] - mx) : 0.0f;   // :80
-        const float sum = sum_f32<NB>(e, v, nc);                                 // :81
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k <= NB; k++) {
-            if (v[k]) acc += (double)(e[k] / sum);                   // :83 + cumsum in choice
-            cdf[k] = acc;
-        }
-        last = acc;
-    } else {
-        double s[NB + 1], e[NB + 1];
-        double mx = -__builtin_inf();
-#pragma unroll
-        for (int k = 0; k <= NB; k++) {
-            const float b = kD32 * sdff[cell[k]];
-            s[k] = kS64 * ssff64[cell[k]] + (double)b;
-            if (v[k]) mx = s[k] > mx ? s[k] : mx;
-        }
-#pragma unroll
-        for (int k = 0; k <= NB; k++) e[k] = v[k] ? exp(s[k] - mx) : 0.0;
-        const double sum = sum_f64<NB>(e, v, nc);
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k <= NB; k++) {
-            if (v[k]) acc += e[k] / sum;
-            cdf[k] = acc;
-        }
-        last = acc;
-    }
-    const double u = draw.get();                                     // :84
-    if (u < 0.0) return kPending;
-    // np.random.choice: cdf /= cdf[-1]; searchsorted(u, side="right")
-    uint32_t target = (uint32_t)cell[NB];
-    bool found = false;
-#pragma unroll
-    for (int k = 0; k <= NB; k++) {
-        if (v[k] && !found && cdf[k] / last > u) {
-            found = true;
-            target = (uint32_t)cell[k];
-        }
-    }
-    return target;
-}
-
-// ---------------------------------------------------------------------------
-// Requesters of target r: the agents adjacent to r whose request is r.
-// Returns m = number of requesters, sets owner (smallest index) and, for
-// rank k, the k-th smallest requester in *sel.
-// ---------------------------------------------------------------------------
-template <int NB>
-__device__ __forceinline__ int requesters(int r, int H, int W, const uint16_t* socc, const uint16_t* sreq,
-                                          uint16_t (&who)[NB], bool (&is)[NB]) {
-    const int rx = r / W, ry = r - (r / W) * W;
-    int m = 0;
-#pragma unroll
-    for (int s = 0; s < NB; s++) {
-        const int cx = rx - nb_dx<NB>(s), cy = ry - nb_dy<NB>(s);
-        bool ok = false;
-        uint16_t j = kEmpty;
-        if (cx >= 0 && cx < H && cy >= 0 && cy < W) {
-            j = socc[cx * W + cy];
-            ok = (j != kEmpty) && sreq[j] == (uint16_t)r;
-        }
-        who[s] = j;
-        is[s] = ok;
-        m += ok ? 1 : 0;
-    }
-    return m;
-}
-
-template <int NB>
-__device__ __forceinline__ uint16_t kth_requester(const uint16_t (&who)[NB], const bool (&is)[NB], int k) {
-    uint16_t sel = kEmpty;
-#pragma unroll
-    for (int s = 0; s < NB; s++) {
-        int rank = 0;
-#pragma unroll
-        for (int q = 0; q < NB; q++) rank += (is[q] && who[q] < who[s]) ? 1 : 0;
-        if (is[s] && rank == k) sel = who[s];
-    }
-    return sel;
-}
-
-// ---------------------------------------------------------------------------
-// LDS carve-up, shared by host (size) and device (pointers).
-// ---------------------------------------------------------------------------
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-struct Carve {
-    size_t map, sff, dff, occ, pos, req, nxt, misc, mt, u, flag, total;
+// ===========================================================================
+// Wave kernel: EW envs per wave, AL = 64 / EW agent lanes per env.
+// ===========================================================================
+struct WaveCarve {
+    size_t grid, dff, req, nxt, u, flag, keys, per_wave;
 };
 
-__host__ __device__ inline Carve carve(int HW, int A, int K, bool f64, bool mt) {
-    Carve c;
+__host__ __device__ inline WaveCarve wave_carve(int PHW, int AL, int EW, int F, bool mt, bool reset) {
+    WaveCarve c;
     size_t o = 0;
-    c.map = o;  o += align16((size_t)HW);
-    c.sff = o;  o += align16((size_t)HW * (f64 ? 8 : 4));
-    c.dff = o;  o += align16((size_t)K * HW * 4);
-    c.occ = o;  o += align16((size_t)K * HW * 2);
+    c.grid = o; o += align16((size_t)EW * PHW);            // u8 codes
+    c.dff = o;  o += align16((size_t)EW * PHW * 4);        // f32 tile, zero halo
+    c.req = o;  o += align16((size_t)EW * AL * 2);
+    c.nxt = o;  o += align16((size_t)EW * AL * 2);
+    c.u = o;    o += mt ? align16((size_t)EW * AL * 8) : 0;
+    c.flag = o; o += mt ? align16((size_t)EW * AL * 2) : 0;
+    c.keys = o; o += reset ? align16((size_t)F * 8) : 0;
+    c.per_wave = o;
+    return c;
+}
+
+__host__ __device__ inline size_t wave_shared_bytes(int PHW) { return align16((size_t)PHW) + align16((size_t)PHW * 4); }
+
+size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves) {
+    const int EW = A <= 32 ? 2 : 1;
+    const int PHW = (H + 2) * (W + 2);
+    return wave_shared_bytes(PHW) + (size_t)waves * wave_carve(PHW, 64 / EW, EW, F, mt, reset).per_wave;
+}
+
+// Philox placement of one env into slot_cell[0..N) (padded cells): all 64 lanes.
+__device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned long long* keys, uint16_t* slot_cell,
+                               int PW, int W, int lane) {
+    const int F = a.F, N = a.N;
+    uint32_t T = reset_threshold(N, F);
+    int C = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        C = 0;
+        for (int j0 = 0; j0 < F; j0 += 64) {
+            const int j = j0 + lane;
+            uint32_t k = 0;
+            bool cand = false;
+            if (j < F) {
+                k = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
+                cand = k <= T;
+            }
+            const unsigned long long m = __ballot(cand);
+            if (cand) keys[C + __popcll(m & ((1ull << lane) - 1ull))] = ((unsigned long long)k << 32) | (unsigned)j;
+            C += __popcll(m);
+        }
+        if (C >= N || T == 0xFFFFFFFFu) break;
+        T = 0xFFFFFFFFu;
+    }
+    wave_sync();
+    for (int i = lane; i < C; i += 64) {
+        const unsigned long long ki = keys[i];
+        int rank = 0;
+        for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
+        if (rank < N) {
+            const int cell = a.free_list[(int)(ki & 0xFFFFu)];
+            const int x = cell / W, y = cell - (cell / W) * W;
+            slot_cell[rank] = (uint16_t)((x + 1) * PW + y + 1);
+        }
+    }
+    wave_sync();
+}
+
+template <int NB, bool MT, int EW, int HT, int WT>
+__global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    using GT = uint8_t;
+    constexpr int AL = 64 / EW;
+    const int H = HT ? HT : a.H, W = WT ? WT : a.W;
+    const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
+    const int A = a.A;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int sub = lane / AL, al = lane - sub * AL;
+    const bool do_reset = !MT && a.auto_reset;
+
+    uint8_t* pmap = smem;
+    float* psff = reinterpret_cast<float*>(smem + align16((size_t)PHW));
+    const WaveCarve cv = wave_carve(PHW, AL, EW, a.F, MT, do_reset);
+    unsigned char* wbase = smem + wave_shared_bytes(PHW) + (size_t)wv * cv.per_wave;
+    GT* grid = reinterpret_cast<GT*>(wbase + cv.grid);
+    float* tile = reinterpret_cast<float*>(wbase + cv.dff);
+    uint16_t* sreq = reinterpret_cast<uint16_t*>(wbase + cv.req);
+    uint16_t* snxt = reinterpret_cast<uint16_t*>(wbase + cv.nxt);
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
+
+    // Block-shared padded map and SFF (host-prepared padded copies).
+    for (int i = threadIdx.x; i < PHW; i += 256) {
+        pmap[i] = a.pmap[i];
+        psff[i] = reinterpret_cast<const float*>(a.psff)[i];
+    }
+    // Zero this wave's DFF tiles once: the halo stays zero for every env it handles.
+    for (int i = lane; i < EW * PHW; i += 64) tile[i] = 0.0f;
+    __syncthreads();
+
+    const long long ngroups = (a.E + EW - 1) / EW;
+    const long long wstride = (long long)gridDim.x * 4;
+    unsigned long long acc_steps = 0, acc_exits = 0, acc_resets = 0;
+
+    for (long long g = (long long)blockIdx.x * 4 + wv; g < ngroups; g += wstride) {
+        const long long e = g * EW + sub;
+        const bool env_ok = e < a.E;
+        const uint32_t genv = (uint32_t)(a.env_base + e);
+        float* dk = tile + sub * PHW;
+        GT* gk = grid + sub * PHW;
+        uint16_t* rq = sreq + sub * AL;
+        uint16_t* nx = snxt + sub * AL;
+
+        // ---- HBM -> registers/LDS: count, positions, DFF -------------------
+        int cnt = env_ok ? a.cnt[e] : 0;
+        const bool rs = do_reset && env_ok && cnt == 0;
+        int pp = -1;
+        if (env_ok && al < A && al < cnt) {
+            const int c = a.pos[e * A + al];
+            const int x = c / W, y = c - (c / W) * W;
+            pp = (x + 1) * PW + y + 1;
+        }
+        const long long cbase = g * EW * (long long)HW;
+        const long long clim = (a.E - g * EW) * (long long)HW;
+        const int ncell = (int)(clim < (long long)EW * HW ? clim : (long long)EW * HW);
+        for (int c = lane; c < ncell; c += 64) {
+            const int s = c / HW, cell = c - s * HW;
+            const int x = cell / W, y = cell - (cell / W) * W;
+            tile[s * PHW + (x + 1) * PW + y + 1] = a.dff[cbase + c];
+        }
+        // grid <- map codes
+        for (int i = lane; i < EW * PHW; i += 64) {
+            const int s = i / PHW;
+            grid[i] = pmap[i - s * PHW];
+        }
+        wave_sync();
+
+        // ---- on-device auto-reset (Philox placement) ------------------------
+        if (do_reset) {
+#pragma unroll
+            for (int s = 0; s < EW; s++) {
+                const bool me = rs && sub == s;
+                if (__ballot(me) == 0ull) continue;
+                const uint32_t ge = (uint32_t)(a.env_base + g * EW + s);
+                wave_reset_env(a, ge, keys, snxt + s * AL, PW, W, lane);
+                for (int i = lane; i < HW; i += 64) {   // zero the env's DFF interior
+                    const int x = i / W, y = i - (i / W) * W;
+                    tile[s * PHW + (x + 1) * PW + y + 1] = 0.0f;
+                }
+                wave_sync();
+            }
+            if (rs) {
+                cnt = a.N;
+                pp = al < cnt ? (int)nx[al] : -1;
+            }
+            wave_sync();
+        }
+        acc_steps += (al == 0 && env_ok) ? (unsigned long long)cnt : 0ull;
+        acc_resets += (al == 0 && rs) ? 1ull : 0ull;
+        const bool live = pp >= 0;
+
+        // ---- occupancy marks; default next = stay -----------------------------
+        if (live) gk[pp] = (GT)(GridCodes<GT>::kAgent | (uint32_t)al);
+        rq[al] = kNoReq;
+        nx[al] = (uint16_t)(live ? pp : 0);
+        wave_sync();
+
+        // ---- decide (model/ffm_core.py:40-88) --------------------------------------
+        uint32_t r = kNoReq;
+        if (live) {
+            if (MT) {
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, DrawPending{});
+            } else {
+                const DrawPhilox d{a.key0, a.key1, a.t, genv, (uint32_t)al};
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, d);
+            }
+        }
+        if (MT) {
+            double* su = reinterpret_cast<double*>(wbase + cv.u) + sub * AL;
+            const unsigned long long pend = __ballot(r == kPending);
+            if (al == 0 && env_ok) {
+                uint32_t* mt_np = a.mt_np + e * 625;
+                unsigned long long mk = (pend >> (sub * AL)) & (AL == 64 ? ~0ull : ((1ull << AL) - 1ull));
+                while (mk) {
+                    const int i = __builtin_ctzll(mk);
+                    mk &= mk - 1ull;
+                    su[i] = mt_u53(mt_np);
+                }
+            }
+            wave_sync();
+            if (r == kPending)
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]});
+        }
+        if (live) rq[al] = (uint16_t)r;
+        wave_sync();
+
+        // ---- resolve (model/ffm_core.py:90-98) ---------------------------------------
+        uint16_t who[NB];
+        bool is[NB];
+        const bool moving = live && r != kNoReq && (int)r != pp;
+        int m = 0, s0 = -1;
+        bool owner = false;
+        if (moving) {
+            m = requesters<NB, GT>((int)r, PW, gk, rq, who, is);
+            s0 = kth_slot<NB>(who, is, 0);
+            owner = s0 >= 0 && who[s0] == al;
+        }
+        if (MT) {
+            uint16_t* fl = reinterpret_cast<uint16_t*>(wbase + cv.flag) + sub * AL;
+            const int fr_m = (owner && m >= 2) ? m : 0;
+            fl[al] = (uint16_t)fr_m;
+            const unsigned long long cont = __ballot(fr_m >= 2);
+            wave_sync();
+            if (al == 0 && env_ok) {
+                uint32_t* mt_np = a.mt_np + e * 625;
+                uint32_t* mt_py = a.mt_py + e * 625;
+                unsigned long long mk = (cont >> (sub * AL)) & (AL == 64 ? ~0ull : ((1ull << AL) - 1ull));
+                while (mk) {
+                    const int i = __builtin_ctzll(mk);
+                    mk &= mk - 1ull;
+                    const double u = mt_u53(mt_np);                                    // np.random.rand()
+                    const int kk = u < 0.5 ? (int)mt_randbelow(mt_py, (uint32_t)fl[i]) : -1;  // random.choice
+                    fl[i] = (uint16_t)(kk >= 0 ? 0x100 | kk : 0x200);
+                }
+            }
+            wave_sync();
+        }
+        if (live && r != kNoReq) {
+            if ((int)r == pp) {
+                dk[pp] += 1.0f;                                                        // :91-93 (stay)
+            } else if (owner) {
+                int ws = -1;
+                if (m == 1) {
+                    ws = s0;
+                } else if (MT) {
+                    const int f = (reinterpret_cast<uint16_t*>(wbase + cv.flag) + sub * AL)[al];
+                    if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
+                } else {
+                    PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)al, kPurFriction);
+                    const double u = ps.next_u53();                                     // :95
+                    if (u < 0.5) ws = kth_slot<NB>(who, is, (int)ps.randbelow((uint32_t)m));   // :96
+                }
+                if (ws >= 0) {
+                    int wcell = (int)r;
+                    uint16_t wi = 0;
+#pragma unroll
+                    for (int s = 0; s < NB; s++)
+                        if (s == ws) {
+                            wcell = (int)r - nb_dx<NB>(s) * PW - nb_dy<NB>(s);
+                            wi = who[s];
+                        }
+                    nx[wi] = (uint16_t)r;
+                    dk[wcell] += 1.0f;                                                 // :97-98
+                }
+            }
+        }
+        wave_sync();
+
+        // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) ---------
+        const int nxt = live ? (int)nx[al] : 0;
+        const bool keep = live && pmap[nxt] != 3;
+        const unsigned long long km = __ballot(keep);
+        const unsigned long long segm = AL == 64 ? ~0ull : (((1ull << AL) - 1ull) << (sub * AL));
+        const int newidx = __popcll(km & segm & ((1ull << lane) - 1ull));
+        const int newcnt = __popcll(km & segm);
+        if (keep) a.pos[e * A + newidx] = (uint16_t)unpad(nxt, PW);
+        if (al == 0 && env_ok) {
+            a.cnt[e] = newcnt;
+            if (rs && a.episodes) a.episodes[e] += 1;
+        }
+        acc_exits += (al == 0 && env_ok) ? (unsigned long long)(cnt - newcnt) : 0ull;
+
+        // ---- update_dff (model/ffm_core.py:106-117) ---------------------------------
+        for (int c = lane; c < EW * HW; c += 64) {          // pass 1: B = c0 * D (halo stays 0)
+            const int s = c / HW, cell = c - s * HW;
+            const int x = cell / W, y = cell - (cell / W) * W;
+            float* p = tile + s * PHW + (x + 1) * PW + y + 1;
+            *p = a.c0 * *p;                                                     // :109
+        }
+        wave_sync();
+        for (int c = lane; c < ncell; c += 64) {
+            const int s = c / HW, cell = c - s * HW;
+            const int x = cell / W, y = cell - (cell / W) * W;
+            const float* p = tile + s * PHW + (x + 1) * PW + y + 1;
+            float acc = *p;
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+                const float t = a.c1 * p[nb_dx<NB>(q) * PW + nb_dy<NB>(q)];      // :113
+                acc = acc + t;
+            }
+            a.dff[cbase + c] = acc < 1e-4f ? 0.0f : acc;                        // :116-117
+        }
+        wave_sync();
+    }
+
+    // ---- counters: one atomic per wave ------------------------------------------------
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc_steps += __shfl_xor(acc_steps, off);
+        acc_exits += __shfl_xor(acc_exits, off);
+        acc_resets += __shfl_xor(acc_resets, off);
+    }
+    if (lane == 0) {
+        if (acc_steps) atomicAdd(&a.counters[0], acc_steps);
+        if (acc_exits) atomicAdd(&a.counters[1], acc_exits);
+        if (acc_resets) atomicAdd(&a.counters[2], acc_resets);
+        if (blockIdx.x == 0 && wv == 0) atomicAdd(&a.counters[3], 1ull);
+    }
+}
+
+// ===========================================================================
+// Block kernel: K envs per workgroup of BS threads.
+// ===========================================================================
+struct BlockCarve {
+    size_t map, sff, grid, dff, pos, req, nxt, misc, u, flag, keys, total;
+};
+
+__host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, bool f64, bool mt, bool reset) {
+    BlockCarve c;
+    size_t o = 0;
+    c.map = o;  o += align16((size_t)PHW);
+    c.sff = o;  o += align16((size_t)PHW * (f64 ? 8 : 4));
+    c.grid = o; o += align16((size_t)K * PHW * 2);
+    c.dff = o;  o += align16((size_t)K * PHW * 4);
     c.pos = o;  o += align16((size_t)K * A * 2);
     c.req = o;  o += align16((size_t)K * A * 2);
     c.nxt = o;  o += align16((size_t)K * A * 2);
     c.misc = o; o += align16((size_t)(8 * K + 64) * 4);
-    c.mt = o;   o += mt ? align16((size_t)K * 2 * 625 * 4) : 0;
     c.u = o;    o += mt ? align16((size_t)K * A * 8) : 0;
     c.flag = o; o += mt ? align16((size_t)K * A * 2) : 0;
+    c.keys = o; o += reset ? align16((size_t)F * 8) : 0;
     c.total = o;
     return c;
 }
 
-size_t core_step_smem_bytes(int HW, int A, int K, bool f64, bool mt) { return carve(HW, A, K, f64, mt).total; }
+size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool mt, bool reset) {
+    return block_carve((H + 2) * (W + 2), A, K, F, f64, mt, reset).total;
+}
 
-// ---------------------------------------------------------------------------
-// The fused step kernel.
-// ---------------------------------------------------------------------------
+// Block-wide exclusive prefix of a 0/1 flag over thread order (+ total).
+template <int BS>
+__device__ __forceinline__ int block_excl_scan(bool flag, int* swsum, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long mask = __ballot(flag);
+    const int lp = __popcll(mask & ((1ull << lane) - 1ull));
+    if (lane == 0) swsum[wave] = __popcll(mask);
+    __syncthreads();
+    int wp = 0, tot = 0;
+#pragma unroll
+    for (int v = 0; v < BS / 64; v++) {
+        const int c = swsum[v];
+        wp += v < wave ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return wp + lp;
+}
+
 template <int NB, bool F64, bool MT, int BS>
-__global__ __launch_bounds__(BS) void core_step_kernel(CoreStepArgs a) {
+__global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    using GT = uint16_t;
     const int tid = threadIdx.x;
-    const int H = a.H, W = a.W, HW = a.HW, A = a.A;
+    const int H = a.H, W = a.W, HW = H * W, PW = W + 2, PHW = (H + 2) * PW, A = a.A;
     const long long e0 = (long long)blockIdx.x * a.K;
     const int K = (int)((a.E - e0) < a.K ? (a.E - e0) : a.K);
-    const Carve cv = carve(HW, A, a.K, F64, MT);
-    uint8_t* smap = smem + cv.map;
-    float* ssff32 = reinterpret_cast<float*>(smem + cv.sff);
-    double* ssff64 = reinterpret_cast<double*>(smem + cv.sff);
-    float* sdff = reinterpret_cast<float*>(smem + cv.dff);
-    uint16_t* socc = reinterpret_cast<uint16_t*>(smem + cv.occ);
+    const bool do_reset = !MT && a.auto_reset;
+    const BlockCarve cv = block_carve(PHW, A, a.K, a.F, F64, MT, do_reset);
+    uint8_t* pmap = smem + cv.map;
+    float* psff32 = reinterpret_cast<float*>(smem + cv.sff);
+    double* psff64 = reinterpret_cast<double*>(smem + cv.sff);
+    GT* grid = reinterpret_cast<GT*>(smem + cv.grid);
+    float* tile = reinterpret_cast<float*>(smem + cv.dff);
     uint16_t* spos = reinterpret_cast<uint16_t*>(smem + cv.pos);
     uint16_t* sreq = reinterpret_cast<uint16_t*>(smem + cv.req);
     uint16_t* snxt = reinterpret_cast<uint16_t*>(smem + cv.nxt);
-    int* scnt = reinterpret_cast<int*>(smem + cv.misc);        // [K] count at step start
-    int* snew = scnt + a.K;                                     // [K] count after exits
-    int* sreset = snew + a.K;                                   // [K] reset flag
-    int* sseg = sreset + a.K;                                   // [K] segment base of the scan
-    int* swsum = sseg + a.K;                                    // [BS/64] wave sums
+    int* scnt = reinterpret_cast<int*>(smem + cv.misc);   // [K] count at step start
+    int* snew = scnt + a.K;                                // [K] count after exits
+    int* sreset = snew + a.K;                              // [K] reset flag
+    int* sseg = sreset + a.K;                              // [K] scan segment base
+    int* swsum = sseg + a.K;                               // [BS/64]
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + cv.keys);
 
-    const int nitems_a = K * A;
-    const int nitems_c = K * HW;
+    const int nA = K * A;
+    const int nP = K * PHW;
 
-    // ---- load shared inputs and this block's env state ----------------------
-    for (int i = tid; i < HW; i += BS) {
-        smap[i] = a.map[i];
-        if (F64) ssff64[i] = reinterpret_cast<const double*>(a.sff)[i];
-        else ssff32[i] = reinterpret_cast<const float*>(a.sff)[i];
+    // ---- load -------------------------------------------------------------------
+    for (int i = tid; i < PHW; i += BS) {
+        pmap[i] = a.pmap[i];
+        if (F64) psff64[i] = reinterpret_cast<const double*>(a.psff)[i];
+        else psff32[i] = reinterpret_cast<const float*>(a.psff)[i];
     }
-    {
-        const float* g = a.dff + e0 * HW;
-        if ((HW & 3) == 0) {
-            const float4* g4 = reinterpret_cast<const float4*>(g);
-            float4* s4 = reinterpret_cast<float4*>(sdff);
-            for (int i = tid; i < nitems_c / 4; i += BS) s4[i] = g4[i];
-        } else {
-            for (int i = tid; i < nitems_c; i += BS) sdff[i] = g[i];
-        }
-        const uint16_t* gp = a.pos + e0 * A;
-        for (int i = tid; i < nitems_a; i += BS) spos[i] = gp[i];
-        for (int i = tid; i < nitems_c; i += BS) socc[i] = kEmpty;
+    for (int i = tid; i < nP; i += BS) {
+        const int k = i / PHW, pc = i - k * PHW;
+        const int x = pc / PW - 1, y = pc - (pc / PW) * PW - 1;
+        const bool in = x >= 0 && x < H && y >= 0 && y < W;
+        tile[i] = in ? a.dff[(e0 + k) * HW + x * W + y] : 0.0f;
+        grid[i] = a.pmap[pc];
     }
     if (tid < K) {
         const int c = a.cnt[e0 + tid];
-        const bool rs = a.auto_reset && c == 0;
+        const bool rs = do_reset && c == 0;
         sreset[tid] = rs ? 1 : 0;
         scnt[tid] = rs ? a.N : c;
     }
-    if (MT) {
-        uint32_t* smt = reinterpret_cast<uint32_t*>(smem + cv.mt);
-        for (int i = tid; i < K * 625; i += BS) {
-            const int k = i / 625, w = i - k * 625;
-            smt[k * 1250 + w] = a.mt_np[(e0 + k) * 625 + w];
-            smt[k * 1250 + 625 + w] = a.mt_py[(e0 + k) * 625 + w];
+    __syncthreads();
+    for (int it = tid; it < nA; it += BS) {
+        const int k = it / A, i = it - k * A;
+        int pp = 0xFFFF;
+        if (i < scnt[k] && !sreset[k]) {
+            const int c = a.pos[(e0 + k) * A + i];
+            const int x = c / W, y = c - (c / W) * W;
+            pp = (x + 1) * PW + y + 1;
+        }
+        spos[it] = (uint16_t)pp;
+    }
+
+    // ---- on-device auto-reset (Philox placement) ------------------------------------
+    if (do_reset) {
+        for (int k = 0; k < K; k++) {
+            if (!sreset[k]) continue;   // block-uniform
+            const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
+            uint32_t T = reset_threshold(a.N, a.F);
+            int C = 0;
+            for (int attempt = 0; attempt < 2; attempt++) {
+                C = 0;
+                for (int j0 = 0; j0 < a.F; j0 += BS) {
+                    const int j = j0 + tid;
+                    uint32_t key = 0;
+                    bool cand = false;
+                    if (j < a.F) {
+                        key = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
+                        cand = key <= T;
+                    }
+                    int tot;
+                    const int ex = block_excl_scan<BS>(cand, swsum, tot);
+                    if (cand) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
+                    C += tot;
+                }
+                if (C >= a.N || T == 0xFFFFFFFFu) break;
+                T = 0xFFFFFFFFu;
+            }
+            __syncthreads();
+            for (int i = tid; i < C; i += BS) {
+                const unsigned long long ki = keys[i];
+                int rank = 0;
+                for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
+                if (rank < a.N) {
+                    const int cell = a.free_list[(int)(ki & 0xFFFFu)];
+                    const int x = cell / W, y = cell - (cell / W) * W;
+                    spos[k * A + rank] = (uint16_t)((x + 1) * PW + y + 1);
+                }
+            }
+            for (int i = tid; i < PHW; i += BS) tile[k * PHW + i] = 0.0f;
+            __syncthreads();
         }
     }
     __syncthreads();
 
-    // ---- on-device auto-reset (Philox): partial Fisher-Yates over the free list
-    if (!MT && a.auto_reset) {
-        bool any = false;
-        for (int k = 0; k < K; k++) any |= sreset[k] != 0;
-        if (any) {
-            for (int i = tid; i < K * a.F; i += BS) {
-                const int k = i / a.F, j = i - k * a.F;
-                if (sreset[k]) socc[k * HW + j] = a.free_list[j];   // scratch: free list copy
-            }
-            for (int i = tid; i < nitems_c; i += BS)
-                if (sreset[i / HW]) sdff[i] = 0.0f;
-            __syncthreads();
-            if (tid < K && sreset[tid]) {
-                uint16_t* sc = socc + tid * HW;
-                uint16_t* p = spos + tid * A;
-                PhiloxStream ps(a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + tid), 0u, kPurReset);
-                for (int s = 0; s < a.N; s++) {
-                    const uint32_t j = (uint32_t)s + ps.randbelow((uint32_t)(a.F - s));
-                    const uint16_t tmp = sc[s];
-                    sc[s] = sc[j];
-                    sc[j] = tmp;
-                    p[s] = sc[s];
-                }
-            }
-            __syncthreads();
-            for (int i = tid; i < nitems_c; i += BS)
-                if (sreset[i / HW]) socc[i] = kEmpty;
-            __syncthreads();
-        }
-    }
-
-    // ---- occupancy of the current positions -------------------------------
-    for (int it = tid; it < nitems_a; it += BS) {
+    // ---- occupancy marks --------------------------------------------------------------
+    for (int it = tid; it < nA; it += BS) {
         const int k = it / A, i = it - k * A;
-        if (i < scnt[k]) socc[k * HW + spos[it]] = (uint16_t)i;
+        if (i < scnt[k]) grid[k * PHW + spos[it]] = (GT)(GridCodes<GT>::kAgent | (uint32_t)i);
         snxt[it] = spos[it];
         sreq[it] = kNoReq;
     }
     __syncthreads();
 
-    // ---- decide (model/ffm_core.py:40-88) ----------------------------------
-    for (int it = tid; it < nitems_a; it += BS) {
+    // ---- decide (model/ffm_core.py:40-88) -----------------------------------------------
+    for (int it = tid; it < nA; it += BS) {
         const int k = it / A, i = it - k * A;
         if (i >= scnt[k]) continue;
-        const int p = spos[it];
-        const int x = p / W, y = p - (p / W) * W;
+        const int pp = spos[it];
         uint32_t r;
         if (MT) {
-            r = decide<NB, F64>(x, y, W, smap, ssff32, ssff64, sdff + k * HW, socc + k * HW, a.kS32, a.kD32,
-                                a.kS64, DrawPending{});
+            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, a.kS32, a.kD32, a.kS64,
+                                    DrawPending{});
         } else {
             const DrawPhilox d{a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i};
-            r = decide<NB, F64>(x, y, W, smap, ssff32, ssff64, sdff + k * HW, socc + k * HW, a.kS32, a.kD32,
-                                a.kS64, d);
+            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, a.kS32, a.kD32, a.kS64, d);
         }
         sreq[it] = (uint16_t)r;
     }
     __syncthreads();
 
     if (MT) {
-        // Draws in agent order from the env's NumPy stream, then redo the choice.
-        uint32_t* smt = reinterpret_cast<uint32_t*>(smem + cv.mt);
+        // NumPy stream: one draw per pending agent, in agent order; then redo the choice.
         double* su = reinterpret_cast<double*>(smem + cv.u);
         if (tid < K) {
-            uint32_t* mt_np = smt + tid * 1250;
+            uint32_t* mt_np = a.mt_np + (e0 + tid) * 625;
             for (int i = 0; i < scnt[tid]; i++)
                 if (sreq[tid * A + i] == kPending) su[tid * A + i] = mt_u53(mt_np);
         }
         __syncthreads();
-        for (int it = tid; it < nitems_a; it += BS) {
+        for (int it = tid; it < nA; it += BS) {
             const int k = it / A, i = it - k * A;
             if (i >= scnt[k] || sreq[it] != kPending) continue;
-            const int p = spos[it];
-            const int x = p / W, y = p - (p / W) * W;
-            sreq[it] = (uint16_t)decide<NB, F64>(x, y, W, smap, ssff32, ssff64, sdff + k * HW, socc + k * HW,
-                                                 a.kS32, a.kD32, a.kS64, DrawFixed{su[it]});
+            sreq[it] = (uint16_t)decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW,
+                                                     a.kS32, a.kD32, a.kS64, DrawFixed{su[it]});
         }
         __syncthreads();
-    }
 
-    // ---- resolve (model/ffm_core.py:90-98) ----------------------------------
-    if (MT) {
-        // pass 1: owners publish their multiplicity; serial draws in owner order.
+        // Owners of contested targets, then their draws in owner (= dict) order.
         uint16_t* sflag = reinterpret_cast<uint16_t*>(smem + cv.flag);
-        for (int it = tid; it < nitems_a; it += BS) {
+        for (int it = tid; it < nA; it += BS) {
             const int k = it / A, i = it - k * A;
             sflag[it] = 0;
             if (i >= scnt[k]) continue;
@@ -399,18 +553,18 @@ __global__ __launch_bounds__(BS) void core_step_kernel(CoreStepArgs a) {
             if (r == kNoReq || r == spos[it]) continue;
             uint16_t who[NB];
             bool is[NB];
-            const int m = requesters<NB>(r, H, W, socc + k * HW, sreq + k * A, who, is);
-            if (m >= 2 && kth_requester<NB>(who, is, 0) == i) sflag[it] = (uint16_t)m;
+            const int m = requesters<NB, GT>(r, PW, grid + k * PHW, sreq + k * A, who, is);
+            const int s0 = kth_slot<NB>(who, is, 0);
+            if (m >= 2 && s0 >= 0 && who[s0] == i) sflag[it] = (uint16_t)m;
         }
         __syncthreads();
-        uint32_t* smt = reinterpret_cast<uint32_t*>(smem + cv.mt);
         if (tid < K) {
-            uint32_t* mt_np = smt + tid * 1250;
-            uint32_t* mt_py = mt_np + 625;
+            uint32_t* mt_np = a.mt_np + (e0 + tid) * 625;
+            uint32_t* mt_py = a.mt_py + (e0 + tid) * 625;
             for (int i = 0; i < scnt[tid]; i++) {
                 const int m = sflag[tid * A + i];
                 if (m >= 2) {
-                    const double u = mt_u53(mt_np);                         // np.random.rand()
+                    const double u = mt_u53(mt_np);                                   // np.random.rand()
                     const int kk = u < 0.5 ? (int)mt_randbelow(mt_py, (uint32_t)m) : -1;   // random.choice
                     sflag[tid * A + i] = (uint16_t)(kk >= 0 ? 0x100 | kk : 0x200);
                 }
@@ -418,64 +572,65 @@ __global__ __launch_bounds__(BS) void core_step_kernel(CoreStepArgs a) {
         }
         __syncthreads();
     }
-    for (int it = tid; it < nitems_a; it += BS) {
+
+    // ---- resolve (model/ffm_core.py:90-98) ---------------------------------------------------
+    for (int it = tid; it < nA; it += BS) {
         const int k = it / A, i = it - k * A;
         if (i >= scnt[k]) continue;
         const int r = sreq[it];
         if (r == kNoReq) continue;
-        float* dk = sdff + k * HW;
-        if (r == spos[it]) {  // stay: the agent's own cell, nobody else can request it
-            dk[r] += 1.0f;                                                    // :93
+        float* dk = tile + k * PHW;
+        const int pp = spos[it];
+        if (r == pp) {
+            dk[pp] += 1.0f;                                                           // :91-93 (stay)
             continue;
         }
         uint16_t who[NB];
         bool is[NB];
-        const int m = requesters<NB>(r, H, W, socc + k * HW, sreq + k * A, who, is);
-        if (kth_requester<NB>(who, is, 0) != i) continue;   // not the owner
-        uint16_t w = kEmpty;
+        const int m = requesters<NB, GT>(r, PW, grid + k * PHW, sreq + k * A, who, is);
+        const int s0 = kth_slot<NB>(who, is, 0);
+        if (s0 < 0 || who[s0] != i) continue;  // not the owner
+        int ws = -1;
         if (m == 1) {
-            w = (uint16_t)i;
+            ws = s0;
         } else if (MT) {
             const int f = reinterpret_cast<uint16_t*>(smem + cv.flag)[it];
-            if (f & 0x100) w = kth_requester<NB>(who, is, f & 0xFF);
+            if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
         } else {
             PhiloxStream ps(a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i, kPurFriction);
-            const double u = ps.next_u53();                                   // :95
-            if (u < 0.5) w = kth_requester<NB>(who, is, (int)ps.randbelow((uint32_t)m));   // :96
+            const double u = ps.next_u53();                                           // :95
+            if (u < 0.5) ws = kth_slot<NB>(who, is, (int)ps.randbelow((uint32_t)m));    // :96
         }
-        if (w != kEmpty) {
-            snxt[k * A + w] = (uint16_t)r;
-            dk[spos[k * A + w]] += 1.0f;                                      // :98
+        if (ws >= 0) {
+            int wcell = r;
+            uint16_t wi = 0;
+#pragma unroll
+            for (int s = 0; s < NB; s++)
+                if (s == ws) {
+                    wcell = r - nb_dx<NB>(s) * PW - nb_dy<NB>(s);
+                    wi = who[s];
+                }
+            snxt[k * A + wi] = (uint16_t)r;
+            dk[wcell] += 1.0f;                                                        // :97-98
         }
     }
     __syncthreads();
 
-    // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) ---------
+    // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) -------------------------
     {
-        const int lane = tid & 63, wave = tid >> 6;
         int carry = 0;
-        for (int base = 0; base < nitems_a; base += BS) {
+        for (int base = 0; base < nA; base += BS) {
             const int it = base + tid;
             const int k = it / A, i = it - k * A;
-            const bool live = it < nitems_a && i < scnt[k];
-            const bool keep = live && smap[snxt[it]] != 3;
-            const unsigned long long mask = __ballot(keep);
-            const int lp = __popcll(mask & ((1ull << lane) - 1ull));
-            if (lane == 0) swsum[wave] = __popcll(mask);
+            const bool live = it < nA && i < scnt[k];
+            const bool keep = live && pmap[snxt[it]] != 3;
+            int tot;
+            const int excl = carry + block_excl_scan<BS>(keep, swsum, tot);
+            if (it < nA && i == 0) sseg[k] = excl;
             __syncthreads();
-            int wp = 0, tot = 0;
-#pragma unroll
-            for (int v = 0; v < BS / 64; v++) {
-                const int c = swsum[v];
-                wp += v < wave ? c : 0;
-                tot += c;
-            }
-            const int excl = carry + wp + lp;
-            if (it < nitems_a && i == 0) sseg[k] = excl;
-            __syncthreads();
-            if (it < nitems_a) {
+            if (it < nA) {
                 const int seg = sseg[k];
-                if (keep) spos[k * A + (excl - seg)] = snxt[it];
+                if (keep) a.pos[(e0 + k) * A + (excl - seg)] = (uint16_t)unpad(snxt[it], PW);
                 if (i == A - 1) snew[k] = excl + (keep ? 1 : 0) - seg;
             }
             carry += tot;
@@ -483,90 +638,58 @@ __global__ __launch_bounds__(BS) void core_step_kernel(CoreStepArgs a) {
         }
     }
 
-    // ---- write agents back; counters ------------------------------------------
-    {
-        uint16_t* gp = a.pos + e0 * A;
-        for (int i = tid; i < nitems_a; i += BS) gp[i] = spos[i];
-        if (tid == 0) {
-            unsigned long long steps = 0, exits = 0, resets = 0;
-            for (int k = 0; k < K; k++) {
-                steps += (unsigned long long)scnt[k];
-                exits += (unsigned long long)(scnt[k] - snew[k]);
-                resets += (unsigned long long)sreset[k];
-            }
-            atomicAdd(&a.counters[0], steps);
-            atomicAdd(&a.counters[1], exits);
-            if (resets) atomicAdd(&a.counters[2], resets);
-            if (blockIdx.x == 0) atomicAdd(&a.counters[3], 1ull);
+    // ---- counters ---------------------------------------------------------------------------
+    if (tid == 0) {
+        unsigned long long steps = 0, exits = 0, resets = 0;
+        for (int k = 0; k < K; k++) {
+            steps += (unsigned long long)scnt[k];
+            exits += (unsigned long long)(scnt[k] - snew[k]);
+            resets += (unsigned long long)sreset[k];
         }
-        if (tid < K) {
-            a.cnt[e0 + tid] = snew[tid];
-            if (sreset[tid] && a.episodes) a.episodes[e0 + tid] += 1;
-        }
-        if (MT) {
-            const uint32_t* smt = reinterpret_cast<const uint32_t*>(smem + cv.mt);
-            for (int i = tid; i < K * 625; i += BS) {
-                const int k = i / 625, w = i - k * 625;
-                a.mt_np[(e0 + k) * 625 + w] = smt[k * 1250 + w];
-                a.mt_py[(e0 + k) * 625 + w] = smt[k * 1250 + 625 + w];
-            }
-        }
+        atomicAdd(&a.counters[0], steps);
+        atomicAdd(&a.counters[1], exits);
+        if (resets) atomicAdd(&a.counters[2], resets);
+        if (blockIdx.x == 0) atomicAdd(&a.counters[3], 1ull);
+    }
+    if (tid < K) {
+        a.cnt[e0 + tid] = snew[tid];
+        if (sreset[tid] && a.episodes) a.episodes[e0 + tid] += 1;
     }
 
-    // ---- update_dff (model/ffm_core.py:106-117) --------------------------------
-    {
-        float* g = a.dff + e0 * HW;
-        for (int c = tid; c < nitems_c; c += BS) {
-            const int k = c / HW, cell = c - k * HW;
-            const int x = cell / W, y = cell - (cell / W) * W;
-            const float* dk = sdff + k * HW;
-            float acc = a.c0 * dk[cell];                          // :109  B = c0 * D
+    // ---- update_dff (model/ffm_core.py:106-117) --------------------------------------------------
+    for (int i = tid; i < nP; i += BS) tile[i] = a.c0 * tile[i];                       // :109 (halo stays 0)
+    __syncthreads();
+    for (int c = tid; c < K * HW; c += BS) {
+        const int k = c / HW, cell = c - k * HW;
+        const int x = cell / W, y = cell - (cell / W) * W;
+        const float* p = tile + k * PHW + (x + 1) * PW + y + 1;
+        float acc = *p;
 #pragma unroll
-            for (int s = 0; s < NB; s++) {
-                const int nx = x + nb_dx<NB>(s), ny = y + nb_dy<NB>(s);
-                const float b = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? a.c0 * dk[nx * W + ny] : 0.0f;
-                const float t = a.c1 * b;                         // :113
-                acc = acc + t;
-            }
-            g[c] = acc < 1e-4f ? 0.0f : acc;                      // :116-117
+        for (int q = 0; q < NB; q++) {
+            const float t = a.c1 * p[nb_dx<NB>(q) * PW + nb_dy<NB>(q)];               // :113
+            acc = acc + t;
         }
+        a.dff[e0 * HW + c] = acc < 1e-4f ? 0.0f : acc;                                // :116-117
     }
 }
 
-// ---------------------------------------------------------------------------
-// Reset every env: Philox partial Fisher-Yates over the free list (the same
-// placement the step kernel's auto-reset performs), counts = N.
-// ---------------------------------------------------------------------------
+// ===========================================================================
+// Reset every env (Philox placement, counts = N); DFF zeroed by the host.
+// ===========================================================================
 __global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint16_t* sc = reinterpret_cast<uint16_t*>(smem);
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
+    uint16_t* slot = reinterpret_cast<uint16_t*>(smem + align16((size_t)a.F * 8));
     const long long e = blockIdx.x;
-    for (int j = threadIdx.x; j < a.F; j += 64) sc[j] = a.free_list[j];
-    __syncthreads();
-    uint16_t* p = a.pos + e * a.A;
-    if (threadIdx.x == 0) {
-        PhiloxStream ps(a.key0, a.key1, a.t, (uint32_t)(a.env_base + e), 0u, kPurReset);
-        for (int s = 0; s < a.N; s++) {
-            const uint32_t j = (uint32_t)s + ps.randbelow((uint32_t)(a.F - s));
-            const uint16_t tmp = sc[s];
-            sc[s] = sc[j];
-            sc[j] = tmp;
-        }
-        a.cnt[e] = a.N;
-    }
-    __syncthreads();
-    for (int s = threadIdx.x; s < a.N; s += 64) p[s] = sc[s];
+    const int PW = a.W + 2;
+    wave_reset_env(a, (uint32_t)(a.env_base + e), keys, slot, PW, a.W, threadIdx.x);
+    for (int s = threadIdx.x; s < a.N; s += 64) a.pos[e * a.A + s] = (uint16_t)unpad(slot[s], PW);
+    if (threadIdx.x == 0) a.cnt[e] = a.N;
 }
 
-hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s) {
-    const size_t smem = align16((size_t)(a.F > 0 ? a.F : 1) * 2);
-    core_reset_kernel<<<dim3((unsigned)a.E), dim3(64), smem, s>>>(a);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
+// ===========================================================================
 // Standalone update_dff (FloorFieldModel.update_dff): src -> dst, per cell.
-// ---------------------------------------------------------------------------
+// ===========================================================================
 template <int NB>
 __global__ __launch_bounds__(256) void update_dff_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                          long long total, int H, int W, float c0, float c1) {
@@ -593,28 +716,82 @@ __global__ void np_expf_kernel(const float* __restrict__ x, float* __restrict__ 
     if (i < n) y[i] = np_expf(x[i]);
 }
 
-// ---------------------------------------------------------------------------
+// ===========================================================================
 // Host launchers.
-// ---------------------------------------------------------------------------
+// ===========================================================================
+template <int NB, bool MT, int EW, int HT, int WT>
+static hipError_t launch_wave_t(const CoreStepArgs& a, int blocks, hipStream_t s) {
+    const size_t smem = core_wave_smem_bytes(a.H, a.W, a.A, a.F, MT, !MT && a.auto_reset, 4);
+    core_wave_kernel<NB, MT, EW, HT, WT><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
+    return hipGetLastError();
+}
+
+template <int NB, bool MT, int EW, int HT, int WT>
+static int occ_wave_t(const CoreStepArgs& a) {
+    const size_t smem = core_wave_smem_bytes(a.H, a.W, a.A, a.F, MT, !MT && a.auto_reset, 4);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, core_wave_kernel<NB, MT, EW, HT, WT>, 256, smem) != hipSuccess)
+        return 0;
+    return n;
+}
+
+// Dispatch over (NB, MT, EW, dims) for the wave kernel: op 0 = launch, 1 = occupancy.
+template <int NB, bool MT, int EW>
+static hipError_t wave_dims(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
+    if (a.H == 12 && a.W == 12) {
+        if (op) { *occ = occ_wave_t<NB, MT, EW, 12, 12>(a); return hipSuccess; }
+        return launch_wave_t<NB, MT, EW, 12, 12>(a, blocks, s);
+    }
+    if (op) { *occ = occ_wave_t<NB, MT, EW, 0, 0>(a); return hipSuccess; }
+    return launch_wave_t<NB, MT, EW, 0, 0>(a, blocks, s);
+}
+
+static hipError_t wave_dispatch(const CoreStepArgs& a, int nb, bool mt, int blocks, hipStream_t s, int op,
+                                int* occ) {
+    const bool two = a.A <= 32;
+    if (nb == 4) {
+        if (mt) return two ? wave_dims<4, true, 2>(a, blocks, s, op, occ) : wave_dims<4, true, 1>(a, blocks, s, op, occ);
+        return two ? wave_dims<4, false, 2>(a, blocks, s, op, occ) : wave_dims<4, false, 1>(a, blocks, s, op, occ);
+    }
+    if (mt) return two ? wave_dims<8, true, 2>(a, blocks, s, op, occ) : wave_dims<8, true, 1>(a, blocks, s, op, occ);
+    return two ? wave_dims<8, false, 2>(a, blocks, s, op, occ) : wave_dims<8, false, 1>(a, blocks, s, op, occ);
+}
+
+hipError_t launch_core_wave(const CoreStepArgs& a, int nb, bool mt, int blocks, hipStream_t s) {
+    return wave_dispatch(a, nb, mt, blocks, s, 0, nullptr);
+}
+
+int core_wave_blocks_per_cu(const CoreStepArgs& a, int nb, bool mt) {
+    int n = 0;
+    (void)wave_dispatch(a, nb, mt, 0, nullptr, 1, &n);
+    return n;
+}
+
 template <int NB, bool F64, bool MT>
-static hipError_t launch_t(const CoreStepArgs& a, int block, hipStream_t s) {
+static hipError_t launch_block_t(const CoreStepArgs& a, int block, hipStream_t s) {
     const long long nblk = (a.E + a.K - 1) / a.K;
-    const size_t smem = carve(a.HW, a.A, a.K, F64, MT).total;
+    const size_t smem = core_block_smem_bytes(a.H, a.W, a.A, a.K, a.F, F64, MT, !MT && a.auto_reset);
     if (block == 512) {
-        core_step_kernel<NB, F64, MT, 512><<<dim3((unsigned)nblk), dim3(512), smem, s>>>(a);
+        core_block_kernel<NB, F64, MT, 512><<<dim3((unsigned)nblk), dim3(512), smem, s>>>(a);
     } else {
-        core_step_kernel<NB, F64, MT, 256><<<dim3((unsigned)nblk), dim3(256), smem, s>>>(a);
+        core_block_kernel<NB, F64, MT, 256><<<dim3((unsigned)nblk), dim3(256), smem, s>>>(a);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_core_step(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s) {
+hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s) {
     if (nb == 4) {
-        if (f64) return mt ? launch_t<4, true, true>(a, block, s) : launch_t<4, true, false>(a, block, s);
-        return mt ? launch_t<4, false, true>(a, block, s) : launch_t<4, false, false>(a, block, s);
+        if (f64) return mt ? launch_block_t<4, true, true>(a, block, s) : launch_block_t<4, true, false>(a, block, s);
+        return mt ? launch_block_t<4, false, true>(a, block, s) : launch_block_t<4, false, false>(a, block, s);
     }
-    if (f64) return mt ? launch_t<8, true, true>(a, block, s) : launch_t<8, true, false>(a, block, s);
-    return mt ? launch_t<8, false, true>(a, block, s) : launch_t<8, false, false>(a, block, s);
+    if (f64) return mt ? launch_block_t<8, true, true>(a, block, s) : launch_block_t<8, true, false>(a, block, s);
+    return mt ? launch_block_t<8, false, true>(a, block, s) : launch_block_t<8, false, false>(a, block, s);
+}
+
+hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s) {
+    const size_t smem = align16((size_t)(a.F > 0 ? a.F : 1) * 8) + align16((size_t)(a.N > 0 ? a.N : 1) * 2);
+    core_reset_kernel<<<dim3((unsigned)a.E), dim3(64), smem, s>>>(a);
+    return hipGetLastError();
 }
 
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0, float c1,

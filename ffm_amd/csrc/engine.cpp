@@ -40,11 +40,13 @@ struct ffm_engine {
     ffm_engine_desc d{};
     int HW = 0, F = 0, K = 1, block = 256;
     bool f64 = false, mt = false;
+    bool wave = false;      // wave-per-env kernel (A <= 64) vs block-per-env kernel
+    int wave_blocks = 0;    // persistent grid of the wave kernel
     float kS32 = 0, kD32 = 0, c0 = 0, c1 = 0;
     double kS64 = 0;
     uint32_t t = 0;
-    uint8_t* d_map = nullptr;
-    void* d_sff = nullptr;
+    uint8_t* d_map = nullptr;    // padded map codes
+    void* d_sff = nullptr;       // padded SFF
     uint16_t* d_free = nullptr;
     uint16_t* d_pos = nullptr;
     int32_t* d_cnt = nullptr;
@@ -130,24 +132,42 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     hipError_t he = hipSetDevice(d.device);
     if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)));
 
-    // Envs per workgroup: fill 256 agent lanes for small envs; LDS-bounded.
+    // Kernel choice.  Small envs (A <= 64, float32 SFF): one wave per env or
+    // env pair, persistent grid.  Otherwise (or when envs_per_block > 0 forces
+    // it): K envs per workgroup, LDS-bounded.
     const int A = d.agent_capacity;
+    const bool reset_lds = !e->mt && d.auto_reset;
+    e->wave = d.envs_per_block <= 0 && A <= 64 && !e->f64 &&
+              ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
     int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);
     if (e->mt) K = 1;
-    while (K > 1 && ffm::core_step_smem_bytes(HW, A, K, e->f64, e->mt) > 64 * 1024) K--;
+    while (K > 1 && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 64 * 1024) K--;
     e->K = K;
-    if (ffm::core_step_smem_bytes(HW, A, K, e->f64, e->mt) > 160 * 1024)
+    if (!e->wave && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 160 * 1024)
         return cleanup(fail(FFM_E_UNSUPPORTED, "env does not fit in LDS (tiled large-map kernel not built yet)"));
 
     const size_t E = (size_t)d.n_envs;
-    const size_t sff_bytes = (size_t)HW * (e->f64 ? 8 : 4);
+    const int PW = W + 2, PHW = (H + 2) * PW;
+    const size_t sff_bytes = (size_t)PHW * (e->f64 ? 8 : 4);
+    // Padded copies (one halo cell each side): map codes normalised to
+    // 0 free / 2 blocked / 3 exit (only ==0 and ==3 matter, model/ffm_core.py:52-53,66,101).
+    std::vector<uint8_t> pmap((size_t)PHW, 2);
+    std::vector<double> psff64((size_t)PHW, 0.0);
+    std::vector<float> psff32((size_t)PHW, 0.0f);
+    for (int x = 0; x < H; x++)
+        for (int y = 0; y < W; y++) {
+            const int i = x * W + y, p = (x + 1) * PW + y + 1;
+            pmap[p] = d.map[i] == 0 ? 0 : d.map[i] == 3 ? 3 : 2;
+            if (e->f64) psff64[p] = reinterpret_cast<const double*>(d.sff)[i];
+            else psff32[p] = reinterpret_cast<const float*>(d.sff)[i];
+        }
 #define ALLOC(p, n)                                                                                   \
     do {                                                                                              \
         he = hipMalloc((void**)&(p), (n));                                                            \
         if (he != hipSuccess) return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he))); \
     } while (0)
-    ALLOC(e->d_map, (size_t)HW);
+    ALLOC(e->d_map, (size_t)PHW);
     ALLOC(e->d_sff, sff_bytes);
     ALLOC(e->d_free, std::max<size_t>(1, fl.size()) * 2);
     ALLOC(e->d_pos, E * A * 2);
@@ -160,8 +180,10 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
         ALLOC(e->d_mt_py, E * 625 * 4);
     }
 #undef ALLOC
-    he = hipMemcpy(e->d_map, d.map, HW, hipMemcpyHostToDevice);
-    if (he == hipSuccess) he = hipMemcpy(e->d_sff, d.sff, sff_bytes, hipMemcpyHostToDevice);
+    he = hipMemcpy(e->d_map, pmap.data(), PHW, hipMemcpyHostToDevice);
+    if (he == hipSuccess)
+        he = hipMemcpy(e->d_sff, e->f64 ? (const void*)psff64.data() : (const void*)psff32.data(), sff_bytes,
+                       hipMemcpyHostToDevice);
     if (he == hipSuccess && !fl.empty()) he = hipMemcpy(e->d_free, fl.data(), fl.size() * 2, hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemset(e->d_pos, 0xFF, E * A * 2);
     if (he == hipSuccess) he = hipMemset(e->d_cnt, 0, E * 4);
@@ -171,6 +193,16 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_np, 0, E * 625 * 4);
     if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_py, 0, E * 625 * 4);
     if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("init: ") + hipGetErrorString(he)));
+    if (e->wave) {
+        int cus = 0;
+        he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device);
+        if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, "hipDeviceGetAttribute"));
+        ffm::CoreStepArgs a{};
+        a.H = H; a.W = W; a.A = A; a.F = e->F; a.auto_reset = reset_lds;
+        const int per_cu = std::max(1, ffm::core_wave_blocks_per_cu(a, d.neighborhood, e->mt));
+        const long long groups = (d.n_envs + (A <= 32 ? 2 : 1) - 1) / (A <= 32 ? 2 : 1);
+        e->wave_blocks = (int)std::min<long long>((groups + 3) / 4, (long long)cus * per_cu);
+    }
     *out = e;
     return FFM_OK;
 }
@@ -197,8 +229,8 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
     a.dff = e->d_dff;
     a.episodes = e->d_eps;
     a.counters = e->d_ctr;
-    a.map = e->d_map;
-    a.sff = e->d_sff;
+    a.pmap = e->d_map;
+    a.psff = e->d_sff;
     a.kS32 = e->kS32;
     a.kD32 = e->kD32;
     a.kS64 = e->kS64;
@@ -221,7 +253,8 @@ int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n_steps; i++) {
         ffm::CoreStepArgs a = make_args(e);
-        HIP_TRY(ffm::launch_core_step(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
+        if (e->wave) HIP_TRY(ffm::launch_core_wave(a, e->d.neighborhood, e->mt, e->wave_blocks, s));
+        else HIP_TRY(ffm::launch_core_block(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
         e->t++;
     }
     return FFM_OK;
@@ -271,13 +304,15 @@ int ffm_engine_set_state(ffm_engine* e, int64_t env0, int64_t n, const uint16_t*
     if (positions && counts) {
         // Positions must be distinct passable, non-exit cells (the reference never
         // holds an agent on an exit: model/ffm_core.py:101-102).
-        std::vector<uint8_t> map(e->HW);
-        HIP_TRY(hipMemcpy(map.data(), e->d_map, e->HW, hipMemcpyDeviceToHost));
+        const int PW = e->d.W + 2, PHW = (e->d.H + 2) * PW;
+        std::vector<uint8_t> pmap(PHW);
+        HIP_TRY(hipMemcpy(pmap.data(), e->d_map, PHW, hipMemcpyDeviceToHost));
         std::vector<uint8_t> seen(e->HW, 0);
         for (int64_t i = 0; i < n; i++) {
             for (int j = 0; j < counts[i]; j++) {
                 const uint16_t c = positions[i * A + j];
-                if (c >= e->HW || map[c] != 0) return fail(FFM_E_INVALID, "agent on a non-free cell");
+                if (c >= e->HW || pmap[(c / e->d.W + 1) * PW + c % e->d.W + 1] != 0)
+                    return fail(FFM_E_INVALID, "agent on a non-free cell");
                 if (seen[c]) return fail(FFM_E_INVALID, "two agents on one cell");
                 seen[c] = 1;
             }

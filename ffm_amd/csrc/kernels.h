@@ -17,8 +17,8 @@ struct CoreStepArgs {
     float* dff;            // [E][HW]
     int* episodes;         // [E] or nullptr
     unsigned long long* counters;  // [4] agent_steps, exits, resets, steps
-    const uint8_t* map;    // [HW]
-    const void* sff;       // [HW] f32 or f64
+    const uint8_t* pmap;   // [(H+2)*(W+2)] padded map codes: 0 free, 2 blocked, 3 exit
+    const void* psff;      // [(H+2)*(W+2)] padded SFF, f32 or f64
     float kS32, kD32;      // f32(-k_S), f32(k_D)
     double kS64;           // -k_S (float64 SFF path)
     float c0, c1;          // f32((1-decay)(1-diffuse)), f32(decay(1-diffuse)/|nb|)
@@ -31,8 +31,11 @@ struct CoreStepArgs {
     uint32_t* mt_py;       // [E][625]
 };
 
-size_t core_step_smem_bytes(int HW, int A, int K, bool f64, bool mt);
-hipError_t launch_core_step(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
+size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves);
+size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool mt, bool reset);
+hipError_t launch_core_wave(const CoreStepArgs& a, int nb, bool mt, int blocks, hipStream_t s);
+int core_wave_blocks_per_cu(const CoreStepArgs& a, int nb, bool mt);
+hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,
                              float c1, hipStream_t s);

@@ -484,25 +484,37 @@ static int free_list(const ffo_core_cfg* c, uint16_t* fl) {
     return F;
 }
 
-static void reset_with_list(const uint16_t* fl0, int F, int32_t N, uint64_t seed, uint32_t t,
-                            int64_t genv, uint16_t* scratch, uint16_t* pos_out) {
-    /* partial Fisher-Yates: slot s takes list[s + randbelow(F - s)]. */
-    memcpy(scratch, fl0, sizeof(uint16_t) * (size_t)F);
-    pstream p;
-    ps_init(&p, seed, t, (uint64_t)genv, 0u, PUR_RESET);
-    for (int s = 0; s < N; s++) {
-        uint32_t j = (uint32_t)s + ps_randbelow(&p, (uint32_t)(F - s));
-        uint16_t tmp = scratch[s]; scratch[s] = scratch[j]; scratch[j] = tmp;
-        pos_out[s] = scratch[s];
+static int cmp_u64(const void* a, const void* b) {
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* Philox-mode placement (DESIGN.md "Placement"): free-list entry j gets the
+ * key philox(t, env, j, RESET).x; the N entries with the smallest
+ * (key, j) pairs, in that order, are the agents 0..N-1.  A uniformly random
+ * ordered sample without replacement, like initialize_agents()
+ * (model/ffm_core.py:23-26), but computable in parallel. */
+static void reset_with_list(const uint16_t* fl, int F, int32_t N, uint64_t seed, uint32_t t,
+                            int64_t genv, uint64_t* scratch, uint16_t* pos_out) {
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (int j = 0; j < F; j++) {
+        const uint32_t ctr[4] = {t, (uint32_t)genv, (uint32_t)j, (uint32_t)PUR_RESET << 28};
+        uint32_t o[4];
+        ffo_philox(ctr, key, o);
+        scratch[j] = ((uint64_t)o[0] << 32) | (uint64_t)j;
     }
+    qsort(scratch, (size_t)F, sizeof(uint64_t), cmp_u64);
+    for (int s = 0; s < N; s++) pos_out[s] = fl[scratch[s] & 0xFFFFu];
 }
 
 void ffo_reset_philox(const ffo_core_cfg* c, int32_t N, uint64_t seed, uint32_t t,
                       int64_t genv, uint16_t* pos_out) {
     const int HW = c->H * c->W;
-    uint16_t* fl = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)HW * 2);
+    uint16_t* fl = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)HW);
+    uint64_t* scratch = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)HW);
     int F = free_list(c, fl);
-    reset_with_list(fl, F, N, seed, t, genv, fl + HW, pos_out);
+    reset_with_list(fl, F, N, seed, t, genv, scratch, pos_out);
+    free(scratch);
     free(fl);
 }
 
@@ -521,7 +533,7 @@ void ffo_core_step_philox_batch(const ffo_core_cfg* c, int64_t E, int32_t A_cap,
     {
         int32_t* occ = (int32_t*)malloc(sizeof(int32_t) * (size_t)HW);
         int32_t* p32 = (int32_t*)malloc(sizeof(int32_t) * (size_t)(A_cap > 0 ? A_cap : 1));
-        uint16_t* scratch = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)HW);
+        uint64_t* scratch = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)HW);
         int32_t* work = (int32_t*)malloc(sizeof(int32_t) * (size_t)(3 * (A_cap > N_reset ? A_cap : N_reset) + HW + 1));
         for (int i = 0; i < HW; i++) occ[i] = -1;
 #ifdef _OPENMP

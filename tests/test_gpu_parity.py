@@ -55,14 +55,18 @@ def test_np_expf_device_exhaustive():
 # ---------------------------------------------------------------------------
 # MT replay: every golden episode, all seeds of a case batched as envs
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kernel", ["auto", "block"])
 @pytest.mark.parametrize("name", case_names())
-def test_engine_replays_reference_goldens(name):
+def test_engine_replays_reference_goldens(name, kernel):
+    """kernel="auto": wave-per-env kernel where A <= 64 (block kernel otherwise);
+    kernel="block": the block-per-env kernel forced for every case."""
     case = load_case(name)
     H, W = case.map.shape
     E = len(case.episodes)
     A = case.N
     eng = _engine(map_array=case.map, sff=case.sff, n_envs=E, n_agents=0, agent_capacity=A,
-                  params=case.params, rng="mt", auto_reset=False)
+                  params=case.params, rng="mt", auto_reset=False,
+                  envs_per_block=1 if kernel == "block" else 0)
     free = np.flatnonzero(case.map.reshape(-1) == 0)
     pos0 = np.full((E, A), 0xFFFF, np.uint16)
     for e, ep in enumerate(case.episodes):
@@ -159,18 +163,28 @@ def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0
 
 
 def test_philox_config2_full_size_matches_cpu():
-    """12x12, 32 agents, 65,536 envs (BASELINE config 2) for 150 steps."""
+    """12x12, 32 agents, 65,536 envs (BASELINE config 2) for 150 steps (wave kernel)."""
     cnt, eps = _philox_compare(12, 12, 32, 65536, 150,
                                {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"})
     assert eps.sum() > 0  # auto-reset exercised
 
 
+@pytest.mark.parametrize("epb", [0, 3])
+@pytest.mark.parametrize("N", [32, 60])
 @pytest.mark.parametrize("params", [
     {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "moore"},
     {"k_S": 1.5, "k_D": 2.5, "diffuse": 0.3, "decay": 0.1, "neighborhood": "neumann"},
 ])
-def test_philox_12x12_param_points(params):
-    _philox_compare(12, 12, 60, 2048, 120, params, seed=7, envs_per_block=3)
+def test_philox_12x12_param_points(params, N, epb):
+    """Both kernels (epb=0: wave kernel, 2 or 1 env per wave; epb=3: block kernel, odd K)."""
+    _philox_compare(12, 12, N, 2047, 120, params, seed=7, envs_per_block=epb)
+
+
+def test_philox_odd_shapes():
+    """Non-square room, runtime-dimension wave kernel, few agents (4 envs/wave lanes idle)."""
+    _philox_compare(9, 17, 5, 777, 80, {"k_S": 2, "k_D": 1, "diffuse": 0.25, "decay": 0.3,
+                                        "neighborhood": "neumann"}, seed=123)
+    _philox_compare(20, 11, 40, 301, 80, {"neighborhood": "moore"}, seed=5, env_base=1 << 20)
 
 
 def test_philox_config3_64x64_matches_cpu():
