@@ -34,18 +34,20 @@ def _stale() -> bool:
                for s in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """Compile the library; `out`/`defines` make diagnostic variants (tools/ablate.sh)."""
+    target = out or LIB_PATH
+    if out is None and not force and not _stale():
         return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc, *FLAGS, "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    tmp = target + ".tmp"
+    cmd = [hipcc, *FLAGS, *[f"-D{d}" for d in defines], "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

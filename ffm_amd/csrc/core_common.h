@@ -77,6 +77,64 @@ __device__ __forceinline__ bool cdf_gt(double ck, double last, double inv_last, 
     return ck / last > u;
 }
 
+// np.random.choice on the exact float64 cdf: cdf /= cdf[-1];
+// idx = searchsorted(cdf, u, side="right").
+template <int NB>
+__device__ __forceinline__ uint32_t exact_pick(const double (&cdf)[NB + 1], double last, const bool (&v)[NB + 1],
+                                               const int (&cell)[NB + 1], double u) {
+    const double inv = 1.0 / last;
+    uint32_t target = (uint32_t)cell[NB];
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        if (v[k] && !found && cdf_gt(cdf[k], last, inv, u)) {
+            found = true;
+            target = (uint32_t)cell[k];
+        }
+    }
+    return target;  // the stay slot has cdf == 1 > u
+}
+
+// Fast path of the choice.  Probabilities from the hardware exp2 (v_exp_f32)
+// and a float32 running sum differ from NumPy's exact pipeline (np.exp f32,
+// pairwise sum, f32 divide, f64 cumsum and normalisation) by less than 1e-5
+// of the total for every argument that matters (|x| < 30; terms below e^-30
+// are < 1e-13 of the total).  A slot is returned only when u is at least
+// kFastMargin = 1e-4 (10x that bound) away from every cdf boundary it is
+// compared with, so the answer equals the exact one; otherwise -1 and the
+// caller runs the exact emulation.
+#ifndef FFM_FAST_MARGIN
+#define FFM_FAST_MARGIN 1e-4f
+#endif
+constexpr float kFastMargin = FFM_FAST_MARGIN;
+
+template <int NB>
+__device__ __forceinline__ int fast_choice(const float (&x)[NB + 1], const bool (&v)[NB + 1], double u) {
+    float cum[NB + 1];
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        acc += v[k] ? __builtin_amdgcn_exp2f(x[k] * 1.44269504088896341f) : 0.0f;
+        cum[k] = acc;
+    }
+    const float t = (float)u * acc;
+    const float d = kFastMargin * acc;
+    int slot = -1;
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        if (v[k] && !done) {
+            if (cum[k] > t + d) {
+                slot = k;
+                done = true;
+            } else if (cum[k] >= t - d) {
+                done = true;   // too close to call: exact path
+            }
+        }
+    }
+    return slot;
+}
+
 // decide() for one agent at padded cell pp: model/ffm_core.py:41-88.
 // Returns the padded target cell, kNoReq, or kPending (draw needed, MT pass 1).
 template <int NB, bool F64, class GT, class Draw>
@@ -103,10 +161,8 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
     v[NB] = true;
     const int nc = nvalid + 1;
 
-    double cdf[NB + 1];
-    double last;
     if (!F64) {
-        float sc[NB + 1], e[NB + 1];
+        float sc[NB + 1];
         float mx = -__builtin_inff();
 #pragma unroll
         for (int k = 0; k <= NB; k++) {
@@ -116,16 +172,32 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
             sc[k] = a + b;                                           // :77
             mx = sc[k] > mx ? sc[k] : mx;                            // :78
         }
+        float xs[NB + 1];
 #pragma unroll
-        for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(sc[k] - mx) : 0.0f;   // :80
-        const float sum = np_sum<NB, float>(e, v, nc);                             // :81
+        for (int k = 0; k <= NB; k++) xs[k] = sc[k] - mx;            // :80 argument, exact
+        const double u = draw.get();                                 // :84
+        if (u < 0.0) return kPending;
+        const int fs = fast_choice<NB>(xs, v, u);
+        if (fs >= 0) {
+            uint32_t target = (uint32_t)cell[NB];
+#pragma unroll
+            for (int k = 0; k < NB; k++)
+                if (k == fs) target = (uint32_t)cell[k];
+            return target;
+        }
+        // u is within the margin of a boundary: the exact NumPy arithmetic decides.
+        float e[NB + 1];
+#pragma unroll
+        for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;                // :80
+        const float sum = np_sum<NB, float>(e, v, nc);                                    // :81
+        double cdf[NB + 1];
         double acc = 0.0;
 #pragma unroll
         for (int k = 0; k <= NB; k++) {
             if (v[k]) acc += (double)(e[k] / sum);                   // :83, then cumsum in choice
             cdf[k] = acc;
         }
-        last = acc;
+        return exact_pick<NB>(cdf, acc, v, cell, u);
     } else {
         double sc[NB + 1], e[NB + 1];
         double mx = -__builtin_inf();
@@ -139,28 +211,17 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
 #pragma unroll
         for (int k = 0; k <= NB; k++) e[k] = v[k] ? exp(sc[k] - mx) : 0.0;
         const double sum = np_sum<NB, double>(e, v, nc);
+        double cdf[NB + 1];
         double acc = 0.0;
 #pragma unroll
         for (int k = 0; k <= NB; k++) {
             if (v[k]) acc += e[k] / sum;
             cdf[k] = acc;
         }
-        last = acc;
+        const double u = draw.get();                                 // :84
+        if (u < 0.0) return kPending;
+        return exact_pick<NB>(cdf, acc, v, cell, u);
     }
-    const double u = draw.get();                                     // :84
-    if (u < 0.0) return kPending;
-    // np.random.choice: cdf /= cdf[-1]; idx = searchsorted(cdf, u, side="right")
-    const double inv = 1.0 / last;
-    uint32_t target = (uint32_t)cell[NB];
-    bool found = false;
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-        if (v[k] && !found && cdf_gt(cdf[k], last, inv, u)) {
-            found = true;
-            target = (uint32_t)cell[k];
-        }
-    }
-    return target;  // the stay slot has cdf == 1 > u
 }
 
 // The requesters of target r (padded): agents adjacent to r whose request is r.

@@ -39,6 +39,31 @@
 #include "core_common.h"
 #include "kernels.h"
 
+#ifndef FFM_STAMPS
+#define FFM_STAMPS 0   // diagnostic builds only: per-phase s_memtime cycle sums per wave
+#endif
+#if FFM_STAMPS
+#define STAMP(k)                                                                           \
+    do {                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        unsigned long long t_;                                                             \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        st[k] += t_ - tlast;                                                               \
+        tlast = t_;                                                                        \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+#ifndef FFM_ABLATE
+#define FFM_ABLATE 0   // diagnostic builds only (tools/ablate.sh): bit k skips one phase
+#endif
+#ifndef FFM_LDS_PAD
+#define FFM_LDS_PAD 0  // diagnostic builds only: extra dynamic LDS per block to pin occupancy
+#endif
+
 namespace ffm {
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -47,7 +72,7 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 // Wave kernel: EW envs per wave, AL = 64 / EW agent lanes per env.
 // ===========================================================================
 struct WaveCarve {
-    size_t grid, dff, req, nxt, u, flag, keys, per_wave;
+    size_t grid, dff, req, nxt, u, flag, keys, spos, per_wave;
 };
 
 __host__ __device__ inline WaveCarve wave_carve(int PHW, int AL, int EW, int F, bool mt, bool reset) {
@@ -60,6 +85,7 @@ __host__ __device__ inline WaveCarve wave_carve(int PHW, int AL, int EW, int F, 
     c.u = o;    o += mt ? align16((size_t)EW * AL * 8) : 0;
     c.flag = o; o += mt ? align16((size_t)EW * AL * 2) : 0;
     c.keys = o; o += reset ? align16((size_t)F * 8) : 0;
+    c.spos = o; o += align16(64 * 2 + 2 * 4);
     c.per_wave = o;
     return c;
 }
@@ -109,6 +135,16 @@ __device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned lo
     wave_sync();
 }
 
+// One env group's HBM state in registers (software pipelining: the next
+// group's loads are issued at the top of a group and staged into LDS at its
+// bottom, so no register is carried across the loop back edge -- the
+// compiler would otherwise wait for the loads at the loop head).
+struct WavePrefetch {
+    float4 d0, d1;
+    int pos;
+    int cnt;
+};
+
 template <int NB, bool MT, int EW, int HT, int WT>
 __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -117,74 +153,143 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
     const int H = HT ? HT : a.H, W = WT ? WT : a.W;
     const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
     const int A = a.A;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int sub = lane / AL, al = lane - sub * AL;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform (SGPR)
+    const int sub = EW == 2 ? (lane >> 5) : 0;
+    const int al = lane - sub * AL;
     const bool do_reset = !MT && a.auto_reset;
 
+    // ---- LDS carve-up: uniform bases, per-lane views ------------------------------
+    const WaveCarve cv = wave_carve(PHW, AL, EW, a.F, MT, do_reset);
     uint8_t* pmap = smem;
     float* psff = reinterpret_cast<float*>(smem + align16((size_t)PHW));
-    const WaveCarve cv = wave_carve(PHW, AL, EW, a.F, MT, do_reset);
     unsigned char* wbase = smem + wave_shared_bytes(PHW) + (size_t)wv * cv.per_wave;
     GT* grid = reinterpret_cast<GT*>(wbase + cv.grid);
     float* tile = reinterpret_cast<float*>(wbase + cv.dff);
     uint16_t* sreq = reinterpret_cast<uint16_t*>(wbase + cv.req);
     uint16_t* snxt = reinterpret_cast<uint16_t*>(wbase + cv.nxt);
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
+    uint16_t* spos = reinterpret_cast<uint16_t*>(wbase + cv.spos);
+    int* scnt = reinterpret_cast<int*>(wbase + cv.spos + 128);
+    GT* gk = grid + sub * PHW;
+    float* dk = tile + sub * PHW;
+    uint16_t* rq = sreq + sub * AL;
+    uint16_t* nx = snxt + sub * AL;
 
-    // Block-shared padded map and SFF (host-prepared padded copies).
-    for (int i = threadIdx.x; i < PHW; i += 256) {
-        pmap[i] = a.pmap[i];
-        psff[i] = reinterpret_cast<const float*>(a.psff)[i];
+    // This lane's two float4 DFF slots (cells 4q..4q+3 of the group, q = lane,
+    // lane + 64): padded tile offsets, fixed for every group.  W % 4 == 0, so a
+    // slot never straddles a row (checked on the host).
+    int tb0 = -1, tb1 = -1;
+    {
+        const int c0 = 4 * lane, c1 = 4 * (lane + 64);
+        if (c0 < EW * HW) {
+            const int s = c0 / HW, cell = c0 - s * HW, x = cell / W, y = cell - (cell / W) * W;
+            tb0 = s * PHW + (x + 1) * PW + y + 1;
+        }
+        if (c1 < EW * HW) {
+            const int s = c1 / HW, cell = c1 - s * HW, x = cell / W, y = cell - (cell / W) * W;
+            tb1 = s * PHW + (x + 1) * PW + y + 1;
+        }
     }
-    // Zero this wave's DFF tiles once: the halo stays zero for every env it handles.
-    for (int i = lane; i < EW * PHW; i += 64) tile[i] = 0.0f;
-    __syncthreads();
 
-    const long long ngroups = (a.E + EW - 1) / EW;
-    const long long wstride = (long long)gridDim.x * 4;
-    unsigned long long acc_steps = 0, acc_exits = 0, acc_resets = 0;
+    const int ngroups = (int)((a.E + EW - 1) / EW);
+    const int wstride = (int)gridDim.x * 4;
+    int g = (int)blockIdx.x * 4 + wv;   // wave-uniform
 
-    for (long long g = (long long)blockIdx.x * 4 + wv; g < ngroups; g += wstride) {
-        const long long e = g * EW + sub;
-        const bool env_ok = e < a.E;
-        const uint32_t genv = (uint32_t)(a.env_base + e);
-        float* dk = tile + sub * PHW;
-        GT* gk = grid + sub * PHW;
-        uint16_t* rq = sreq + sub * AL;
-        uint16_t* nx = snxt + sub * AL;
+    auto prefetch = [&](int gg, WavePrefetch& pf) {
+        pf.d0 = pf.d1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        pf.pos = 0;
+        pf.cnt = 0;
+        if (gg < 0) return;
+        const long long e0 = (long long)gg * EW;
+        const int nenv = (int)((a.E - e0) < EW ? (a.E - e0) : EW);
+        const int* cp = a.cnt + e0;
+        const uint16_t* pp = a.pos + e0 * A;
+        const float4* dp = reinterpret_cast<const float4*>(a.dff + e0 * HW);
+        const int n4 = nenv * HW / 4;
+        if (sub < nenv) pf.cnt = cp[sub];
+        if (sub < nenv && al < A) pf.pos = pp[sub * A + al];
+        if (lane < n4) pf.d0 = dp[lane];
+        if (lane + 64 < n4) pf.d1 = dp[lane + 64];
+    };
+    auto stage = [&](const WavePrefetch& pf0) {
+        WavePrefetch pf = pf0;
+        if (FFM_ABLATE & 512) {   // diagnostic: fixed synthetic state (agents on row 5/6)
+            pf.d0 = pf.d1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            pf.cnt = a.N;
+            pf.pos = (5 + (al >= 10) + (al >= 20)) * W + 1 + (al % 10);
+            if (FFM_ABLATE & 1024) asm volatile("" ::"v"(pf0.d0.x), "v"(pf0.d1.x), "v"(pf0.pos), "v"(pf0.cnt));
+        }
+        if (tb0 >= 0) {
+            float* p = tile + tb0;
+            p[0] = pf.d0.x; p[1] = pf.d0.y; p[2] = pf.d0.z; p[3] = pf.d0.w;
+        }
+        if (tb1 >= 0) {
+            float* p = tile + tb1;
+            p[0] = pf.d1.x; p[1] = pf.d1.y; p[2] = pf.d1.z; p[3] = pf.d1.w;
+        }
+        spos[lane] = (uint16_t)pf.pos;
+        if (al == 0) scnt[sub] = pf.cnt;
+    };
 
-        // ---- HBM -> registers/LDS: count, positions, DFF -------------------
-        int cnt = env_ok ? a.cnt[e] : 0;
-        const bool rs = do_reset && env_ok && cnt == 0;
+    {
+        WavePrefetch pf0;
+        prefetch(g < ngroups ? g : -1, pf0);
+        // Block-shared padded map and SFF; this wave's grids (map codes; agents are
+        // marked per step and unmarked after it) and zero-halo DFF tiles.
+        for (int i = threadIdx.x; i < PHW; i += 256) {
+            pmap[i] = a.pmap[i];
+            psff[i] = reinterpret_cast<const float*>(a.psff)[i];
+        }
+        for (int i = lane; i < EW * PHW; i += 64) tile[i] = 0.0f;
+        __syncthreads();
+        for (int i = lane; i < EW * PHW; i += 64) grid[i] = pmap[i - (i / PHW) * PHW];
+        wave_sync();
+        stage(pf0);
+        wave_sync();
+    }
+
+    int c_steps = 0, c_exits = 0, c_resets = 0;   // per lane; only al == 0 lanes count
+#if FFM_STAMPS
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+
+    for (; g < ngroups; g += wstride) {
+        WavePrefetch nxtpf;
+        prefetch(((FFM_ABLATE & 8) || ((FFM_ABLATE & 512) && !(FFM_ABLATE & 1024))) ? -1
+                                                                              : (g + wstride < ngroups ? g + wstride : -1),
+                 nxtpf);
+
+        const long long e0 = (long long)g * EW;
+        const int nenv = (int)((a.E - e0) < EW ? (a.E - e0) : EW);
+        const bool env_ok = sub < nenv;
+        const uint32_t genv = (uint32_t)(a.env_base + e0 + sub);
+
+        int cnt = scnt[sub];
+        const bool rs = do_reset && env_ok && cnt == 0 && !(FFM_ABLATE & 32);
         int pp = -1;
         if (env_ok && al < A && al < cnt) {
-            const int c = a.pos[e * A + al];
+            const int c = spos[lane];
             const int x = c / W, y = c - (c / W) * W;
             pp = (x + 1) * PW + y + 1;
         }
-        const long long cbase = g * EW * (long long)HW;
-        const long long clim = (a.E - g * EW) * (long long)HW;
-        const int ncell = (int)(clim < (long long)EW * HW ? clim : (long long)EW * HW);
-        for (int c = lane; c < ncell; c += 64) {
-            const int s = c / HW, cell = c - s * HW;
-            const int x = cell / W, y = cell - (cell / W) * W;
-            tile[s * PHW + (x + 1) * PW + y + 1] = a.dff[cbase + c];
-        }
-        // grid <- map codes
-        for (int i = lane; i < EW * PHW; i += 64) {
-            const int s = i / PHW;
-            grid[i] = pmap[i - s * PHW];
-        }
-        wave_sync();
 
         // ---- on-device auto-reset (Philox placement) ------------------------
         if (do_reset) {
 #pragma unroll
             for (int s = 0; s < EW; s++) {
-                const bool me = rs && sub == s;
-                if (__ballot(me) == 0ull) continue;
-                const uint32_t ge = (uint32_t)(a.env_base + g * EW + s);
-                wave_reset_env(a, ge, keys, snxt + s * AL, PW, W, lane);
+                if (__ballot(rs && sub == s) == 0ull) continue;
+                const uint32_t ge = (uint32_t)(a.env_base + e0 + s);
+                if (FFM_ABLATE & 64) {   // diagnostic: trivial placement (first N free cells)
+                    if (lane < a.N) {
+                        const int cell = a.free_list[lane];
+                        snxt[s * AL + lane] = (uint16_t)((cell / W + 1) * PW + cell % W + 1);
+                    }
+                    wave_sync();
+                } else {
+                    wave_reset_env(a, ge, keys, snxt + s * AL, PW, W, lane);
+                }
                 for (int i = lane; i < HW; i += 64) {   // zero the env's DFF interior
                     const int x = i / W, y = i - (i / W) * W;
                     tile[s * PHW + (x + 1) * PW + y + 1] = 0.0f;
@@ -197,21 +302,27 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
             }
             wave_sync();
         }
-        acc_steps += (al == 0 && env_ok) ? (unsigned long long)cnt : 0ull;
-        acc_resets += (al == 0 && rs) ? 1ull : 0ull;
+        c_steps += (al == 0 && env_ok) ? cnt : 0;
+        c_resets += (al == 0 && rs) ? 1 : 0;
         const bool live = pp >= 0;
+        STAMP(0);
 
         // ---- occupancy marks; default next = stay -----------------------------
         if (live) gk[pp] = (GT)(GridCodes<GT>::kAgent | (uint32_t)al);
         rq[al] = kNoReq;
         nx[al] = (uint16_t)(live ? pp : 0);
         wave_sync();
+        STAMP(1);
 
         // ---- decide (model/ffm_core.py:40-88) --------------------------------------
         uint32_t r = kNoReq;
-        if (live) {
+        if (live && !(FFM_ABLATE & 1)) {
             if (MT) {
                 r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, DrawPending{});
+            } else if (FFM_ABLATE & 256) {   // diagnostic: cheap hash instead of Philox
+                const uint32_t hsh = (genv * 2654435761u) ^ ((uint32_t)al * 40503u) ^ (a.t * 97u);
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64,
+                                          DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)});
             } else {
                 const DrawPhilox d{a.key0, a.key1, a.t, genv, (uint32_t)al};
                 r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, d);
@@ -221,7 +332,7 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
             double* su = reinterpret_cast<double*>(wbase + cv.u) + sub * AL;
             const unsigned long long pend = __ballot(r == kPending);
             if (al == 0 && env_ok) {
-                uint32_t* mt_np = a.mt_np + e * 625;
+                uint32_t* mt_np = a.mt_np + (e0 + sub) * 625;
                 unsigned long long mk = (pend >> (sub * AL)) & (AL == 64 ? ~0ull : ((1ull << AL) - 1ull));
                 while (mk) {
                     const int i = __builtin_ctzll(mk);
@@ -233,70 +344,78 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
             if (r == kPending)
                 r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]});
         }
+        STAMP(2);
         if (live) rq[al] = (uint16_t)r;
         wave_sync();
+        STAMP(3);
 
         // ---- resolve (model/ffm_core.py:90-98) ---------------------------------------
-        uint16_t who[NB];
-        bool is[NB];
-        const bool moving = live && r != kNoReq && (int)r != pp;
-        int m = 0, s0 = -1;
-        bool owner = false;
-        if (moving) {
-            m = requesters<NB, GT>((int)r, PW, gk, rq, who, is);
-            s0 = kth_slot<NB>(who, is, 0);
-            owner = s0 >= 0 && who[s0] == al;
-        }
-        if (MT) {
-            uint16_t* fl = reinterpret_cast<uint16_t*>(wbase + cv.flag) + sub * AL;
-            const int fr_m = (owner && m >= 2) ? m : 0;
-            fl[al] = (uint16_t)fr_m;
-            const unsigned long long cont = __ballot(fr_m >= 2);
-            wave_sync();
-            if (al == 0 && env_ok) {
-                uint32_t* mt_np = a.mt_np + e * 625;
-                uint32_t* mt_py = a.mt_py + e * 625;
-                unsigned long long mk = (cont >> (sub * AL)) & (AL == 64 ? ~0ull : ((1ull << AL) - 1ull));
-                while (mk) {
-                    const int i = __builtin_ctzll(mk);
-                    mk &= mk - 1ull;
-                    const double u = mt_u53(mt_np);                                    // np.random.rand()
-                    const int kk = u < 0.5 ? (int)mt_randbelow(mt_py, (uint32_t)fl[i]) : -1;  // random.choice
-                    fl[i] = (uint16_t)(kk >= 0 ? 0x100 | kk : 0x200);
-                }
+        {
+            uint16_t who[NB];
+            bool is[NB];
+            const bool moving = live && r != kNoReq && (int)r != pp;
+            int m = 0, s0 = -1;
+            bool owner = false;
+            if (moving) {
+                m = requesters<NB, GT>((int)r, PW, gk, rq, who, is);
+                s0 = kth_slot<NB>(who, is, 0);
+                owner = s0 >= 0 && who[s0] == al;
             }
-            wave_sync();
-        }
-        if (live && r != kNoReq) {
-            if ((int)r == pp) {
-                dk[pp] += 1.0f;                                                        // :91-93 (stay)
-            } else if (owner) {
-                int ws = -1;
-                if (m == 1) {
-                    ws = s0;
-                } else if (MT) {
-                    const int f = (reinterpret_cast<uint16_t*>(wbase + cv.flag) + sub * AL)[al];
-                    if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
-                } else {
-                    PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)al, kPurFriction);
-                    const double u = ps.next_u53();                                     // :95
-                    if (u < 0.5) ws = kth_slot<NB>(who, is, (int)ps.randbelow((uint32_t)m));   // :96
+            if (MT) {
+                uint16_t* fl = reinterpret_cast<uint16_t*>(wbase + cv.flag) + sub * AL;
+                const int fr_m = (owner && m >= 2) ? m : 0;
+                fl[al] = (uint16_t)fr_m;
+                const unsigned long long cont = __ballot(fr_m >= 2);
+                wave_sync();
+                if (al == 0 && env_ok) {
+                    uint32_t* mt_np = a.mt_np + (e0 + sub) * 625;
+                    uint32_t* mt_py = a.mt_py + (e0 + sub) * 625;
+                    unsigned long long mk = (cont >> (sub * AL)) & (AL == 64 ? ~0ull : ((1ull << AL) - 1ull));
+                    while (mk) {
+                        const int i = __builtin_ctzll(mk);
+                        mk &= mk - 1ull;
+                        const double u = mt_u53(mt_np);                                   // np.random.rand()
+                        const int kk = u < 0.5 ? (int)mt_randbelow(mt_py, (uint32_t)fl[i]) : -1;   // random.choice
+                        fl[i] = (uint16_t)(kk >= 0 ? 0x100 | kk : 0x200);
+                    }
                 }
-                if (ws >= 0) {
-                    int wcell = (int)r;
-                    uint16_t wi = 0;
+                wave_sync();
+            }
+            if (live && r != kNoReq && !(FFM_ABLATE & 2)) {
+                if ((int)r == pp) {
+                    dk[pp] += 1.0f;                                                       // :91-93 (stay)
+                } else if (owner) {
+                    int ws = -1;
+                    if (m == 1) {
+                        ws = s0;
+                    } else if (MT) {
+                        const int f = (reinterpret_cast<uint16_t*>(wbase + cv.flag) + sub * AL)[al];
+                        if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
+                    } else if (FFM_ABLATE & 128) {   // diagnostic: cheap hash instead of Philox
+                        const uint32_t hsh = (genv * 2654435761u) ^ ((uint32_t)al * 40503u) ^ a.t;
+                        if (hsh & 1) ws = kth_slot<NB>(who, is, (int)((hsh >> 8) % (uint32_t)m));
+                    } else {
+                        PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)al, kPurFriction);
+                        const double u = ps.next_u53();                                    // :95
+                        if (u < 0.5) ws = kth_slot<NB>(who, is, (int)ps.randbelow((uint32_t)m));   // :96
+                    }
+                    if (ws >= 0) {
+                        int wcell = (int)r;
+                        uint16_t wi = 0;
 #pragma unroll
-                    for (int s = 0; s < NB; s++)
-                        if (s == ws) {
-                            wcell = (int)r - nb_dx<NB>(s) * PW - nb_dy<NB>(s);
-                            wi = who[s];
-                        }
-                    nx[wi] = (uint16_t)r;
-                    dk[wcell] += 1.0f;                                                 // :97-98
+                        for (int s = 0; s < NB; s++)
+                            if (s == ws) {
+                                wcell = (int)r - nb_dx<NB>(s) * PW - nb_dy<NB>(s);
+                                wi = who[s];
+                            }
+                        nx[wi] = (uint16_t)r;
+                        dk[wcell] += 1.0f;                                                // :97-98
+                    }
                 }
             }
         }
         wave_sync();
+        STAMP(4);
 
         // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) ---------
         const int nxt = live ? (int)nx[al] : 0;
@@ -305,48 +424,92 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
         const unsigned long long segm = AL == 64 ? ~0ull : (((1ull << AL) - 1ull) << (sub * AL));
         const int newidx = __popcll(km & segm & ((1ull << lane) - 1ull));
         const int newcnt = __popcll(km & segm);
-        if (keep) a.pos[e * A + newidx] = (uint16_t)unpad(nxt, PW);
-        if (al == 0 && env_ok) {
-            a.cnt[e] = newcnt;
-            if (rs && a.episodes) a.episodes[e] += 1;
-        }
-        acc_exits += (al == 0 && env_ok) ? (unsigned long long)(cnt - newcnt) : 0ull;
+        c_exits += (al == 0 && env_ok) ? cnt - newcnt : 0;
+        if (live) gk[pp] = 0;   // unmark: agents only ever stand on free cells
+        STAMP(5);
 
-        // ---- update_dff (model/ffm_core.py:106-117) ---------------------------------
-        for (int c = lane; c < EW * HW; c += 64) {          // pass 1: B = c0 * D (halo stays 0)
-            const int s = c / HW, cell = c - s * HW;
-            const int x = cell / W, y = cell - (cell / W) * W;
-            float* p = tile + s * PHW + (x + 1) * PW + y + 1;
-            *p = a.c0 * *p;                                                     // :109
-        }
-        wave_sync();
-        for (int c = lane; c < ncell; c += 64) {
-            const int s = c / HW, cell = c - s * HW;
-            const int x = cell / W, y = cell - (cell / W) * W;
-            const float* p = tile + s * PHW + (x + 1) * PW + y + 1;
-            float acc = *p;
+        // ---- update_dff (model/ffm_core.py:106-117), float4 per lane ------------------
+        float b0[4], b1[4];
+        if (tb0 >= 0) {                          // pass 1: B = c0 * D in place (halo stays 0)
+            float* p = tile + tb0;
 #pragma unroll
-            for (int q = 0; q < NB; q++) {
-                const float t = a.c1 * p[nb_dx<NB>(q) * PW + nb_dy<NB>(q)];      // :113
-                acc = acc + t;
-            }
-            a.dff[cbase + c] = acc < 1e-4f ? 0.0f : acc;                        // :116-117
+            for (int j = 0; j < 4; j++) { b0[j] = a.c0 * p[j]; p[j] = b0[j]; }        // :109
+        }
+        if (tb1 >= 0) {
+            float* p = tile + tb1;
+#pragma unroll
+            for (int j = 0; j < 4; j++) { b1[j] = a.c0 * p[j]; p[j] = b1[j]; }
         }
         wave_sync();
+        float o0[4], o1[4];
+        if (tb0 >= 0) {
+            const float* p = tile + tb0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float acc = b0[j];
+#pragma unroll
+                for (int k = 0; k < NB; k++) {
+                    if (FFM_ABLATE & 4) break;
+                    const float t = a.c1 * p[j + nb_dx<NB>(k) * PW + nb_dy<NB>(k)];      // :113
+                    acc = acc + t;
+                }
+                o0[j] = acc < 1e-4f ? 0.0f : acc;                                        // :116-117
+            }
+        }
+        if (tb1 >= 0) {
+            const float* p = tile + tb1;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float acc = b1[j];
+#pragma unroll
+                for (int k = 0; k < NB; k++) {
+                    if (FFM_ABLATE & 4) break;
+                    const float t = a.c1 * p[j + nb_dx<NB>(k) * PW + nb_dy<NB>(k)];
+                    acc = acc + t;
+                }
+                o1[j] = acc < 1e-4f ? 0.0f : acc;
+            }
+        }
+        wave_sync();
+        STAMP(6);
+
+        // ---- stage the next group (its loads were issued at the top), then store ------
+        stage(nxtpf);
+        if (!(FFM_ABLATE & 16)) {
+            uint16_t* gp = a.pos + e0 * A;
+            int* gc = a.cnt + e0;
+            float4* gd = reinterpret_cast<float4*>(a.dff + e0 * HW);
+            const int n4 = nenv * HW / 4;
+            if (keep) gp[sub * A + newidx] = (uint16_t)unpad(nxt, PW);
+            if (al == 0 && env_ok) {
+                gc[sub] = newcnt;
+                if (rs && a.episodes) a.episodes[e0 + sub] += 1;
+            }
+            if (tb0 >= 0 && lane < n4) gd[lane] = make_float4(o0[0], o0[1], o0[2], o0[3]);
+            if (tb1 >= 0 && lane + 64 < n4) gd[lane + 64] = make_float4(o1[0], o1[1], o1[2], o1[3]);
+        }
+        wave_sync();
+        STAMP(7);
     }
 
     // ---- counters: one atomic per wave ------------------------------------------------
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        acc_steps += __shfl_xor(acc_steps, off);
-        acc_exits += __shfl_xor(acc_exits, off);
-        acc_resets += __shfl_xor(acc_resets, off);
+        c_steps += __shfl_xor(c_steps, off);
+        c_exits += __shfl_xor(c_exits, off);
+        c_resets += __shfl_xor(c_resets, off);
     }
     if (lane == 0) {
-        if (acc_steps) atomicAdd(&a.counters[0], acc_steps);
-        if (acc_exits) atomicAdd(&a.counters[1], acc_exits);
-        if (acc_resets) atomicAdd(&a.counters[2], acc_resets);
+        if (c_steps) atomicAdd(&a.counters[0], (unsigned long long)c_steps);
+        if (c_exits) atomicAdd(&a.counters[1], (unsigned long long)c_exits);
+        if (c_resets) atomicAdd(&a.counters[2], (unsigned long long)c_resets);
         if (blockIdx.x == 0 && wv == 0) atomicAdd(&a.counters[3], 1ull);
+#if FFM_STAMPS
+        if (a.dbg) {
+            for (int k = 0; k < 8; k++) atomicAdd(&a.dbg[k], st[k]);
+            atomicAdd(&a.dbg[8], 1ull);
+        }
+#endif
     }
 }
 
@@ -721,14 +884,14 @@ __global__ void np_expf_kernel(const float* __restrict__ x, float* __restrict__ 
 // ===========================================================================
 template <int NB, bool MT, int EW, int HT, int WT>
 static hipError_t launch_wave_t(const CoreStepArgs& a, int blocks, hipStream_t s) {
-    const size_t smem = core_wave_smem_bytes(a.H, a.W, a.A, a.F, MT, !MT && a.auto_reset, 4);
+    const size_t smem = core_wave_smem_bytes(a.H, a.W, a.A, a.F, MT, !MT && a.auto_reset, 4) + FFM_LDS_PAD;
     core_wave_kernel<NB, MT, EW, HT, WT><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
     return hipGetLastError();
 }
 
 template <int NB, bool MT, int EW, int HT, int WT>
 static int occ_wave_t(const CoreStepArgs& a) {
-    const size_t smem = core_wave_smem_bytes(a.H, a.W, a.A, a.F, MT, !MT && a.auto_reset, 4);
+    const size_t smem = core_wave_smem_bytes(a.H, a.W, a.A, a.F, MT, !MT && a.auto_reset, 4) + FFM_LDS_PAD;
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, core_wave_kernel<NB, MT, EW, HT, WT>, 256, smem) != hipSuccess)
         return 0;

@@ -56,6 +56,7 @@ struct ffm_engine {
     unsigned long long* d_ctr = nullptr;
     uint32_t* d_mt_np = nullptr;
     uint32_t* d_mt_py = nullptr;
+    unsigned long long* d_dbg = nullptr;   // diagnostic counters (FFM_STAMPS builds)
 };
 
 extern "C" {
@@ -76,6 +77,7 @@ static void release(ffm_engine* e) {
     (void)hipFree(e->d_ctr);
     (void)hipFree(e->d_mt_np);
     (void)hipFree(e->d_mt_py);
+    (void)hipFree(e->d_dbg);
     delete e;
 }
 
@@ -137,7 +139,8 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     // it): K envs per workgroup, LDS-bounded.
     const int A = d.agent_capacity;
     const bool reset_lds = !e->mt && d.auto_reset;
-    e->wave = d.envs_per_block <= 0 && A <= 64 && !e->f64 &&
+    const int EW = A <= 32 ? 2 : 1;
+    e->wave = d.envs_per_block <= 0 && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
               ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
     int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);
@@ -175,6 +178,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_dff, E * HW * 4);
     ALLOC(e->d_eps, E * 4);
     ALLOC(e->d_ctr, 4 * 8);
+    ALLOC(e->d_dbg, 16 * 8);
     if (e->mt) {
         ALLOC(e->d_mt_np, E * 625 * 4);
         ALLOC(e->d_mt_py, E * 625 * 4);
@@ -190,6 +194,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     if (he == hipSuccess) he = hipMemset(e->d_dff, 0, E * HW * 4);
     if (he == hipSuccess) he = hipMemset(e->d_eps, 0, E * 4);
     if (he == hipSuccess) he = hipMemset(e->d_ctr, 0, 32);
+    if (he == hipSuccess) he = hipMemset(e->d_dbg, 0, 128);
     if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_np, 0, E * 625 * 4);
     if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_py, 0, E * 625 * 4);
     if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("init: ") + hipGetErrorString(he)));
@@ -245,6 +250,7 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
     a.F = e->F;
     a.mt_np = e->d_mt_np;
     a.mt_py = e->d_mt_py;
+    a.dbg = e->d_dbg;
     return a;
 }
 
@@ -409,6 +415,13 @@ int ffm_engine_get_step_index(ffm_engine* e, uint32_t* t) {
 int ffm_engine_set_step_index(ffm_engine* e, uint32_t t) {
     if (!e) return fail(FFM_E_INVALID, "null engine");
     e->t = t;
+    return FFM_OK;
+}
+
+// Diagnostic (not part of the ABI header): read the FFM_STAMPS counters.
+int ffm_debug_read(ffm_engine* e, uint64_t* out, int n) {
+    if (!e || !out || n < 0 || n > 16) return fail(FFM_E_INVALID, "bad args");
+    HIP_TRY(hipMemcpy(out, e->d_dbg, (size_t)n * 8, hipMemcpyDeviceToHost));
     return FFM_OK;
 }
 

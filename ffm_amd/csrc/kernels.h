@@ -29,6 +29,7 @@ struct CoreStepArgs {
     int F;
     uint32_t* mt_np;       // [E][625] MT mode
     uint32_t* mt_py;       // [E][625]
+    unsigned long long* dbg;  // diagnostic builds: [16] per-phase cycle sums (else unused)
 };
 
 size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves);

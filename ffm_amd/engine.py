@@ -14,7 +14,7 @@ import random as _pyrandom
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libffm_amd.so")
+LIB_PATH = os.environ.get("FFM_LIB_PATH") or os.path.join(_HERE, "_lib", "libffm_amd.so")
 
 ABI_VERSION = 1
 OK, E_INVALID, E_HIP, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -4
