@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libffm_amd.so")
 SOURCES = ["core_step.hip", "engine.cpp"]
-HEADERS = ["device_common.h", "kernels.h", os.path.join("..", "..", "include", "ffm_amd.h")]
+HEADERS = ["device_common.h", "core_common.h", "kernels.h", os.path.join("..", "..", "include", "ffm_amd.h")]
 ARCH = os.environ.get("FFM_OFFLOAD_ARCH", "gfx950")
 FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -29,9 +29,9 @@ def _stale() -> bool:
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    deps = SOURCES + HEADERS + [os.path.basename(__file__)]
-    return any(os.path.getmtime(os.path.join(CSRC, s) if not s.endswith("build.py") else __file__) > t
-               for s in deps)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps.append(os.path.abspath(__file__))
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:

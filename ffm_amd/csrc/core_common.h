@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t exact_pick(const double (&cdf)[NB + 1], doub
 // are < 1e-13 of the total).  A slot is returned only when u is at least
 // kFastMargin = 1e-4 (10x that bound) away from every cdf boundary it is
 // compared with, so the answer equals the exact one; otherwise -1 and the
-// caller runs the exact emulation.
+// caller runs the exact emulation.  Branch-free (selects only).
 #ifndef FFM_FAST_MARGIN
 #define FFM_FAST_MARGIN 1e-4f
 #endif
@@ -114,7 +114,8 @@ __device__ __forceinline__ int fast_choice(const float (&x)[NB + 1], const bool 
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k <= NB; k++) {
-        acc += v[k] ? __builtin_amdgcn_exp2f(x[k] * 1.44269504088896341f) : 0.0f;
+        const float e = __builtin_amdgcn_exp2f(x[k] * 1.44269504088896341f);
+        acc += v[k] ? e : 0.0f;
         cum[k] = acc;
     }
     const float t = (float)u * acc;
@@ -123,68 +124,66 @@ __device__ __forceinline__ int fast_choice(const float (&x)[NB + 1], const bool 
     bool done = false;
 #pragma unroll
     for (int k = 0; k <= NB; k++) {
-        if (v[k] && !done) {
-            if (cum[k] > t + d) {
-                slot = k;
-                done = true;
-            } else if (cum[k] >= t - d) {
-                done = true;   // too close to call: exact path
-            }
-        }
+        const bool gt = v[k] && !done && cum[k] > t + d;
+        const bool close = v[k] && !done && !gt && cum[k] >= t - d;
+        slot = gt ? k : slot;
+        done = done || gt || close;
     }
     return slot;
 }
 
 // decide() for one agent at padded cell pp: model/ffm_core.py:41-88.
 // Returns the padded target cell, kNoReq, or kPending (draw needed, MT pass 1).
+// Every slot is evaluated unconditionally (all neighbour cells exist in the
+// padded grid), so the LDS loads issue together and no lane diverges except
+// into the rare exact path.
 template <int NB, bool F64, class GT, class Draw>
 __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const float* sff32,
                                            const double* sff64, const float* dff, float kS32, float kD32,
                                            double kS64, const Draw& draw) {
     int cell[NB + 1];
     bool v[NB + 1];
+    uint32_t g[NB];
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
+        g[s] = grid[cell[s]];
+    }
+    cell[NB] = pp;                                                   // :64 stay, last
+    v[NB] = true;
     int nvalid = 0;
     int exit_cell = -1;
 #pragma unroll
-    for (int s = 0; s < NB; s++) {
-        const int c = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
-        cell[s] = c;
-        const uint32_t g = grid[c];
-        const bool ok = g == 0u || g == 3u;                          // :52-60
-        v[s] = ok;
-        nvalid += ok ? 1 : 0;
-        if (g == 3u && exit_cell < 0) exit_cell = c;                 // :66-72 first exit
+    for (int s = NB - 1; s >= 0; s--) {
+        v[s] = g[s] == 0u || g[s] == 3u;                             // :52-60
+        nvalid += v[s] ? 1 : 0;
+        exit_cell = g[s] == 3u ? cell[s] : exit_cell;                // :66-72 first exit
     }
-    if (nvalid == 0) return kNoReq;                                  // :63
-    if (exit_cell >= 0) return (uint32_t)exit_cell;
-    cell[NB] = pp;                                                   // :64 stay, last
-    v[NB] = true;
     const int nc = nvalid + 1;
 
     if (!F64) {
         float sc[NB + 1];
-        float mx = -__builtin_inff();
 #pragma unroll
         for (int k = 0; k <= NB; k++) {
-            if (!v[k]) { sc[k] = 0.0f; continue; }
             const float a = kS32 * sff32[cell[k]];
             const float b = kD32 * dff[cell[k]];
             sc[k] = a + b;                                           // :77
-            mx = sc[k] > mx ? sc[k] : mx;                            // :78
         }
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k <= NB; k++) mx = (v[k] && sc[k] > mx) ? sc[k] : mx;   // :78
         float xs[NB + 1];
 #pragma unroll
-        for (int k = 0; k <= NB; k++) xs[k] = sc[k] - mx;            // :80 argument, exact
+        for (int k = 0; k <= NB; k++) xs[k] = v[k] ? sc[k] - mx : -__builtin_inff();   // :80 argument, exact
         const double u = draw.get();                                 // :84
+        if (nvalid == 0) return kNoReq;                              // :63
+        if (exit_cell >= 0) return (uint32_t)exit_cell;
         if (u < 0.0) return kPending;
         const int fs = fast_choice<NB>(xs, v, u);
-        if (fs >= 0) {
-            uint32_t target = (uint32_t)cell[NB];
+        uint32_t target = (uint32_t)cell[NB];
 #pragma unroll
-            for (int k = 0; k < NB; k++)
-                if (k == fs) target = (uint32_t)cell[k];
-            return target;
-        }
+        for (int k = 0; k < NB; k++) target = k == fs ? (uint32_t)cell[k] : target;
+        if (fs >= 0) return target;
         // u is within the margin of a boundary: the exact NumPy arithmetic decides.
         float e[NB + 1];
 #pragma unroll
@@ -199,6 +198,8 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
         }
         return exact_pick<NB>(cdf, acc, v, cell, u);
     } else {
+        if (nvalid == 0) return kNoReq;
+        if (exit_cell >= 0) return (uint32_t)exit_cell;
         double sc[NB + 1], e[NB + 1];
         double mx = -__builtin_inf();
 #pragma unroll
@@ -229,16 +230,21 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
 template <int NB, class GT>
 __device__ __forceinline__ int requesters(int r, int PW, const GT* grid, const uint16_t* sreq,
                                           uint16_t (&who)[NB], bool (&is)[NB]) {
+    uint32_t g[NB];
+#pragma unroll
+    for (int s = 0; s < NB; s++) g[s] = grid[r - nb_dx<NB>(s) * PW - nb_dy<NB>(s)];
+    uint16_t q[NB];
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        const bool ag = (g[s] & GridCodes<GT>::kAgent) != 0u;
+        who[s] = ag ? (uint16_t)(g[s] & GridCodes<GT>::kIdx) : (uint16_t)0xFFFF;
+        q[s] = sreq[ag ? (g[s] & GridCodes<GT>::kIdx) : 0u];         // unconditional load
+    }
     int m = 0;
 #pragma unroll
     for (int s = 0; s < NB; s++) {
-        const uint32_t g = grid[r - nb_dx<NB>(s) * PW - nb_dy<NB>(s)];
-        const bool ag = (g & GridCodes<GT>::kAgent) != 0u;
-        const uint16_t j = ag ? (uint16_t)(g & GridCodes<GT>::kIdx) : (uint16_t)0xFFFF;
-        const bool ok = ag && sreq[j] == (uint16_t)r;
-        who[s] = j;
-        is[s] = ok;
-        m += ok ? 1 : 0;
+        is[s] = who[s] != 0xFFFF && q[s] == (uint16_t)r;
+        m += is[s] ? 1 : 0;
     }
     return m;
 }

@@ -249,6 +249,7 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
         wave_sync();
     }
 
+    if (FFM_ABLATE & 4096) return;   // diagnostic: prologue only
     int c_steps = 0, c_exits = 0, c_resets = 0;   // per lane; only al == 0 lanes count
 #if FFM_STAMPS
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -500,10 +501,13 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
         c_resets += __shfl_xor(c_resets, off);
     }
     if (lane == 0) {
-        if (c_steps) atomicAdd(&a.counters[0], (unsigned long long)c_steps);
-        if (c_exits) atomicAdd(&a.counters[1], (unsigned long long)c_exits);
-        if (c_resets) atomicAdd(&a.counters[2], (unsigned long long)c_resets);
-        if (blockIdx.x == 0 && wv == 0) atomicAdd(&a.counters[3], 1ull);
+        // Counters live in one 32-B slot per wave: no two waves ever add to the
+        // same address (a single contended word saturates near 100 adds/us).
+        unsigned long long* slot = a.counters + 4 * ((size_t)blockIdx.x * 4 + wv);
+        if (c_steps) atomicAdd(&slot[0], (unsigned long long)c_steps);
+        if (c_exits) atomicAdd(&slot[1], (unsigned long long)c_exits);
+        if (c_resets) atomicAdd(&slot[2], (unsigned long long)c_resets);
+        if (blockIdx.x == 0 && wv == 0) atomicAdd(&slot[3], 1ull);
 #if FFM_STAMPS
         if (a.dbg) {
             for (int k = 0; k < 8; k++) atomicAdd(&a.dbg[k], st[k]);
@@ -809,10 +813,11 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             exits += (unsigned long long)(scnt[k] - snew[k]);
             resets += (unsigned long long)sreset[k];
         }
-        atomicAdd(&a.counters[0], steps);
-        atomicAdd(&a.counters[1], exits);
-        if (resets) atomicAdd(&a.counters[2], resets);
-        if (blockIdx.x == 0) atomicAdd(&a.counters[3], 1ull);
+        unsigned long long* slot = a.counters + 4 * (size_t)blockIdx.x;   // one slot per block
+        atomicAdd(&slot[0], steps);
+        atomicAdd(&slot[1], exits);
+        if (resets) atomicAdd(&slot[2], resets);
+        if (blockIdx.x == 0) atomicAdd(&slot[3], 1ull);
     }
     if (tid < K) {
         a.cnt[e0 + tid] = snew[tid];

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -53,7 +54,8 @@ struct ffm_engine {
     float* d_dff = nullptr;
     float* d_tmp = nullptr;
     int32_t* d_eps = nullptr;
-    unsigned long long* d_ctr = nullptr;
+    unsigned long long* d_ctr = nullptr;   // [ctr_slots][4], summed on read
+    size_t ctr_slots = 1;
     uint32_t* d_mt_np = nullptr;
     uint32_t* d_mt_py = nullptr;
     unsigned long long* d_dbg = nullptr;   // diagnostic counters (FFM_STAMPS builds)
@@ -177,7 +179,14 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_cnt, E * 4);
     ALLOC(e->d_dff, E * HW * 4);
     ALLOC(e->d_eps, E * 4);
-    ALLOC(e->d_ctr, 4 * 8);
+    // One counter slot per wave (wave kernel) or block (block kernel): summed by
+    // ffm_engine_get_counters, never contended on the device.
+    {
+        const long long groups = (d.n_envs + EW - 1) / EW;
+        const long long blocks = (d.n_envs + K - 1) / K;
+        e->ctr_slots = (size_t)std::max<long long>(std::max<long long>(1, blocks), (groups + 3) / 4 * 4);
+    }
+    ALLOC(e->d_ctr, e->ctr_slots * 32);
     ALLOC(e->d_dbg, 16 * 8);
     if (e->mt) {
         ALLOC(e->d_mt_np, E * 625 * 4);
@@ -193,7 +202,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     if (he == hipSuccess) he = hipMemset(e->d_cnt, 0, E * 4);
     if (he == hipSuccess) he = hipMemset(e->d_dff, 0, E * HW * 4);
     if (he == hipSuccess) he = hipMemset(e->d_eps, 0, E * 4);
-    if (he == hipSuccess) he = hipMemset(e->d_ctr, 0, 32);
+    if (he == hipSuccess) he = hipMemset(e->d_ctr, 0, e->ctr_slots * 32);
     if (he == hipSuccess) he = hipMemset(e->d_dbg, 0, 128);
     if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_np, 0, E * 625 * 4);
     if (he == hipSuccess && e->mt) he = hipMemset(e->d_mt_py, 0, E * 625 * 4);
@@ -207,6 +216,10 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
         const int per_cu = std::max(1, ffm::core_wave_blocks_per_cu(a, d.neighborhood, e->mt));
         const long long groups = (d.n_envs + (A <= 32 ? 2 : 1) - 1) / (A <= 32 ? 2 : 1);
         e->wave_blocks = (int)std::min<long long>((groups + 3) / 4, (long long)cus * per_cu);
+        if (const char* ov = std::getenv("FFM_WAVE_BLOCKS")) {   // diagnostic override of the grid
+            const long long v = std::atoll(ov);
+            if (v > 0) e->wave_blocks = (int)std::min<long long>(v, (groups + 3) / 4);
+        }
     }
     *out = e;
     return FFM_OK;
@@ -387,10 +400,12 @@ int ffm_engine_get_mt_state(ffm_engine* e, int64_t env, uint32_t* np_key, int32_
 int ffm_engine_get_counters(ffm_engine* e, uint64_t* counters, void* stream) {
     if (!e || !counters) return fail(FFM_E_INVALID, "null argument");
     hipStream_t s = (hipStream_t)stream;
-    unsigned long long c[4];
-    HIP_TRY(hipMemcpyAsync(c, e->d_ctr, 32, hipMemcpyDeviceToHost, s));
+    std::vector<unsigned long long> c(e->ctr_slots * 4);
+    HIP_TRY(hipMemcpyAsync(c.data(), e->d_ctr, e->ctr_slots * 32, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    for (int i = 0; i < 4; i++) counters[i] = c[i];
+    for (int i = 0; i < 4; i++) counters[i] = 0;
+    for (size_t j = 0; j < e->ctr_slots; j++)
+        for (int i = 0; i < 4; i++) counters[i] += c[j * 4 + i];
     return FFM_OK;
 }
 
@@ -403,6 +418,7 @@ int ffm_engine_device_buffers(ffm_engine* e, ffm_device_buffers* out) {
     out->counters = reinterpret_cast<uint64_t*>(e->d_ctr);
     out->mt_np = e->d_mt_np;
     out->mt_py = e->d_mt_py;
+    out->counter_slots = (int64_t)e->ctr_slots;
     return FFM_OK;
 }
 

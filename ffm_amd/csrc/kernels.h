@@ -16,7 +16,7 @@ struct CoreStepArgs {
     int* cnt;              // [E]
     float* dff;            // [E][HW]
     int* episodes;         // [E] or nullptr
-    unsigned long long* counters;  // [4] agent_steps, exits, resets, steps
+    unsigned long long* counters;  // [slots][4] agent_steps, exits, resets, steps (one slot per wave/block)
     const uint8_t* pmap;   // [(H+2)*(W+2)] padded map codes: 0 free, 2 blocked, 3 exit
     const void* psff;      // [(H+2)*(W+2)] padded SFF, f32 or f64
     float kS32, kD32;      // f32(-k_S), f32(k_D)

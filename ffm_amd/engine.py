@@ -48,7 +48,7 @@ class DeviceBuffers(C.Structure):
     _fields_ = [
         ("positions", C.c_void_p), ("counts", C.c_void_p), ("dff", C.c_void_p),
         ("episodes", C.c_void_p), ("counters", C.c_void_p),
-        ("mt_np", C.c_void_p), ("mt_py", C.c_void_p),
+        ("mt_np", C.c_void_p), ("mt_py", C.c_void_p), ("counter_slots", C.c_int64),
     ]
 
 

@@ -87,9 +87,11 @@ typedef struct {
     int32_t* counts;          /* [E] */
     float* dff;               /* [E][H*W] */
     int32_t* episodes;        /* [E] completed resets */
-    uint64_t* counters;       /* [4]: agent_steps, exits, resets, steps */
+    uint64_t* counters;       /* [counter_slots][4]: agent_steps, exits, resets, steps;
+                                 one slot per wave/workgroup (uncontended), sum over slots */
     uint32_t* mt_np;          /* [E][625] (MT mode only, else NULL) */
     uint32_t* mt_py;          /* [E][625] */
+    int64_t counter_slots;
 } ffm_device_buffers;
 
 typedef struct ffm_engine ffm_engine;

@@ -68,8 +68,22 @@ int run(float* dff, unsigned short* pos, int* cnt, long long E, int blocks, cons
     return 0;
 }
 
+__global__ void fill_rand(float* p, long long n, unsigned seed) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) { unsigned h = (unsigned)i * 2654435761u ^ seed; h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15; p[i] = (float)(h & 0xFFFFFF) * 1e-6f; }
+}
 int probe();
 int main() {
+    {
+        const long long E = 65536;
+        float* d; unsigned short* ps; int* c;
+        CK(hipMalloc(&d, E * HW * 4)); CK(hipMalloc(&ps, E * A * 2)); CK(hipMalloc(&c, E * 4));
+        CK(hipMemset(d, 0, E * HW * 4));
+        run<1>(d, ps, c, E, 1024, "zeros: dff only");
+        fill_rand<<<(E * HW + 255) / 256, 256>>>(d, E * HW, 7);
+        CK(hipDeviceSynchronize());
+        run<1>(d, ps, c, E, 1024, "random: dff only");
+    }
     if (probe()) return 1;
     const long long E = 65536;
     float* dff;
