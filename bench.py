@@ -88,24 +88,31 @@ def main():
     torch.cuda.synchronize()
     c0 = eng.counters(stream)
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # Timed region: K back-to-back step launches on the stream, nothing in between.
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record(stream)
-        eng.step(1, stream)
-        ends[i].record(stream)
+    eng.step(args.steps, stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     c1 = eng.counters(stream)
-    kern_ms = [a.elapsed_time(b) for a, b in zip(starts, ends)]
     elapsed = t1 - t0
     agent_steps = c1["agent_steps"] - c0["agent_steps"]
+
+    # Per-launch kernel time for the roofline: HIP events around each launch on
+    # the launch stream (a separate pass, so the events do not perturb `value`).
+    nk = min(args.steps, 200)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
+    for i in range(nk):
+        starts[i].record(stream)
+        eng.step(1, stream)
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    kern_ms = [a.elapsed_time(b) for a, b in zip(starts, ends)]
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

@@ -90,7 +90,10 @@ __host__ __device__ inline WaveCarve wave_carve(int PHW, int AL, int EW, int F, 
     return c;
 }
 
-__host__ __device__ inline size_t wave_shared_bytes(int PHW) { return align16((size_t)PHW) + align16((size_t)PHW * 4); }
+// Block-shared LDS of the wave kernel: padded map codes, padded SFF, padded free-cell list.
+__host__ __device__ inline size_t wave_shared_bytes(int PHW) {
+    return align16((size_t)PHW) + align16((size_t)PHW * 4) + align16((size_t)PHW * 2);
+}
 
 size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves) {
     const int EW = A <= 32 ? 2 : 1;
@@ -98,10 +101,44 @@ size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int
     return wave_shared_bytes(PHW) + (size_t)waves * wave_carve(PHW, 64 / EW, EW, F, mt, reset).per_wave;
 }
 
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 // Philox placement of one env into slot_cell[0..N) (padded cells): all 64 lanes.
-__device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned long long* keys, uint16_t* slot_cell,
-                               int PW, int W, int lane) {
+// fl = padded free-cell list (LDS).  F <= 128: every (key, j) in registers, two
+// per lane, ranks by broadcasting each key with v_readlane.  Larger F: threshold
+// the keys into an LDS candidate list first (about 2N + 16 survive).
+__device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned long long* keys, const uint16_t* fl,
+                               uint16_t* slot_cell, int lane) {
     const int F = a.F, N = a.N;
+    if (F <= 128) {
+        const int j0 = lane, j1 = lane + 64;
+        const unsigned long long k0 =
+            j0 < F ? ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j0) << 32) | (unsigned)j0
+                   : ~0ull;
+        const unsigned long long k1 =
+            j1 < F ? ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j1) << 32) | (unsigned)j1
+                   : ~0ull;
+        int r0 = 0, r1 = 0;
+        const int n0 = F < 64 ? F : 64;
+        for (int q = 0; q < n0; q++) {
+            const unsigned long long kq = readlane64(k0, q);
+            r0 += kq < k0 ? 1 : 0;
+            r1 += kq < k1 ? 1 : 0;
+        }
+        for (int q = 0; q < F - 64; q++) {
+            const unsigned long long kq = readlane64(k1, q);
+            r0 += kq < k0 ? 1 : 0;
+            r1 += kq < k1 ? 1 : 0;
+        }
+        if (j0 < F && r0 < N) slot_cell[r0] = fl[j0];
+        if (j1 < F && r1 < N) slot_cell[r1] = fl[j1];
+        wave_sync();
+        return;
+    }
     uint32_t T = reset_threshold(N, F);
     int C = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
@@ -126,11 +163,7 @@ __device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned lo
         const unsigned long long ki = keys[i];
         int rank = 0;
         for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-        if (rank < N) {
-            const int cell = a.free_list[(int)(ki & 0xFFFFu)];
-            const int x = cell / W, y = cell - (cell / W) * W;
-            slot_cell[rank] = (uint16_t)((x + 1) * PW + y + 1);
-        }
+        if (rank < N) slot_cell[rank] = fl[(int)(ki & 0xFFFFu)];
     }
     wave_sync();
 }
@@ -163,6 +196,7 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
     const WaveCarve cv = wave_carve(PHW, AL, EW, a.F, MT, do_reset);
     uint8_t* pmap = smem;
     float* psff = reinterpret_cast<float*>(smem + align16((size_t)PHW));
+    uint16_t* pfree = reinterpret_cast<uint16_t*>(smem + align16((size_t)PHW) + align16((size_t)PHW * 4));
     unsigned char* wbase = smem + wave_shared_bytes(PHW) + (size_t)wv * cv.per_wave;
     GT* grid = reinterpret_cast<GT*>(wbase + cv.grid);
     float* tile = reinterpret_cast<float*>(wbase + cv.dff);
@@ -241,6 +275,7 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
             pmap[i] = a.pmap[i];
             psff[i] = reinterpret_cast<const float*>(a.psff)[i];
         }
+        for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
         for (int i = lane; i < EW * PHW; i += 64) tile[i] = 0.0f;
         __syncthreads();
         for (int i = lane; i < EW * PHW; i += 64) grid[i] = pmap[i - (i / PHW) * PHW];
@@ -283,13 +318,10 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
                 if (__ballot(rs && sub == s) == 0ull) continue;
                 const uint32_t ge = (uint32_t)(a.env_base + e0 + s);
                 if (FFM_ABLATE & 64) {   // diagnostic: trivial placement (first N free cells)
-                    if (lane < a.N) {
-                        const int cell = a.free_list[lane];
-                        snxt[s * AL + lane] = (uint16_t)((cell / W + 1) * PW + cell % W + 1);
-                    }
+                    if (lane < a.N) snxt[s * AL + lane] = pfree[lane];
                     wave_sync();
                 } else {
-                    wave_reset_env(a, ge, keys, snxt + s * AL, PW, W, lane);
+                    wave_reset_env(a, ge, keys, pfree, snxt + s * AL, lane);
                 }
                 for (int i = lane; i < HW; i += 64) {   // zero the env's DFF interior
                     const int x = i / W, y = i - (i / W) * W;
@@ -655,11 +687,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
                 const unsigned long long ki = keys[i];
                 int rank = 0;
                 for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-                if (rank < a.N) {
-                    const int cell = a.free_list[(int)(ki & 0xFFFFu)];
-                    const int x = cell / W, y = cell - (cell / W) * W;
-                    spos[k * A + rank] = (uint16_t)((x + 1) * PW + y + 1);
-                }
+                if (rank < a.N) spos[k * A + rank] = a.free_padded[(int)(ki & 0xFFFFu)];
             }
             for (int i = tid; i < PHW; i += BS) tile[k * PHW + i] = 0.0f;
             __syncthreads();
@@ -848,9 +876,12 @@ __global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     uint16_t* slot = reinterpret_cast<uint16_t*>(smem + align16((size_t)a.F * 8));
+    uint16_t* fl = slot + align16((size_t)(a.N > 0 ? a.N : 1) * 2) / 2;
     const long long e = blockIdx.x;
     const int PW = a.W + 2;
-    wave_reset_env(a, (uint32_t)(a.env_base + e), keys, slot, PW, a.W, threadIdx.x);
+    for (int i = threadIdx.x; i < a.F; i += 64) fl[i] = a.free_padded[i];
+    wave_sync();
+    wave_reset_env(a, (uint32_t)(a.env_base + e), keys, fl, slot, threadIdx.x);
     for (int s = threadIdx.x; s < a.N; s += 64) a.pos[e * a.A + s] = (uint16_t)unpad(slot[s], PW);
     if (threadIdx.x == 0) a.cnt[e] = a.N;
 }
@@ -957,7 +988,8 @@ hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, i
 }
 
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s) {
-    const size_t smem = align16((size_t)(a.F > 0 ? a.F : 1) * 8) + align16((size_t)(a.N > 0 ? a.N : 1) * 2);
+    const size_t smem = align16((size_t)(a.F > 0 ? a.F : 1) * 8) + align16((size_t)(a.N > 0 ? a.N : 1) * 2) +
+                        align16((size_t)(a.F > 0 ? a.F : 1) * 2);
     core_reset_kernel<<<dim3((unsigned)a.E), dim3(64), smem, s>>>(a);
     return hipGetLastError();
 }

@@ -49,6 +49,7 @@ struct ffm_engine {
     uint8_t* d_map = nullptr;    // padded map codes
     void* d_sff = nullptr;       // padded SFF
     uint16_t* d_free = nullptr;
+    uint16_t* d_free_padded = nullptr;
     uint16_t* d_pos = nullptr;
     int32_t* d_cnt = nullptr;
     float* d_dff = nullptr;
@@ -71,6 +72,7 @@ static void release(ffm_engine* e) {
     (void)hipFree(e->d_map);
     (void)hipFree(e->d_sff);
     (void)hipFree(e->d_free);
+    (void)hipFree(e->d_free_padded);
     (void)hipFree(e->d_pos);
     (void)hipFree(e->d_cnt);
     (void)hipFree(e->d_dff);
@@ -175,6 +177,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_map, (size_t)PHW);
     ALLOC(e->d_sff, sff_bytes);
     ALLOC(e->d_free, std::max<size_t>(1, fl.size()) * 2);
+    ALLOC(e->d_free_padded, std::max<size_t>(1, fl.size()) * 2);
     ALLOC(e->d_pos, E * A * 2);
     ALLOC(e->d_cnt, E * 4);
     ALLOC(e->d_dff, E * HW * 4);
@@ -198,6 +201,11 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
         he = hipMemcpy(e->d_sff, e->f64 ? (const void*)psff64.data() : (const void*)psff32.data(), sff_bytes,
                        hipMemcpyHostToDevice);
     if (he == hipSuccess && !fl.empty()) he = hipMemcpy(e->d_free, fl.data(), fl.size() * 2, hipMemcpyHostToDevice);
+    if (he == hipSuccess && !fl.empty()) {
+        std::vector<uint16_t> fp(fl.size());
+        for (size_t i = 0; i < fl.size(); i++) fp[i] = (uint16_t)((fl[i] / W + 1) * PW + fl[i] % W + 1);
+        he = hipMemcpy(e->d_free_padded, fp.data(), fp.size() * 2, hipMemcpyHostToDevice);
+    }
     if (he == hipSuccess) he = hipMemset(e->d_pos, 0xFF, E * A * 2);
     if (he == hipSuccess) he = hipMemset(e->d_cnt, 0, E * 4);
     if (he == hipSuccess) he = hipMemset(e->d_dff, 0, E * HW * 4);
@@ -260,6 +268,7 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
     a.auto_reset = e->d.auto_reset && !e->mt;
     a.N = e->d.n_agents;
     a.free_list = e->d_free;
+    a.free_padded = e->d_free_padded;
     a.F = e->F;
     a.mt_np = e->d_mt_np;
     a.mt_py = e->d_mt_py;

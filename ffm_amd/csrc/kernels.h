@@ -26,6 +26,7 @@ struct CoreStepArgs {
     uint32_t t;            // step index (Philox counter word 0)
     int auto_reset, N;     // re-place N agents when an env empties
     const uint16_t* free_list;  // [F] row-major free cells
+    const uint16_t* free_padded;  // [F] the same cells as padded indices (x+1)*(W+2)+y+1
     int F;
     uint32_t* mt_np;       // [E][625] MT mode
     uint32_t* mt_py;       // [E][625]
