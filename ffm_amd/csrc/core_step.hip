@@ -60,6 +60,9 @@
 #ifndef FFM_ABLATE
 #define FFM_ABLATE 0   // diagnostic builds only (tools/ablate.sh): bit k skips one phase
 #endif
+#ifndef FFM_WAVES_PER_EU
+#define FFM_WAVES_PER_EU 0   // minimum waves/SIMD requested for the wave kernel (0 = compiler's choice)
+#endif
 #ifndef FFM_LDS_PAD
 #define FFM_LDS_PAD 0  // diagnostic builds only: extra dynamic LDS per block to pin occupancy
 #endif
@@ -179,7 +182,11 @@ struct WavePrefetch {
 };
 
 template <int NB, bool MT, int EW, int HT, int WT>
-__global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
+__global__ __launch_bounds__(256)
+#if FFM_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(FFM_WAVES_PER_EU)))
+#endif
+void core_wave_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     using GT = uint8_t;
     constexpr int AL = 64 / EW;
@@ -302,41 +309,14 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
         const bool env_ok = sub < nenv;
         const uint32_t genv = (uint32_t)(a.env_base + e0 + sub);
 
-        int cnt = scnt[sub];
-        const bool rs = do_reset && env_ok && cnt == 0 && !(FFM_ABLATE & 32);
+        const int cnt = scnt[sub];
         int pp = -1;
         if (env_ok && al < A && al < cnt) {
             const int c = spos[lane];
             const int x = c / W, y = c - (c / W) * W;
             pp = (x + 1) * PW + y + 1;
         }
-
-        // ---- on-device auto-reset (Philox placement) ------------------------
-        if (do_reset) {
-#pragma unroll
-            for (int s = 0; s < EW; s++) {
-                if (__ballot(rs && sub == s) == 0ull) continue;
-                const uint32_t ge = (uint32_t)(a.env_base + e0 + s);
-                if (FFM_ABLATE & 64) {   // diagnostic: trivial placement (first N free cells)
-                    if (lane < a.N) snxt[s * AL + lane] = pfree[lane];
-                    wave_sync();
-                } else {
-                    wave_reset_env(a, ge, keys, pfree, snxt + s * AL, lane);
-                }
-                for (int i = lane; i < HW; i += 64) {   // zero the env's DFF interior
-                    const int x = i / W, y = i - (i / W) * W;
-                    tile[s * PHW + (x + 1) * PW + y + 1] = 0.0f;
-                }
-                wave_sync();
-            }
-            if (rs) {
-                cnt = a.N;
-                pp = al < cnt ? (int)nx[al] : -1;
-            }
-            wave_sync();
-        }
         c_steps += (al == 0 && env_ok) ? cnt : 0;
-        c_resets += (al == 0 && rs) ? 1 : 0;
         const bool live = pp >= 0;
         STAMP(0);
 
@@ -459,6 +439,24 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
         const int newcnt = __popcll(km & segm);
         c_exits += (al == 0 && env_ok) ? cnt - newcnt : 0;
         if (live) gk[pp] = 0;   // unmark: agents only ever stand on free cells
+
+        // ---- auto-reset of an env this step emptied (Philox placement keyed by t) ---
+        // Done at the END of the step, when the decide/resolve registers are dead.
+        const bool rs = do_reset && env_ok && newcnt == 0 && !(FFM_ABLATE & 32);
+        if (do_reset) {
+#pragma unroll
+            for (int s = 0; s < EW; s++) {
+                if (__ballot(rs && sub == s) == 0ull) continue;
+                const uint32_t ge = (uint32_t)(a.env_base + e0 + s);
+                if (FFM_ABLATE & 64) {   // diagnostic: trivial placement (first N free cells)
+                    if (lane < a.N) snxt[s * AL + lane] = pfree[lane];
+                    wave_sync();
+                } else {
+                    wave_reset_env(a, ge, keys, pfree, snxt + s * AL, lane);
+                }
+            }
+        }
+        c_resets += (al == 0 && rs) ? 1 : 0;
         STAMP(5);
 
         // ---- update_dff (model/ffm_core.py:106-117), float4 per lane ------------------
@@ -507,6 +505,8 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
         STAMP(6);
 
         // ---- stage the next group (its loads were issued at the top), then store ------
+        const int rst_pos = rs && al < a.N ? (int)nx[al] : -1;   // placement of a reset env
+        const unsigned long long rsm = __ballot(rs);
         stage(nxtpf);
         if (!(FFM_ABLATE & 16)) {
             uint16_t* gp = a.pos + e0 * A;
@@ -514,12 +514,19 @@ __global__ __launch_bounds__(256) void core_wave_kernel(CoreStepArgs a) {
             float4* gd = reinterpret_cast<float4*>(a.dff + e0 * HW);
             const int n4 = nenv * HW / 4;
             if (keep) gp[sub * A + newidx] = (uint16_t)unpad(nxt, PW);
+            if (rst_pos >= 0) gp[sub * A + al] = (uint16_t)unpad(rst_pos, PW);
             if (al == 0 && env_ok) {
-                gc[sub] = newcnt;
+                gc[sub] = rs ? a.N : newcnt;
                 if (rs && a.episodes) a.episodes[e0 + sub] += 1;
             }
-            if (tb0 >= 0 && lane < n4) gd[lane] = make_float4(o0[0], o0[1], o0[2], o0[3]);
-            if (tb1 >= 0 && lane + 64 < n4) gd[lane + 64] = make_float4(o1[0], o1[1], o1[2], o1[3]);
+            // a reset env starts its next episode with a zero DFF
+            const int zs0 = (4 * lane) / HW, zs1 = (4 * (lane + 64)) / HW;
+            const bool z0 = zs0 < EW && ((rsm >> (zs0 * AL)) & 1ull);
+            const bool z1 = zs1 < EW && ((rsm >> (zs1 * AL)) & 1ull);
+            if (tb0 >= 0 && lane < n4)
+                gd[lane] = z0 ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(o0[0], o0[1], o0[2], o0[3]);
+            if (tb1 >= 0 && lane + 64 < n4)
+                gd[lane + 64] = z1 ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(o1[0], o1[1], o1[2], o1[3]);
         }
         wave_sync();
         STAMP(7);
@@ -640,58 +647,19 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         grid[i] = a.pmap[pc];
     }
     if (tid < K) {
-        const int c = a.cnt[e0 + tid];
-        const bool rs = do_reset && c == 0;
-        sreset[tid] = rs ? 1 : 0;
-        scnt[tid] = rs ? a.N : c;
+        scnt[tid] = a.cnt[e0 + tid];
+        sreset[tid] = 0;
     }
     __syncthreads();
     for (int it = tid; it < nA; it += BS) {
         const int k = it / A, i = it - k * A;
         int pp = 0xFFFF;
-        if (i < scnt[k] && !sreset[k]) {
+        if (i < scnt[k]) {
             const int c = a.pos[(e0 + k) * A + i];
             const int x = c / W, y = c - (c / W) * W;
             pp = (x + 1) * PW + y + 1;
         }
         spos[it] = (uint16_t)pp;
-    }
-
-    // ---- on-device auto-reset (Philox placement) ------------------------------------
-    if (do_reset) {
-        for (int k = 0; k < K; k++) {
-            if (!sreset[k]) continue;   // block-uniform
-            const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
-            uint32_t T = reset_threshold(a.N, a.F);
-            int C = 0;
-            for (int attempt = 0; attempt < 2; attempt++) {
-                C = 0;
-                for (int j0 = 0; j0 < a.F; j0 += BS) {
-                    const int j = j0 + tid;
-                    uint32_t key = 0;
-                    bool cand = false;
-                    if (j < a.F) {
-                        key = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
-                        cand = key <= T;
-                    }
-                    int tot;
-                    const int ex = block_excl_scan<BS>(cand, swsum, tot);
-                    if (cand) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
-                    C += tot;
-                }
-                if (C >= a.N || T == 0xFFFFFFFFu) break;
-                T = 0xFFFFFFFFu;
-            }
-            __syncthreads();
-            for (int i = tid; i < C; i += BS) {
-                const unsigned long long ki = keys[i];
-                int rank = 0;
-                for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-                if (rank < a.N) spos[k * A + rank] = a.free_padded[(int)(ki & 0xFFFFu)];
-            }
-            for (int i = tid; i < PHW; i += BS) tile[k * PHW + i] = 0.0f;
-            __syncthreads();
-        }
     }
     __syncthreads();
 
@@ -833,6 +801,44 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         }
     }
 
+    // ---- auto-reset of envs this step emptied (Philox placement keyed by t) -------------------
+    if (do_reset) {
+        if (tid < K) sreset[tid] = snew[tid] == 0 ? 1 : 0;
+        __syncthreads();
+        for (int k = 0; k < K; k++) {
+            if (!sreset[k]) continue;   // block-uniform
+            const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
+            uint32_t T = reset_threshold(a.N, a.F);
+            int C = 0;
+            for (int attempt = 0; attempt < 2; attempt++) {
+                C = 0;
+                for (int j0 = 0; j0 < a.F; j0 += BS) {
+                    const int j = j0 + tid;
+                    uint32_t key = 0;
+                    bool cand = false;
+                    if (j < a.F) {
+                        key = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
+                        cand = key <= T;
+                    }
+                    int tot;
+                    const int ex = block_excl_scan<BS>(cand, swsum, tot);
+                    if (cand) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
+                    C += tot;
+                }
+                if (C >= a.N || T == 0xFFFFFFFFu) break;
+                T = 0xFFFFFFFFu;
+            }
+            __syncthreads();
+            for (int i = tid; i < C; i += BS) {
+                const unsigned long long ki = keys[i];
+                int rank = 0;
+                for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
+                if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[(int)(ki & 0xFFFFu)], PW);
+            }
+            __syncthreads();
+        }
+    }
+
     // ---- counters ---------------------------------------------------------------------------
     if (tid == 0) {
         unsigned long long steps = 0, exits = 0, resets = 0;
@@ -848,7 +854,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         if (blockIdx.x == 0) atomicAdd(&slot[3], 1ull);
     }
     if (tid < K) {
-        a.cnt[e0 + tid] = snew[tid];
+        a.cnt[e0 + tid] = sreset[tid] ? a.N : snew[tid];
         if (sreset[tid] && a.episodes) a.episodes[e0 + tid] += 1;
     }
 
@@ -865,7 +871,8 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             const float t = a.c1 * p[nb_dx<NB>(q) * PW + nb_dy<NB>(q)];               // :113
             acc = acc + t;
         }
-        a.dff[e0 * HW + c] = acc < 1e-4f ? 0.0f : acc;                                // :116-117
+        // :116-117; an env reset this step starts its next episode with a zero DFF
+        a.dff[e0 * HW + c] = (acc < 1e-4f || sreset[k]) ? 0.0f : acc;
     }
 }
 

@@ -75,7 +75,8 @@ typedef struct {
     int32_t agent_capacity;   /* A: slots per env (>= n_agents) */
     int32_t n_agents;         /* N placed by reset / auto-reset */
     int32_t rng_mode;         /* FFM_RNG_* */
-    int32_t auto_reset;       /* 1: an env that empties is re-placed at the start of the next step */
+    int32_t auto_reset;       /* 1: an env emptied by a step is re-placed (Philox, keyed by that
+                                 step) and its DFF zeroed at the end of that step */
     uint64_t seed;            /* Philox key */
     int64_t env_base;         /* global id of env 0 (multi-GPU sharding keys RNG by global id) */
     int32_t device;           /* HIP device ordinal */

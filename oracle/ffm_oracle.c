@@ -543,17 +543,19 @@ void ffo_core_step_philox_batch(const ffo_core_cfg* c, int64_t E, int32_t A_cap,
             uint16_t* pe = pos + e * (int64_t)A_cap;
             float* de = dff + e * (int64_t)HW;
             int32_t n = counts[e];
+            total += (uint64_t)n;
+            for (int i = 0; i < n; i++) p32[i] = pe[i];
+            rngctx r = {1, NULL, NULL, seed, t, (uint64_t)(env_base + e)};
+            core_step(c, p32, &n, de, occ, work, &r);
+            for (int i = 0; i < n; i++) pe[i] = (uint16_t)p32[i];
+            /* Auto-reset at the END of the step that empties an env (DESIGN.md
+             * "Episodes"): placement keyed by this step's t, DFF zeroed. */
             if (auto_reset && n == 0) {
                 reset_with_list(fl, F, N_reset, seed, t, env_base + e, scratch, pe);
                 n = N_reset;
                 for (int i = 0; i < HW; i++) de[i] = 0.0f;
                 if (episodes) episodes[e]++;
             }
-            total += (uint64_t)n;
-            for (int i = 0; i < n; i++) p32[i] = pe[i];
-            rngctx r = {1, NULL, NULL, seed, t, (uint64_t)(env_base + e)};
-            core_step(c, p32, &n, de, occ, work, &r);
-            for (int i = 0; i < n; i++) pe[i] = (uint16_t)p32[i];
             counts[e] = n;
         }
         free(occ);
