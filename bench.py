@@ -114,13 +114,15 @@ def main():
     torch.cuda.synchronize()
     kern_ms = [a.elapsed_time(b) for a, b in zip(starts, ends)]
 
+    # Achievable HBM bandwidth on this box: a device-to-device copy of the same
+    # number of bytes one launch moves (read + write), for context beside `peak`.
+    copy_gbs = copy_bandwidth(torch, stream, E * (2 * A + 4 * H * W + 4))
+
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        n = torch.tensor([agent_steps], dtype=torch.int64, device="cuda")
-        dist.all_reduce(n, op=dist.ReduceOp.SUM)
-        agent_steps = int(n.item())
+        from ffm_amd.dist import reduce_counters, reduce_max
+        elapsed = reduce_max(elapsed, device="cuda")
+        d = {k: c1[k] - c0[k] for k in ("agent_steps", "exits", "resets", "steps")}
+        agent_steps = reduce_counters(d, device="cuda")["agent_steps"]
 
     if rank == 0:
         bytes_per_env_step = 2 * (2 * A + 4 * H * W + 4)
@@ -158,6 +160,8 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                 "bytes_per_launch_algorithmic": E * bytes_per_env_step,
+                "achievable_copy_GBs": copy_gbs,
+                "frac_of_copy": achieved / copy_gbs if copy_gbs else None,
             },
             "cpu_baseline": None,
         }
@@ -167,6 +171,26 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def copy_bandwidth(torch, stream, nbytes, reps=50):
+    """GB/s (read + write bytes) of a device-to-device copy of `nbytes`."""
+    n = max(1, nbytes // 4)
+    src = torch.ones(n, dtype=torch.float32, device="cuda")
+    dst = torch.empty_like(src)
+    with torch.cuda.stream(stream):
+        for _ in range(5):
+            dst.copy_(src)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            dst.copy_(src)
+        b.record(stream)
+    torch.cuda.synchronize()
+    sec = a.elapsed_time(b) / 1e3 / reps
+    del src, dst
+    return 2 * n * 4 / sec / 1e9
 
 
 def cpu_baseline(args, m, s, params, torch):
@@ -197,6 +221,14 @@ def cpu_baseline(args, m, s, params, torch):
         total += core.step_philox_batch(pos, cnt, dff, eps, args.seed, t, True, A, 0, threads)
         t += 1
     elapsed = time.perf_counter() - tb
+    # single-thread rate on a smaller slice of the same state (~3 s)
+    n1 = min(E, 512)
+    p1, c1_, d1, e1 = pos[:n1].copy(), cnt[:n1].copy(), dff[:n1].copy(), eps[:n1].copy()
+    t1, tot1, st1 = t, 0, time.perf_counter()
+    while time.perf_counter() - st1 < 3.0:
+        tot1 += core.step_philox_batch(p1, c1_, d1, e1, args.seed, t1, True, A, 0, 1)
+        t1 += 1
+    one_thread = tot1 / (time.perf_counter() - st1)
     # bit-exact check of the first envs against a fresh GPU engine
     nchk = min(1024, E)
     g = Engine(m, s, n_envs=nchk, n_agents=A, params=params, rng="philox", seed=args.seed,
@@ -220,7 +252,7 @@ def cpu_baseline(args, m, s, params, torch):
         "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
         "sample": (f"oracle/ffm_oracle.c Philox mode, {E} envs x {steps} steps of the same workload "
                    f"(OpenMP {threads} threads, {model}); first {nchk} envs bit-exact vs GPU: {ok}"),
-        "seconds": elapsed, "bit_exact_vs_gpu": ok,
+        "seconds": elapsed, "bit_exact_vs_gpu": ok, "value_1thread": one_thread,
     }
 
 

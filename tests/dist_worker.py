@@ -1,0 +1,80 @@
+"""Per-rank bodies of the world-size-2 ``gloo`` tests (tests/test_dist.py).
+
+Each rank steps its shard of the global env range (ffm_amd.dist.shard_range),
+keyed by global env id, then the shards are gathered on rank 0 and compared
+with a single-process run of the whole range.  ``backend`` is the CPU oracle
+(tests here) or the HIP engine on cuda:0 (the -m gpu variant).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch.distributed as dist
+
+PARAMS = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"}
+SEED, A, STEPS = 42, 32, 40
+
+
+def room():
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    return m, l1_sff(m)
+
+
+def run_oracle(env_base, n):
+    """Philox-mode run of envs [env_base, env_base+n) on the CPU oracle."""
+    from oracle import oracle as O
+    m, s = room()
+    core = O.Core(m, s, PARAMS)
+    pos = np.zeros((n, A), np.uint16)
+    for e in range(n):
+        pos[e] = core.reset_philox(A, SEED, 0, env_base + e)
+    cnt = np.full(n, A, np.int32)
+    dff = np.zeros((n, 12, 12), np.float32)
+    eps = np.zeros(n, np.int32)
+    tot = 0
+    for t in range(1, STEPS + 1):
+        tot += core.step_philox_batch(pos, cnt, dff, eps, SEED, t, True, A, env_base, 1)
+    return pos, cnt, dff.reshape(n, -1), eps, {"agent_steps": tot, "exits": 0, "resets": int(eps.sum()),
+                                                "steps": STEPS}
+
+
+def run_engine(env_base, n):
+    """The same on the MI355X through the C ABI (all ranks share cuda:0)."""
+    from ffm_amd.engine import Engine
+    m, s = room()
+    eng = Engine(m, s, n_envs=n, n_agents=A, params=PARAMS, rng="philox", seed=SEED,
+                 auto_reset=True, env_base=env_base, device=0)
+    eng.reset()
+    eng.step(STEPS)
+    pos, cnt, dff = eng.get_state()
+    eps = eng.get_episodes() if hasattr(eng, "get_episodes") else np.zeros(n, np.int32)
+    c = eng.counters()
+    eng.close()
+    return pos, cnt, dff.reshape(n, -1), eps, c
+
+
+def worker(rank, world, port, n_global, backend, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ffm_amd.dist import shard_range, reduce_counters
+        base, n = shard_range(n_global, rank, world)
+        run = run_oracle if backend == "oracle" else run_engine
+        pos, cnt, dff, eps, c = run(base, n)
+        # live agents only: slots past count are unspecified
+        mask = np.arange(A)[None, :] < cnt[:, None]
+        pos = np.where(mask, pos, 0xFFFF).astype(np.int32)
+        # shards differ in size by one env: gather as objects (small test sizes)
+        gathered = []
+        for p in (pos, cnt, dff.view(np.int32)):
+            parts = [None] * world
+            dist.all_gather_object(parts, p)
+            gathered.append(np.concatenate(parts))
+        red = reduce_counters(c)
+        if rank == 0:
+            np.savez(out_path, pos=gathered[0], cnt=gathered[1], dff=gathered[2],
+                     agent_steps=red["agent_steps"], steps=red["steps"])
+    finally:
+        dist.destroy_process_group()

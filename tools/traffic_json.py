@@ -1,0 +1,53 @@
+"""Per-launch HBM bytes of the step kernel from the two PMC passes of tools/traffic.sh.
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md,
+HBM/rocprofv3 section): FETCH_SIZE counts 128-B streaming requests at 64 B, so
+it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
+"""
+import csv
+import json
+import os
+import sys
+
+out = sys.argv[1]
+args = sys.argv[2:]
+
+
+def per_dispatch(path, counter):
+    vals = []
+    for root, _, files in os.walk(path):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                with open(os.path.join(root, f)) as fh:
+                    for r in csv.DictReader(fh):
+                        if "core_wave_kernel" in r["Kernel_Name"] or "core_block_kernel" in r["Kernel_Name"]:
+                            if r["Counter_Name"] == counter:
+                                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+f = per_dispatch(os.path.join(out, "fetch"), "FETCH_SIZE")
+w = per_dispatch(os.path.join(out, "write"), "WRITE_SIZE")
+f = f[10:] or f   # drop the warmup launches
+w = w[10:] or w
+fk = sum(f) / len(f)
+wk = sum(w) / len(w)
+
+def arg(name, default):
+    return args[args.index(name) + 1] if name in args else default
+
+E = int(arg("--envs", 65536)); S = int(arg("--size", 12)); A = int(arg("--agents", 32))
+alg = E * 2 * (2 * A + 4 * S * S + 4)
+res = {
+    "config": f"{S}x{S}_A{A}_E{E}",
+    "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
+    "fetch_size_kib_raw": fk, "write_size_kib_raw": wk,
+    "read_bytes_corrected": 2 * fk * 1024, "write_bytes": wk * 1024,
+    "algorithmic_bytes_per_launch": alg,
+    "launches": [len(f), len(w)],
+    "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM/rocprofv3 section); WRITE_SIZE as is",
+}
+res["traffic_over_algorithmic"] = res["hbm_bytes_per_launch"] / alg
+print(json.dumps(res, indent=1))
+with open(os.path.join(out, "traffic.json"), "w") as fh:
+    json.dump(res, fh, indent=1)
