@@ -102,17 +102,17 @@ def main():
     elapsed = t1 - t0
     agent_steps = c1["agent_steps"] - c0["agent_steps"]
 
-    # Per-launch kernel time for the roofline: HIP events around each launch on
-    # the launch stream (a separate pass, so the events do not perturb `value`).
+    # Kernel time for the roofline: HIP events on the launch stream bracketing
+    # nk back-to-back launches (a separate pass, so events do not perturb
+    # `value`); per-launch event pairs would add their own gaps to each launch.
     nk = min(args.steps, 200)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nk)]
-    for i in range(nk):
-        starts[i].record(stream)
-        eng.step(1, stream)
-        ends[i].record(stream)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    eng.step(nk, stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
-    kern_ms = [a.elapsed_time(b) for a, b in zip(starts, ends)]
+    kern_ms = [ev0.elapsed_time(ev1) / nk]
 
     # Achievable HBM bandwidth on this box: a device-to-device copy of the same
     # number of bytes one launch moves (read + write), for context beside `peak`.

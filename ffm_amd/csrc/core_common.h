@@ -263,6 +263,23 @@ __device__ __forceinline__ int kth_slot(const uint16_t (&who)[NB], const bool (&
     return sel;
 }
 
+// Philox-mode friction for a contested target: z, w = words 2, 3
+// of the owner's decide block.  Coin: z < 2^31 (exactly 1/2).  Winner rank:
+// Lemire multiply-shift of w by m, exact through rejection of the low word below
+// 2^32 mod m (probability < m/2^32); a rejected word is replaced from the owner's
+// friction stream.  Returns the rank in [0, m) or -1 (nobody moves).
+__device__ __forceinline__ int philox_friction(uint32_t z, uint32_t w, uint32_t m, uint32_t k0, uint32_t k1,
+                                               uint32_t t, uint32_t genv, uint32_t owner) {
+    if (z >= 0x80000000u) return -1;
+    const uint32_t thr = (uint32_t)((0x044101000ull >> (4 * m)) & 0xFu);   // 2^32 mod m, m = 2..8
+    unsigned long long prod = (unsigned long long)w * m;
+    if ((uint32_t)prod < thr) {
+        PhiloxStream ps(k0, k1, t, genv, owner, kPurFriction);
+        do prod = (unsigned long long)ps.next() * m; while ((uint32_t)prod < thr);
+    }
+    return (int)(prod >> 32);
+}
+
 // Philox-mode placement key of free-list entry j (see DESIGN.md "Placement").
 __device__ __forceinline__ uint32_t reset_key(uint32_t k0, uint32_t k1, uint32_t t, uint32_t genv, uint32_t j) {
     return philox(make_uint4(t, genv, j, kPurReset << 28), k0, k1).x;

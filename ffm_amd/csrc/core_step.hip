@@ -85,7 +85,7 @@ __host__ __device__ inline WaveCarve wave_carve(int PHW, int AL, int EW, int F, 
     c.dff = o;  o += align16((size_t)EW * PHW * 4);        // f32 tile, zero halo
     c.req = o;  o += align16((size_t)EW * AL * 2);
     c.nxt = o;  o += align16((size_t)EW * AL * 2);
-    c.u = o;    o += mt ? align16((size_t)EW * AL * 8) : 0;
+    c.u = o;    o += align16((size_t)EW * AL * 8);        // MT: f64 draws; Philox: friction words
     c.flag = o; o += mt ? align16((size_t)EW * AL * 2) : 0;
     c.keys = o; o += reset ? align16((size_t)F * 8) : 0;
     c.spos = o; o += align16(64 * 2 + 2 * 4);
@@ -337,8 +337,11 @@ void core_wave_kernel(CoreStepArgs a) {
                 r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64,
                                           DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)});
             } else {
-                const DrawPhilox d{a.key0, a.key1, a.t, genv, (uint32_t)al};
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, d);
+                const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
+                // words 2, 3 feed the friction draw if this agent owns a contested target
+                reinterpret_cast<uint2*>(wbase + cv.u)[lane] = make_uint2(pb.z, pb.w);
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64,
+                                          DrawFixed{u53(pb.x, pb.y)});
             }
         }
         if (MT) {
@@ -408,9 +411,9 @@ void core_wave_kernel(CoreStepArgs a) {
                         const uint32_t hsh = (genv * 2654435761u) ^ ((uint32_t)al * 40503u) ^ a.t;
                         if (hsh & 1) ws = kth_slot<NB>(who, is, (int)((hsh >> 8) % (uint32_t)m));
                     } else {
-                        PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)al, kPurFriction);
-                        const double u = ps.next_u53();                                    // :95
-                        if (u < 0.5) ws = kth_slot<NB>(who, is, (int)ps.randbelow((uint32_t)m));   // :96
+                        const uint2 f = reinterpret_cast<const uint2*>(wbase + cv.u)[lane];
+                        const int kk = philox_friction(f.x, f.y, (uint32_t)m, a.key0, a.key1, a.t, genv, (uint32_t)al);
+                        if (kk >= 0) ws = kth_slot<NB>(who, is, kk);                            // :95-96
                     }
                     if (ws >= 0) {
                         int wcell = (int)r;
@@ -760,9 +763,10 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             const int f = reinterpret_cast<uint16_t*>(smem + cv.flag)[it];
             if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
         } else {
-            PhiloxStream ps(a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i, kPurFriction);
-            const double u = ps.next_u53();                                           // :95
-            if (u < 0.5) ws = kth_slot<NB>(who, is, (int)ps.randbelow((uint32_t)m));    // :96
+            const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
+            const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)i, kPurDecide << 28), a.key0, a.key1);
+            const int kk = philox_friction(pb.z, pb.w, (uint32_t)m, a.key0, a.key1, a.t, genv, (uint32_t)i);
+            if (kk >= 0) ws = kth_slot<NB>(who, is, kk);                                // :95-96
         }
         if (ws >= 0) {
             int wcell = r;

@@ -246,14 +246,6 @@ static double ps_u53(pstream* p) {
     return u53_from_words(a, b);
 }
 
-static uint32_t ps_randbelow(pstream* p, uint32_t n) {
-    if (n <= 1) return 0;
-    int k = bit_length(n);
-    uint32_t r = ps_next(p) >> (32 - k);
-    while (r >= n) r = ps_next(p) >> (32 - k);
-    return r;
-}
-
 /* ======================================================================
  * Draw dispatch: MT mode consumes the two global streams in the reference's
  * order; Philox mode keys every draw by (t, env, agent/owner, purpose).
@@ -282,11 +274,24 @@ static int draw_friction(rngctx* r, int owner, uint32_t m) {
         if (u < 0.5) return (int)ffo_py_randbelow(r->py, m);  /* random.choice, :96 */
         return -1;
     }
-    pstream p;
-    ps_init(&p, r->seed, r->t, r->genv, (uint32_t)owner, PUR_FRICTION);
-    double u = ps_u53(&p);
-    if (u < 0.5) return (int)ps_randbelow(&p, m);
-    return -1;
+    /* Philox mode: the owner's decide block B supplies the
+     * coin (B.z < 2^31, probability exactly 1/2) and the winner rank by
+     * Lemire's multiply-shift on B.w, exact through rejection; a rejected word
+     * (probability < m/2^32) is replaced by the owner's friction stream. */
+    uint32_t ctr[4] = {r->t, (uint32_t)r->genv, (uint32_t)owner, (uint32_t)PUR_DECIDE << 28};
+    uint32_t key[2] = {(uint32_t)r->seed, (uint32_t)(r->seed >> 32)};
+    uint32_t b[4];
+    ffo_philox(ctr, key, b);
+    if (b[2] >= 0x80000000u) return -1;
+    if (m <= 1) return 0;
+    const uint32_t thr = (uint32_t)(-m) % m;
+    uint64_t prod = (uint64_t)b[3] * m;
+    if ((uint32_t)prod < thr) {
+        pstream p;
+        ps_init(&p, r->seed, r->t, r->genv, (uint32_t)owner, PUR_FRICTION);
+        do prod = (uint64_t)ps_next(&p) * m; while ((uint32_t)prod < thr);
+    }
+    return (int)(prod >> 32);
 }
 
 /* ======================================================================
