@@ -137,19 +137,25 @@ __device__ __forceinline__ int fast_choice(const float (&x)[NB + 1], const bool 
 // Every slot is evaluated unconditionally (all neighbour cells exist in the
 // padded grid), so the LDS loads issue together and no lane diverges except
 // into the rare exact path.
+// The DFF tile may use a wider row stride than the grid: the tile index of grid
+// cell c in row x + dx of the agent is c + dd0 + dx * dws (dd0 = dws = 0 when the
+// tile shares the grid's layout).
 template <int NB, bool F64, class GT, class Draw>
 __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const float* sff32,
-                                           const double* sff64, const float* dff, float kS32, float kD32,
-                                           double kS64, const Draw& draw) {
+                                           const double* sff64, const float* dff, int dd0, int dws,
+                                           float kS32, float kD32, double kS64, const Draw& draw) {
     int cell[NB + 1];
+    int dcell[NB + 1];
     bool v[NB + 1];
     uint32_t g[NB];
 #pragma unroll
     for (int s = 0; s < NB; s++) {
         cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
+        dcell[s] = cell[s] + dd0 + nb_dx<NB>(s) * dws;
         g[s] = grid[cell[s]];
     }
     cell[NB] = pp;                                                   // :64 stay, last
+    dcell[NB] = pp + dd0;
     v[NB] = true;
     int nvalid = 0;
     int exit_cell = -1;
@@ -166,7 +172,7 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
 #pragma unroll
         for (int k = 0; k <= NB; k++) {
             const float a = kS32 * sff32[cell[k]];
-            const float b = kD32 * dff[cell[k]];
+            const float b = kD32 * dff[dcell[k]];
             sc[k] = a + b;                                           // :77
         }
         float mx = -__builtin_inff();
@@ -205,7 +211,7 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
 #pragma unroll
         for (int k = 0; k <= NB; k++) {
             if (!v[k]) { sc[k] = 0.0; continue; }
-            const float b = kD32 * dff[cell[k]];
+            const float b = kD32 * dff[dcell[k]];
             sc[k] = kS64 * sff64[cell[k]] + (double)b;
             mx = sc[k] > mx ? sc[k] : mx;
         }

@@ -78,11 +78,18 @@ struct WaveCarve {
     size_t grid, dff, req, nxt, u, flag, keys, spos, per_wave;
 };
 
-__host__ __device__ inline WaveCarve wave_carve(int PHW, int AL, int EW, int F, bool mt, bool reset) {
+// DFF tile of one env: 4 leading zero floats, then rows of DW = W + 4 floats
+// (16-B aligned, W % 4 == 0): a zero halo row above and below the map; columns
+// W..W+3 of each row are zero and serve as the right halo of that row and the left
+// halo of the next (the leading 4 floats are the left halo of the top halo row,
+// read by Moore diagonals).  TS floats per env; cell (x, y) at 4 + (x+1)*DW + y.
+__host__ __device__ inline int wave_tile_floats(int H, int W) { return 4 + (H + 2) * (W + 4); }
+
+__host__ __device__ inline WaveCarve wave_carve(int PHW, int TS, int AL, int EW, int F, bool mt, bool reset) {
     WaveCarve c;
     size_t o = 0;
     c.grid = o; o += align16((size_t)EW * PHW);            // u8 codes
-    c.dff = o;  o += align16((size_t)EW * PHW * 4);        // f32 tile, zero halo
+    c.dff = o;  o += align16((size_t)EW * TS * 4);         // f32 tiles, zero halo
     c.req = o;  o += align16((size_t)EW * AL * 2);
     c.nxt = o;  o += align16((size_t)EW * AL * 2);
     c.u = o;    o += align16((size_t)EW * AL * 8);        // MT: f64 draws; Philox: friction words
@@ -101,7 +108,8 @@ __host__ __device__ inline size_t wave_shared_bytes(int PHW) {
 size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves) {
     const int EW = A <= 32 ? 2 : 1;
     const int PHW = (H + 2) * (W + 2);
-    return wave_shared_bytes(PHW) + (size_t)waves * wave_carve(PHW, 64 / EW, EW, F, mt, reset).per_wave;
+    return wave_shared_bytes(PHW) +
+           (size_t)waves * wave_carve(PHW, wave_tile_floats(H, W), 64 / EW, EW, F, mt, reset).per_wave;
 }
 
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
@@ -110,35 +118,28 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
     return ((unsigned long long)hi << 32) | lo;
 }
 
-// Philox placement of one env into slot_cell[0..N) (padded cells): all 64 lanes.
-// fl = padded free-cell list (LDS).  F <= 128: every (key, j) in registers, two
-// per lane, ranks by broadcasting each key with v_readlane.  Larger F: threshold
-// the keys into an LDS candidate list first (about 2N + 16 survive).
+// Philox placement of one env, stored straight to its global positions gpos[0..N)
+// (unpadded cell indices): all 64 lanes.
+// fl = padded free-cell list (LDS).  F <= 128: the (key, j) pairs go to LDS and
+// each lane ranks its two by broadcast reads -- few registers, because this
+// rarely-taken branch sits inside the step loop and would otherwise set the
+// kernel's VGPR peak.  Larger F: threshold the keys into an LDS candidate list
+// first (about 2N + 16 survive).
 __device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned long long* keys, const uint16_t* fl,
-                               uint16_t* slot_cell, int lane) {
+                               uint16_t* gpos, int lane) {
+    const int PW = a.W + 2;
     const int F = a.F, N = a.N;
     if (F <= 128) {
-        const int j0 = lane, j1 = lane + 64;
-        const unsigned long long k0 =
-            j0 < F ? ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j0) << 32) | (unsigned)j0
-                   : ~0ull;
-        const unsigned long long k1 =
-            j1 < F ? ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j1) << 32) | (unsigned)j1
-                   : ~0ull;
-        int r0 = 0, r1 = 0;
-        const int n0 = F < 64 ? F : 64;
-        for (int q = 0; q < n0; q++) {
-            const unsigned long long kq = readlane64(k0, q);
-            r0 += kq < k0 ? 1 : 0;
-            r1 += kq < k1 ? 1 : 0;
+        for (int j = lane; j < F; j += 64)
+            keys[j] = ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j) << 32) | (unsigned)j;
+        wave_sync();
+        for (int j = lane; j < F; j += 64) {
+            const unsigned long long kj = keys[j];
+            int r = 0;
+#pragma unroll 4
+            for (int q = 0; q < F; q++) r += keys[q] < kj ? 1 : 0;
+            if (r < N) gpos[r] = (uint16_t)unpad(fl[j], PW);
         }
-        for (int q = 0; q < F - 64; q++) {
-            const unsigned long long kq = readlane64(k1, q);
-            r0 += kq < k0 ? 1 : 0;
-            r1 += kq < k1 ? 1 : 0;
-        }
-        if (j0 < F && r0 < N) slot_cell[r0] = fl[j0];
-        if (j1 < F && r1 < N) slot_cell[r1] = fl[j1];
         wave_sync();
         return;
     }
@@ -166,7 +167,7 @@ __device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned lo
         const unsigned long long ki = keys[i];
         int rank = 0;
         for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-        if (rank < N) slot_cell[rank] = fl[(int)(ki & 0xFFFFu)];
+        if (rank < N) gpos[rank] = (uint16_t)unpad(fl[(int)(ki & 0xFFFFu)], PW);
     }
     wave_sync();
 }
@@ -192,6 +193,8 @@ void core_wave_kernel(CoreStepArgs a) {
     constexpr int AL = 64 / EW;
     const int H = HT ? HT : a.H, W = WT ? WT : a.W;
     const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
+    const int DW = W + 4, TS = wave_tile_floats(H, W);   // DFF tile row stride / floats per env
+    constexpr int kDWS = 2;                    // DW - PW
     const int A = a.A;
     const int lane = (int)(threadIdx.x & 63);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform (SGPR)
@@ -200,7 +203,7 @@ void core_wave_kernel(CoreStepArgs a) {
     const bool do_reset = !MT && a.auto_reset;
 
     // ---- LDS carve-up: uniform bases, per-lane views ------------------------------
-    const WaveCarve cv = wave_carve(PHW, AL, EW, a.F, MT, do_reset);
+    const WaveCarve cv = wave_carve(PHW, TS, AL, EW, a.F, MT, do_reset);
     uint8_t* pmap = smem;
     float* psff = reinterpret_cast<float*>(smem + align16((size_t)PHW));
     uint16_t* pfree = reinterpret_cast<uint16_t*>(smem + align16((size_t)PHW) + align16((size_t)PHW * 4));
@@ -213,23 +216,23 @@ void core_wave_kernel(CoreStepArgs a) {
     uint16_t* spos = reinterpret_cast<uint16_t*>(wbase + cv.spos);
     int* scnt = reinterpret_cast<int*>(wbase + cv.spos + 128);
     GT* gk = grid + sub * PHW;
-    float* dk = tile + sub * PHW;
+    float* dk = tile + sub * TS;
     uint16_t* rq = sreq + sub * AL;
     uint16_t* nx = snxt + sub * AL;
 
     // This lane's two float4 DFF slots (cells 4q..4q+3 of the group, q = lane,
-    // lane + 64): padded tile offsets, fixed for every group.  W % 4 == 0, so a
-    // slot never straddles a row (checked on the host).
+    // lane + 64): 16-B aligned tile offsets, fixed for every group.  W % 4 == 0, so
+    // a slot never straddles a row (checked on the host).
     int tb0 = -1, tb1 = -1;
     {
         const int c0 = 4 * lane, c1 = 4 * (lane + 64);
         if (c0 < EW * HW) {
             const int s = c0 / HW, cell = c0 - s * HW, x = cell / W, y = cell - (cell / W) * W;
-            tb0 = s * PHW + (x + 1) * PW + y + 1;
+            tb0 = s * TS + 4 + (x + 1) * DW + y;
         }
         if (c1 < EW * HW) {
             const int s = c1 / HW, cell = c1 - s * HW, x = cell / W, y = cell - (cell / W) * W;
-            tb1 = s * PHW + (x + 1) * PW + y + 1;
+            tb1 = s * TS + 4 + (x + 1) * DW + y;
         }
     }
 
@@ -261,14 +264,8 @@ void core_wave_kernel(CoreStepArgs a) {
             pf.pos = (5 + (al >= 10) + (al >= 20)) * W + 1 + (al % 10);
             if (FFM_ABLATE & 1024) asm volatile("" ::"v"(pf0.d0.x), "v"(pf0.d1.x), "v"(pf0.pos), "v"(pf0.cnt));
         }
-        if (tb0 >= 0) {
-            float* p = tile + tb0;
-            p[0] = pf.d0.x; p[1] = pf.d0.y; p[2] = pf.d0.z; p[3] = pf.d0.w;
-        }
-        if (tb1 >= 0) {
-            float* p = tile + tb1;
-            p[0] = pf.d1.x; p[1] = pf.d1.y; p[2] = pf.d1.z; p[3] = pf.d1.w;
-        }
+        if (tb0 >= 0) *reinterpret_cast<float4*>(tile + tb0) = pf.d0;   // ds_write_b128
+        if (tb1 >= 0) *reinterpret_cast<float4*>(tile + tb1) = pf.d1;
         spos[lane] = (uint16_t)pf.pos;
         if (al == 0) scnt[sub] = pf.cnt;
     };
@@ -283,7 +280,7 @@ void core_wave_kernel(CoreStepArgs a) {
             psff[i] = reinterpret_cast<const float*>(a.psff)[i];
         }
         for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
-        for (int i = lane; i < EW * PHW; i += 64) tile[i] = 0.0f;
+        for (int i = lane; i < EW * TS; i += 64) tile[i] = 0.0f;
         __syncthreads();
         for (int i = lane; i < EW * PHW; i += 64) grid[i] = pmap[i - (i / PHW) * PHW];
         wave_sync();
@@ -310,11 +307,12 @@ void core_wave_kernel(CoreStepArgs a) {
         const uint32_t genv = (uint32_t)(a.env_base + e0 + sub);
 
         const int cnt = scnt[sub];
-        int pp = -1;
+        int pp = -1, dd0 = 0;   // padded grid cell; DFF tile index = grid index + dd0 (+ 2 per row below)
         if (env_ok && al < A && al < cnt) {
             const int c = spos[lane];
             const int x = c / W, y = c - (c / W) * W;
             pp = (x + 1) * PW + y + 1;
+            dd0 = (x + 1) * kDWS + 3;
         }
         c_steps += (al == 0 && env_ok) ? cnt : 0;
         const bool live = pp >= 0;
@@ -331,16 +329,16 @@ void core_wave_kernel(CoreStepArgs a) {
         uint32_t r = kNoReq;
         if (live && !(FFM_ABLATE & 1)) {
             if (MT) {
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, DrawPending{});
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawPending{});
             } else if (FFM_ABLATE & 256) {   // diagnostic: cheap hash instead of Philox
                 const uint32_t hsh = (genv * 2654435761u) ^ ((uint32_t)al * 40503u) ^ (a.t * 97u);
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64,
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
                                           DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)});
             } else {
                 const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
                 // words 2, 3 feed the friction draw if this agent owns a contested target
                 reinterpret_cast<uint2*>(wbase + cv.u)[lane] = make_uint2(pb.z, pb.w);
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64,
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
                                           DrawFixed{u53(pb.x, pb.y)});
             }
         }
@@ -358,7 +356,7 @@ void core_wave_kernel(CoreStepArgs a) {
             }
             wave_sync();
             if (r == kPending)
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]});
+                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]});
         }
         STAMP(2);
         if (live) rq[al] = (uint16_t)r;
@@ -399,7 +397,7 @@ void core_wave_kernel(CoreStepArgs a) {
             }
             if (live && r != kNoReq && !(FFM_ABLATE & 2)) {
                 if ((int)r == pp) {
-                    dk[pp] += 1.0f;                                                       // :91-93 (stay)
+                    dk[pp + dd0] += 1.0f;                                                 // :91-93 (stay)
                 } else if (owner) {
                     int ws = -1;
                     if (m == 1) {
@@ -425,7 +423,7 @@ void core_wave_kernel(CoreStepArgs a) {
                                 wi = who[s];
                             }
                         nx[wi] = (uint16_t)r;
-                        dk[wcell] += 1.0f;                                                // :97-98
+                        dk[wcell + (wcell / PW) * kDWS + 3] += 1.0f;                      // :97-98
                     }
                 }
             }
@@ -443,72 +441,57 @@ void core_wave_kernel(CoreStepArgs a) {
         c_exits += (al == 0 && env_ok) ? cnt - newcnt : 0;
         if (live) gk[pp] = 0;   // unmark: agents only ever stand on free cells
 
-        // ---- auto-reset of an env this step emptied (Philox placement keyed by t) ---
-        // Done at the END of the step, when the decide/resolve registers are dead.
+        // An env this step emptied is re-placed at the end of the group (below).
         const bool rs = do_reset && env_ok && newcnt == 0 && !(FFM_ABLATE & 32);
-        if (do_reset) {
-#pragma unroll
-            for (int s = 0; s < EW; s++) {
-                if (__ballot(rs && sub == s) == 0ull) continue;
-                const uint32_t ge = (uint32_t)(a.env_base + e0 + s);
-                if (FFM_ABLATE & 64) {   // diagnostic: trivial placement (first N free cells)
-                    if (lane < a.N) snxt[s * AL + lane] = pfree[lane];
-                    wave_sync();
-                } else {
-                    wave_reset_env(a, ge, keys, pfree, snxt + s * AL, lane);
-                }
-            }
-        }
         c_resets += (al == 0 && rs) ? 1 : 0;
         STAMP(5);
 
         // ---- update_dff (model/ffm_core.py:106-117), float4 per lane ------------------
+        // Pass 1: B = c0 * D in place (:109; halo stays 0).  Pass 2: per slot, three
+        // aligned ds_read_b128 (rows x-1, x, x+1) and the scalars left/right of them.
         float b0[4], b1[4];
-        if (tb0 >= 0) {                          // pass 1: B = c0 * D in place (halo stays 0)
-            float* p = tile + tb0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) { b0[j] = a.c0 * p[j]; p[j] = b0[j]; }        // :109
-        }
-        if (tb1 >= 0) {
-            float* p = tile + tb1;
-#pragma unroll
-            for (int j = 0; j < 4; j++) { b1[j] = a.c0 * p[j]; p[j] = b1[j]; }
-        }
+        auto scale = [&](int tb, float (&bq)[4]) {
+            float4* p = reinterpret_cast<float4*>(tile + tb);
+            const float4 q = *p;
+            bq[0] = a.c0 * q.x; bq[1] = a.c0 * q.y; bq[2] = a.c0 * q.z; bq[3] = a.c0 * q.w;
+            *p = make_float4(bq[0], bq[1], bq[2], bq[3]);
+        };
+        if (tb0 >= 0) scale(tb0, b0);
+        if (tb1 >= 0) scale(tb1, b1);
         wave_sync();
+        auto stencil = [&](int tb, const float (&bq)[4], float (&o)[4]) {
+            const float* p = tile + tb;
+            float v[3][6];   // rows dx = -1..1, columns -1..4 of the slot (B values)
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx += 2) {
+                const float4 q = *reinterpret_cast<const float4*>(p + dx * DW);
+                v[dx + 1][1] = q.x; v[dx + 1][2] = q.y; v[dx + 1][3] = q.z; v[dx + 1][4] = q.w;
+            }
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx++) {
+                v[dx + 1][0] = p[dx * DW - 1];
+                v[dx + 1][5] = p[dx * DW + 4];
+            }
+            v[1][1] = bq[0]; v[1][2] = bq[1]; v[1][3] = bq[2]; v[1][4] = bq[3];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float acc = bq[j];
+#pragma unroll
+                for (int k = 0; k < NB; k++) {
+                    if (FFM_ABLATE & 4) break;
+                    const float t = a.c1 * v[1 + nb_dx<NB>(k)][j + 1 + nb_dy<NB>(k)];     // :113
+                    acc = acc + t;
+                }
+                o[j] = acc < 1e-4f ? 0.0f : acc;                                         // :116-117
+            }
+        };
         float o0[4], o1[4];
-        if (tb0 >= 0) {
-            const float* p = tile + tb0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                float acc = b0[j];
-#pragma unroll
-                for (int k = 0; k < NB; k++) {
-                    if (FFM_ABLATE & 4) break;
-                    const float t = a.c1 * p[j + nb_dx<NB>(k) * PW + nb_dy<NB>(k)];      // :113
-                    acc = acc + t;
-                }
-                o0[j] = acc < 1e-4f ? 0.0f : acc;                                        // :116-117
-            }
-        }
-        if (tb1 >= 0) {
-            const float* p = tile + tb1;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                float acc = b1[j];
-#pragma unroll
-                for (int k = 0; k < NB; k++) {
-                    if (FFM_ABLATE & 4) break;
-                    const float t = a.c1 * p[j + nb_dx<NB>(k) * PW + nb_dy<NB>(k)];
-                    acc = acc + t;
-                }
-                o1[j] = acc < 1e-4f ? 0.0f : acc;
-            }
-        }
+        if (tb0 >= 0) stencil(tb0, b0, o0);
+        if (tb1 >= 0) stencil(tb1, b1, o1);
         wave_sync();
         STAMP(6);
 
         // ---- stage the next group (its loads were issued at the top), then store ------
-        const int rst_pos = rs && al < a.N ? (int)nx[al] : -1;   // placement of a reset env
         const unsigned long long rsm = __ballot(rs);
         stage(nxtpf);
         if (!(FFM_ABLATE & 16)) {
@@ -517,7 +500,6 @@ void core_wave_kernel(CoreStepArgs a) {
             float4* gd = reinterpret_cast<float4*>(a.dff + e0 * HW);
             const int n4 = nenv * HW / 4;
             if (keep) gp[sub * A + newidx] = (uint16_t)unpad(nxt, PW);
-            if (rst_pos >= 0) gp[sub * A + al] = (uint16_t)unpad(rst_pos, PW);
             if (al == 0 && env_ok) {
                 gc[sub] = rs ? a.N : newcnt;
                 if (rs && a.episodes) a.episodes[e0 + sub] += 1;
@@ -530,6 +512,14 @@ void core_wave_kernel(CoreStepArgs a) {
                 gd[lane] = z0 ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(o0[0], o0[1], o0[2], o0[3]);
             if (tb1 >= 0 && lane + 64 < n4)
                 gd[lane + 64] = z1 ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(o1[0], o1[1], o1[2], o1[3]);
+        }
+        // ---- auto-reset: Philox placement keyed by t, stored straight
+        // to the env's positions.  Rare; placed last, where little else is live.
+        if (rsm) {   // wave-uniform
+#pragma unroll
+            for (int s = 0; s < EW; s++)
+                if ((rsm >> (s * AL)) & 1ull)
+                    wave_reset_env(a, (uint32_t)(a.env_base + e0 + s), keys, pfree, a.pos + (e0 + s) * A, lane);
         }
         wave_sync();
         STAMP(7);
@@ -682,11 +672,11 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         const int pp = spos[it];
         uint32_t r;
         if (MT) {
-            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, a.kS32, a.kD32, a.kS64,
+            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64,
                                     DrawPending{});
         } else {
             const DrawPhilox d{a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i};
-            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, a.kS32, a.kD32, a.kS64, d);
+            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64, d);
         }
         sreq[it] = (uint16_t)r;
     }
@@ -704,7 +694,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         for (int it = tid; it < nA; it += BS) {
             const int k = it / A, i = it - k * A;
             if (i >= scnt[k] || sreq[it] != kPending) continue;
-            sreq[it] = (uint16_t)decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW,
+            sreq[it] = (uint16_t)decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
                                                      a.kS32, a.kD32, a.kS64, DrawFixed{su[it]});
         }
         __syncthreads();
@@ -836,6 +826,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             for (int i = tid; i < C; i += BS) {
                 const unsigned long long ki = keys[i];
                 int rank = 0;
+#pragma unroll 4
                 for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
                 if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[(int)(ki & 0xFFFFu)], PW);
             }
@@ -886,14 +877,11 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
 __global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
-    uint16_t* slot = reinterpret_cast<uint16_t*>(smem + align16((size_t)a.F * 8));
-    uint16_t* fl = slot + align16((size_t)(a.N > 0 ? a.N : 1) * 2) / 2;
+    uint16_t* fl = reinterpret_cast<uint16_t*>(smem + align16((size_t)a.F * 8));
     const long long e = blockIdx.x;
-    const int PW = a.W + 2;
     for (int i = threadIdx.x; i < a.F; i += 64) fl[i] = a.free_padded[i];
     wave_sync();
-    wave_reset_env(a, (uint32_t)(a.env_base + e), keys, fl, slot, threadIdx.x);
-    for (int s = threadIdx.x; s < a.N; s += 64) a.pos[e * a.A + s] = (uint16_t)unpad(slot[s], PW);
+    wave_reset_env(a, (uint32_t)(a.env_base + e), keys, fl, a.pos + e * a.A, threadIdx.x);
     if (threadIdx.x == 0) a.cnt[e] = a.N;
 }
 

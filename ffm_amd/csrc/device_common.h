@@ -48,6 +48,9 @@ __device__ __forceinline__ int bit_length(uint32_t n) { return n ? 32 - __builti
 
 // ---- Philox4x32-10 ----------------------------------------------------------
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
+    // Opaque key: keeps the compiler from hoisting the 20-word key schedule out of
+    // the step loop into SGPRs (it spills them); 2 s_add per round are cheaper.
+    asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int r = 0; r < 10; r++) {
         // one v_mad_u64_u32 per product: ~30% cheaper than mul_lo + mul_hi on gfx950
