@@ -81,18 +81,18 @@ __device__ __forceinline__ bool cdf_gt(double ck, double last, double inv_last, 
 // idx = searchsorted(cdf, u, side="right").
 template <int NB>
 __device__ __forceinline__ uint32_t exact_pick(const double (&cdf)[NB + 1], double last, const bool (&v)[NB + 1],
-                                               const int (&cell)[NB + 1], double u) {
+                                               double u) {
     const double inv = 1.0 / last;
-    uint32_t target = (uint32_t)cell[NB];
+    uint32_t slot = NB;
     bool found = false;
 #pragma unroll
     for (int k = 0; k < NB; k++) {
         if (v[k] && !found && cdf_gt(cdf[k], last, inv, u)) {
             found = true;
-            target = (uint32_t)cell[k];
+            slot = (uint32_t)k;
         }
     }
-    return target;  // the stay slot has cdf == 1 > u
+    return slot;  // the stay slot has cdf == 1 > u
 }
 
 // Fast path of the choice.  Probabilities from the hardware exp2 (v_exp_f32)
@@ -133,7 +133,8 @@ __device__ __forceinline__ int fast_choice(const float (&x)[NB + 1], const bool 
 }
 
 // decide() for one agent at padded cell pp: model/ffm_core.py:41-88.
-// Returns the padded target cell, kNoReq, or kPending (draw needed, MT pass 1).
+// Returns the chosen slot (neighbour index, NB = stay), kNoReq, or kPending (draw
+// needed, MT pass 1); slot_cell() turns a slot into the padded target cell.
 // Every slot is evaluated unconditionally (all neighbour cells exist in the
 // padded grid), so the LDS loads issue together and no lane diverges except
 // into the rare exact path.
@@ -158,12 +159,12 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
     dcell[NB] = pp + dd0;
     v[NB] = true;
     int nvalid = 0;
-    int exit_cell = -1;
+    int exit_slot = -1;
 #pragma unroll
     for (int s = NB - 1; s >= 0; s--) {
         v[s] = g[s] == 0u || g[s] == 3u;                             // :52-60
         nvalid += v[s] ? 1 : 0;
-        exit_cell = g[s] == 3u ? cell[s] : exit_cell;                // :66-72 first exit
+        exit_slot = g[s] == 3u ? s : exit_slot;                      // :66-72 first exit
     }
     const int nc = nvalid + 1;
 
@@ -183,13 +184,10 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
         for (int k = 0; k <= NB; k++) xs[k] = v[k] ? sc[k] - mx : -__builtin_inff();   // :80 argument, exact
         const double u = draw.get();                                 // :84
         if (nvalid == 0) return kNoReq;                              // :63
-        if (exit_cell >= 0) return (uint32_t)exit_cell;
+        if (exit_slot >= 0) return (uint32_t)exit_slot;
         if (u < 0.0) return kPending;
         const int fs = fast_choice<NB>(xs, v, u);
-        uint32_t target = (uint32_t)cell[NB];
-#pragma unroll
-        for (int k = 0; k < NB; k++) target = k == fs ? (uint32_t)cell[k] : target;
-        if (fs >= 0) return target;
+        if (fs >= 0) return (uint32_t)fs;
         // u is within the margin of a boundary: the exact NumPy arithmetic decides.
         float e[NB + 1];
 #pragma unroll
@@ -202,10 +200,10 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
             if (v[k]) acc += (double)(e[k] / sum);                   // :83, then cumsum in choice
             cdf[k] = acc;
         }
-        return exact_pick<NB>(cdf, acc, v, cell, u);
+        return exact_pick<NB>(cdf, acc, v, u);
     } else {
         if (nvalid == 0) return kNoReq;
-        if (exit_cell >= 0) return (uint32_t)exit_cell;
+        if (exit_slot >= 0) return (uint32_t)exit_slot;
         double sc[NB + 1], e[NB + 1];
         double mx = -__builtin_inf();
 #pragma unroll
@@ -227,8 +225,17 @@ __device__ __forceinline__ uint32_t decide(int pp, int PW, const GT* grid, const
         }
         const double u = draw.get();                                 // :84
         if (u < 0.0) return kPending;
-        return exact_pick<NB>(cdf, acc, v, cell, u);
+        return exact_pick<NB>(cdf, acc, v, u);
     }
+}
+
+// Padded cell of slot `slot` around pp (kNoReq / kPending pass through).
+template <int NB>
+__device__ __forceinline__ uint32_t slot_cell(uint32_t slot, int pp, int PW) {
+    int off = 0;
+#pragma unroll
+    for (int s = 0; s < NB; s++) off = slot == (uint32_t)s ? nb_dx<NB>(s) * PW + nb_dy<NB>(s) : off;
+    return slot <= (uint32_t)NB ? (uint32_t)(pp + off) : slot;
 }
 
 // The requesters of target r (padded): agents adjacent to r whose request is r.
@@ -301,6 +308,11 @@ __device__ __forceinline__ uint32_t reset_threshold(int N, int F) {
 __device__ __forceinline__ int unpad(int pp, int PW) {
     const int x = pp / PW - 1, y = pp - (pp / PW) * PW - 1;
     return x * (PW - 2) + y;
+}
+
+// Number of set bits of `m` in lanes below this one (v_mbcnt; no per-lane mask).
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __device__ __forceinline__ void wave_sync() {

@@ -63,6 +63,9 @@
 #ifndef FFM_WAVES_PER_EU
 #define FFM_WAVES_PER_EU 0   // minimum waves/SIMD requested for the wave kernel (0 = compiler's choice)
 #endif
+#ifndef FFM_PREFETCH_LATE
+#define FFM_PREFETCH_LATE 1   // 0: next group's loads at the top; 1: after decide; 2: after resolve
+#endif
 #ifndef FFM_LDS_PAD
 #define FFM_LDS_PAD 0  // diagnostic builds only: extra dynamic LDS per block to pin occupancy
 #endif
@@ -94,8 +97,8 @@ __host__ __device__ inline WaveCarve wave_carve(int PHW, int TS, int AL, int EW,
     c.nxt = o;  o += align16((size_t)EW * AL * 2);
     c.u = o;    o += align16((size_t)EW * AL * 8);        // MT: f64 draws; Philox: friction words
     c.flag = o; o += mt ? align16((size_t)EW * AL * 2) : 0;
-    c.keys = o; o += reset ? align16((size_t)F * 8) : 0;
     c.spos = o; o += align16(64 * 2 + 2 * 4);
+    c.keys = o; o += reset ? align16((size_t)F * 8) : 0;   // last: the only runtime-sized region
     c.per_wave = o;
     return c;
 }
@@ -156,7 +159,7 @@ __device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned lo
                 cand = k <= T;
             }
             const unsigned long long m = __ballot(cand);
-            if (cand) keys[C + __popcll(m & ((1ull << lane) - 1ull))] = ((unsigned long long)k << 32) | (unsigned)j;
+            if (cand) keys[C + lanes_below(m)] = ((unsigned long long)k << 32) | (unsigned)j;
             C += __popcll(m);
         }
         if (C >= N || T == 0xFFFFFFFFu) break;
@@ -223,9 +226,14 @@ void core_wave_kernel(CoreStepArgs a) {
     // This lane's two float4 DFF slots (cells 4q..4q+3 of the group, q = lane,
     // lane + 64): 16-B aligned tile offsets, fixed for every group.  W % 4 == 0, so
     // a slot never straddles a row (checked on the host).
+    // Recomputed where used (from an opaque copy of the lane id) rather than kept
+    // live across the step loop: two VGPRs fewer at the decide-phase peak.
     int tb0 = -1, tb1 = -1;
-    {
-        const int c0 = 4 * lane, c1 = 4 * (lane + 64);
+    auto slots = [&]() {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int c0 = 4 * ln, c1 = 4 * (ln + 64);
+        tb0 = tb1 = -1;
         if (c0 < EW * HW) {
             const int s = c0 / HW, cell = c0 - s * HW, x = cell / W, y = cell - (cell / W) * W;
             tb0 = s * TS + 4 + (x + 1) * DW + y;
@@ -234,7 +242,8 @@ void core_wave_kernel(CoreStepArgs a) {
             const int s = c1 / HW, cell = c1 - s * HW, x = cell / W, y = cell - (cell / W) * W;
             tb1 = s * TS + 4 + (x + 1) * DW + y;
         }
-    }
+    };
+    slots();
 
     const int ngroups = (int)((a.E + EW - 1) / EW);
     const int wstride = (int)gridDim.x * 4;
@@ -289,17 +298,25 @@ void core_wave_kernel(CoreStepArgs a) {
     }
 
     if (FFM_ABLATE & 4096) return;   // diagnostic: prologue only
-    int c_steps = 0, c_exits = 0, c_resets = 0;   // per lane; only al == 0 lanes count
+    unsigned c_steps = 0, c_exits = 0, c_resets = 0;   // wave-uniform (SGPRs)
 #if FFM_STAMPS
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tlast = __builtin_amdgcn_s_memtime();
 #endif
 
     for (; g < ngroups; g += wstride) {
+        // Opaque group index: stops loop strength reduction from turning every
+        // per-lane global address into a 64-bit induction variable (VGPR pairs).
+        asm volatile("" : "+s"(g));
+        // Next group's HBM loads: issued after decide (FFM_PREFETCH_LATE), so that the
+        // prefetch registers are not live across the decide phase (the VGPR peak).
         WavePrefetch nxtpf;
-        prefetch(((FFM_ABLATE & 8) || ((FFM_ABLATE & 512) && !(FFM_ABLATE & 1024))) ? -1
-                                                                              : (g + wstride < ngroups ? g + wstride : -1),
-                 nxtpf);
+        auto issue_prefetch = [&]() {
+            prefetch(((FFM_ABLATE & 8) || ((FFM_ABLATE & 512) && !(FFM_ABLATE & 1024))) ? -1
+                                                                                  : (g + wstride < ngroups ? g + wstride : -1),
+                     nxtpf);
+        };
+        if (!FFM_PREFETCH_LATE) issue_prefetch();
 
         const long long e0 = (long long)g * EW;
         const int nenv = (int)((a.E - e0) < EW ? (a.E - e0) : EW);
@@ -314,7 +331,9 @@ void core_wave_kernel(CoreStepArgs a) {
             pp = (x + 1) * PW + y + 1;
             dd0 = (x + 1) * kDWS + 3;
         }
-        c_steps += (al == 0 && env_ok) ? cnt : 0;
+        // agent-steps of the group: counts at step start of its (1 or 2) envs
+        const unsigned gcnt = (unsigned)__builtin_amdgcn_readfirstlane(scnt[0] + (EW == 2 && nenv > 1 ? scnt[1] : 0));
+        c_steps += gcnt;
         const bool live = pp >= 0;
         STAMP(0);
 
@@ -329,17 +348,17 @@ void core_wave_kernel(CoreStepArgs a) {
         uint32_t r = kNoReq;
         if (live && !(FFM_ABLATE & 1)) {
             if (MT) {
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawPending{});
+                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawPending{}), pp, PW);
             } else if (FFM_ABLATE & 256) {   // diagnostic: cheap hash instead of Philox
                 const uint32_t hsh = (genv * 2654435761u) ^ ((uint32_t)al * 40503u) ^ (a.t * 97u);
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
-                                          DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)});
+                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
+                                          DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)}), pp, PW);
             } else {
                 const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
                 // words 2, 3 feed the friction draw if this agent owns a contested target
                 reinterpret_cast<uint2*>(wbase + cv.u)[lane] = make_uint2(pb.z, pb.w);
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
-                                          DrawFixed{u53(pb.x, pb.y)});
+                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
+                                          DrawFixed{u53(pb.x, pb.y)}), pp, PW);
             }
         }
         if (MT) {
@@ -356,12 +375,14 @@ void core_wave_kernel(CoreStepArgs a) {
             }
             wave_sync();
             if (r == kPending)
-                r = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]});
+                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]}), pp, PW);
         }
         STAMP(2);
         if (live) rq[al] = (uint16_t)r;
         wave_sync();
         STAMP(3);
+
+        if (FFM_PREFETCH_LATE == 1) issue_prefetch();
 
         // ---- resolve (model/ffm_core.py:90-98) ---------------------------------------
         {
@@ -431,24 +452,30 @@ void core_wave_kernel(CoreStepArgs a) {
         wave_sync();
         STAMP(4);
 
+        if (FFM_PREFETCH_LATE == 2) issue_prefetch();
+
         // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) ---------
         const int nxt = live ? (int)nx[al] : 0;
         const bool keep = live && pmap[nxt] != 3;
         const unsigned long long km = __ballot(keep);
         const unsigned long long segm = AL == 64 ? ~0ull : (((1ull << AL) - 1ull) << (sub * AL));
-        const int newidx = __popcll(km & segm & ((1ull << lane) - 1ull));
+        const int newidx = lanes_below(km & segm);
         const int newcnt = __popcll(km & segm);
-        c_exits += (al == 0 && env_ok) ? cnt - newcnt : 0;
+        c_exits += gcnt - (unsigned)__popcll(km);
         if (live) gk[pp] = 0;   // unmark: agents only ever stand on free cells
 
         // An env this step emptied is re-placed at the end of the group (below).
         const bool rs = do_reset && env_ok && newcnt == 0 && !(FFM_ABLATE & 32);
-        c_resets += (al == 0 && rs) ? 1 : 0;
+        {
+            const unsigned long long rb = __ballot(rs);
+            c_resets += (unsigned)((rb & 1ull) + (EW == 2 ? ((rb >> AL) & 1ull) : 0ull));
+        }
         STAMP(5);
 
         // ---- update_dff (model/ffm_core.py:106-117), float4 per lane ------------------
         // Pass 1: B = c0 * D in place (:109; halo stays 0).  Pass 2: per slot, three
         // aligned ds_read_b128 (rows x-1, x, x+1) and the scalars left/right of them.
+        slots();
         float b0[4], b1[4];
         auto scale = [&](int tb, float (&bq)[4]) {
             float4* p = reinterpret_cast<float4*>(tile + tb);
@@ -526,12 +553,6 @@ void core_wave_kernel(CoreStepArgs a) {
     }
 
     // ---- counters: one atomic per wave ------------------------------------------------
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        c_steps += __shfl_xor(c_steps, off);
-        c_exits += __shfl_xor(c_exits, off);
-        c_resets += __shfl_xor(c_resets, off);
-    }
     if (lane == 0) {
         // Counters live in one 32-B slot per wave: no two waves ever add to the
         // same address (a single contended word saturates near 100 adds/us).
@@ -583,7 +604,7 @@ template <int BS>
 __device__ __forceinline__ int block_excl_scan(bool flag, int* swsum, int& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long mask = __ballot(flag);
-    const int lp = __popcll(mask & ((1ull << lane) - 1ull));
+    const int lp = lanes_below(mask);
     if (lane == 0) swsum[wave] = __popcll(mask);
     __syncthreads();
     int wp = 0, tot = 0;
@@ -672,11 +693,11 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         const int pp = spos[it];
         uint32_t r;
         if (MT) {
-            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64,
-                                    DrawPending{});
+            r = slot_cell<NB>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64,
+                                    DrawPending{}), pp, PW);
         } else {
             const DrawPhilox d{a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i};
-            r = decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64, d);
+            r = slot_cell<NB>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64, d), pp, PW);
         }
         sreq[it] = (uint16_t)r;
     }
@@ -694,8 +715,8 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         for (int it = tid; it < nA; it += BS) {
             const int k = it / A, i = it - k * A;
             if (i >= scnt[k] || sreq[it] != kPending) continue;
-            sreq[it] = (uint16_t)decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
-                                                     a.kS32, a.kD32, a.kS64, DrawFixed{su[it]});
+            sreq[it] = (uint16_t)slot_cell<NB>(decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
+                                                     a.kS32, a.kD32, a.kS64, DrawFixed{su[it]}), spos[it], PW);
         }
         __syncthreads();
 
