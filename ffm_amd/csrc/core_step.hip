@@ -226,14 +226,9 @@ void core_wave_kernel(CoreStepArgs a) {
     // This lane's two float4 DFF slots (cells 4q..4q+3 of the group, q = lane,
     // lane + 64): 16-B aligned tile offsets, fixed for every group.  W % 4 == 0, so
     // a slot never straddles a row (checked on the host).
-    // Recomputed where used (from an opaque copy of the lane id) rather than kept
-    // live across the step loop: two VGPRs fewer at the decide-phase peak.
     int tb0 = -1, tb1 = -1;
-    auto slots = [&]() {
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int c0 = 4 * ln, c1 = 4 * (ln + 64);
-        tb0 = tb1 = -1;
+    {
+        const int c0 = 4 * lane, c1 = 4 * (lane + 64);
         if (c0 < EW * HW) {
             const int s = c0 / HW, cell = c0 - s * HW, x = cell / W, y = cell - (cell / W) * W;
             tb0 = s * TS + 4 + (x + 1) * DW + y;
@@ -242,8 +237,7 @@ void core_wave_kernel(CoreStepArgs a) {
             const int s = c1 / HW, cell = c1 - s * HW, x = cell / W, y = cell - (cell / W) * W;
             tb1 = s * TS + 4 + (x + 1) * DW + y;
         }
-    };
-    slots();
+    }
 
     const int ngroups = (int)((a.E + EW - 1) / EW);
     const int wstride = (int)gridDim.x * 4;
@@ -305,9 +299,6 @@ void core_wave_kernel(CoreStepArgs a) {
 #endif
 
     for (; g < ngroups; g += wstride) {
-        // Opaque group index: stops loop strength reduction from turning every
-        // per-lane global address into a 64-bit induction variable (VGPR pairs).
-        asm volatile("" : "+s"(g));
         // Next group's HBM loads: issued after decide (FFM_PREFETCH_LATE), so that the
         // prefetch registers are not live across the decide phase (the VGPR peak).
         WavePrefetch nxtpf;
@@ -475,7 +466,6 @@ void core_wave_kernel(CoreStepArgs a) {
         // ---- update_dff (model/ffm_core.py:106-117), float4 per lane ------------------
         // Pass 1: B = c0 * D in place (:109; halo stays 0).  Pass 2: per slot, three
         // aligned ds_read_b128 (rows x-1, x, x+1) and the scalars left/right of them.
-        slots();
         float b0[4], b1[4];
         auto scale = [&](int tb, float (&bq)[4]) {
             float4* p = reinterpret_cast<float4*>(tile + tb);
