@@ -116,20 +116,22 @@ __device__ __forceinline__ int fast_choice(const float (&x)[NB + 1], const bool 
     for (int k = 0; k <= NB; k++) {
         const float e = __builtin_amdgcn_exp2f(x[k] * 1.44269504088896341f);
         acc += v[k] ? e : 0.0f;
-        cum[k] = acc;
+        cum[k] = v[k] ? acc : -1.0f;   // invalid slots never selected
     }
     const float t = (float)u * acc;
     const float d = kFastMargin * acc;
-    int slot = -1;
-    bool done = false;
+    // The valid cum values are non-decreasing, so the first slot with cum >= t - d
+    // is the only candidate: it is the answer when cum > t + d, else u is too
+    // close to a boundary (-1).  Selects from the top down: VALU only.
+    int slot = NB;
+    float cs = cum[NB];
 #pragma unroll
-    for (int k = 0; k <= NB; k++) {
-        const bool gt = v[k] && !done && cum[k] > t + d;
-        const bool close = v[k] && !done && !gt && cum[k] >= t - d;
-        slot = gt ? k : slot;
-        done = done || gt || close;
+    for (int k = NB - 1; k >= 0; k--) {
+        const bool ge = cum[k] >= t - d;
+        slot = ge ? k : slot;
+        cs = ge ? cum[k] : cs;
     }
-    return slot;
+    return cs > t + d ? slot : -1;
 }
 
 // decide() for one agent at padded cell pp: model/ffm_core.py:41-88.

@@ -52,6 +52,13 @@
         st[k] += t_ - tlast;                                                               \
         tlast = t_;                                                                        \
     } while (0)
+#elif defined(FFM_MARKS)   // diagnostic: phase markers in the ISA (tools/phase_count.py)
+#define STAMP(k)                                   \
+    do {                                           \
+        __builtin_amdgcn_sched_barrier(0);         \
+        asm volatile("; @PHASE " #k ::: "memory"); \
+        __builtin_amdgcn_sched_barrier(0);         \
+    } while (0)
 #else
 #define STAMP(k) \
     do {         \
