@@ -264,6 +264,29 @@ __device__ __forceinline__ int requesters(int r, int PW, const GT* grid, const u
     return m;
 }
 
+// Direction-coded occupancy grid (u16, wave and pack kernels): 0 free, 2
+// blocked, 3 exit; an agent cell holds kAgent | index | slot << 8, where slot is
+// the neighbour index its decide chose (NB = stay, kNoDir = no request).
+struct DirCodes {
+    static constexpr uint32_t kAgent = 0x80u, kIdx = 0x7Fu, kNoDir = 0xFu;
+};
+
+// Requesters of target r from a direction-coded grid: the agents on r's
+// neighbour cells whose chosen slot points at r -- one LDS round trip.
+template <int NB>
+__device__ __forceinline__ int requesters_dir(int r, int PW, const uint16_t* grid, uint16_t (&who)[NB],
+                                              bool (&is)[NB]) {
+    int m = 0;
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        const uint32_t c = grid[r - nb_dx<NB>(s) * PW - nb_dy<NB>(s)];
+        is[s] = (c & DirCodes::kAgent) != 0u && ((c >> 8) & 0xFu) == (uint32_t)s;
+        who[s] = (uint16_t)(c & DirCodes::kIdx);
+        m += is[s] ? 1 : 0;
+    }
+    return m;
+}
+
 // Slot (neighbour index) of the k-th smallest requester.
 template <int NB>
 __device__ __forceinline__ int kth_slot(const uint16_t (&who)[NB], const bool (&is)[NB], int k) {

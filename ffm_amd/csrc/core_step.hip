@@ -38,6 +38,7 @@
 
 #include "core_common.h"
 #include "kernels.h"
+#include "wave_reset.h"
 
 #ifndef FFM_STAMPS
 #define FFM_STAMPS 0   // diagnostic builds only: per-phase s_memtime cycle sums per wave
@@ -98,7 +99,7 @@ __host__ __device__ inline int wave_tile_floats(int H, int W) { return 4 + (H + 
 __host__ __device__ inline WaveCarve wave_carve(int PHW, int TS, int AL, int EW, int F, bool mt, bool reset) {
     WaveCarve c;
     size_t o = 0;
-    c.grid = o; o += align16((size_t)EW * PHW);            // u8 codes
+    c.grid = o; o += align16((size_t)EW * PHW * 2);        // u16 direction-coded cells
     c.dff = o;  o += align16((size_t)EW * TS * 4);         // f32 tiles, zero halo
     c.req = o;  o += align16((size_t)EW * AL * 2);
     c.nxt = o;  o += align16((size_t)EW * AL * 2);
@@ -122,66 +123,6 @@ size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int
            (size_t)waves * wave_carve(PHW, wave_tile_floats(H, W), 64 / EW, EW, F, mt, reset).per_wave;
 }
 
-__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((unsigned long long)hi << 32) | lo;
-}
-
-// Philox placement of one env, stored straight to its global positions gpos[0..N)
-// (unpadded cell indices): all 64 lanes.
-// fl = padded free-cell list (LDS).  F <= 128: the (key, j) pairs go to LDS and
-// each lane ranks its two by broadcast reads -- few registers, because this
-// rarely-taken branch sits inside the step loop and would otherwise set the
-// kernel's VGPR peak.  Larger F: threshold the keys into an LDS candidate list
-// first (about 2N + 16 survive).
-__device__ void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsigned long long* keys, const uint16_t* fl,
-                               uint16_t* gpos, int lane) {
-    const int PW = a.W + 2;
-    const int F = a.F, N = a.N;
-    if (F <= 128) {
-        for (int j = lane; j < F; j += 64)
-            keys[j] = ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j) << 32) | (unsigned)j;
-        wave_sync();
-        for (int j = lane; j < F; j += 64) {
-            const unsigned long long kj = keys[j];
-            int r = 0;
-#pragma unroll 4
-            for (int q = 0; q < F; q++) r += keys[q] < kj ? 1 : 0;
-            if (r < N) gpos[r] = (uint16_t)unpad(fl[j], PW);
-        }
-        wave_sync();
-        return;
-    }
-    uint32_t T = reset_threshold(N, F);
-    int C = 0;
-    for (int attempt = 0; attempt < 2; attempt++) {
-        C = 0;
-        for (int j0 = 0; j0 < F; j0 += 64) {
-            const int j = j0 + lane;
-            uint32_t k = 0;
-            bool cand = false;
-            if (j < F) {
-                k = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
-                cand = k <= T;
-            }
-            const unsigned long long m = __ballot(cand);
-            if (cand) keys[C + lanes_below(m)] = ((unsigned long long)k << 32) | (unsigned)j;
-            C += __popcll(m);
-        }
-        if (C >= N || T == 0xFFFFFFFFu) break;
-        T = 0xFFFFFFFFu;
-    }
-    wave_sync();
-    for (int i = lane; i < C; i += 64) {
-        const unsigned long long ki = keys[i];
-        int rank = 0;
-        for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-        if (rank < N) gpos[rank] = (uint16_t)unpad(fl[(int)(ki & 0xFFFFu)], PW);
-    }
-    wave_sync();
-}
-
 // One env group's HBM state in registers (software pipelining: the next
 // group's loads are issued at the top of a group and staged into LDS at its
 // bottom, so no register is carried across the loop back edge -- the
@@ -199,7 +140,7 @@ __attribute__((amdgpu_waves_per_eu(FFM_WAVES_PER_EU)))
 #endif
 void core_wave_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    using GT = uint8_t;
+    using GT = uint16_t;   // DirCodes
     constexpr int AL = 64 / EW;
     const int H = HT ? HT : a.H, W = WT ? WT : a.W;
     const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
@@ -227,7 +168,6 @@ void core_wave_kernel(CoreStepArgs a) {
     int* scnt = reinterpret_cast<int*>(wbase + cv.spos + 128);
     GT* gk = grid + sub * PHW;
     float* dk = tile + sub * TS;
-    uint16_t* rq = sreq + sub * AL;
     uint16_t* nx = snxt + sub * AL;
 
     // This lane's two float4 DFF slots (cells 4q..4q+3 of the group, q = lane,
@@ -336,32 +276,31 @@ void core_wave_kernel(CoreStepArgs a) {
         STAMP(0);
 
         // ---- occupancy marks; default next = stay -----------------------------
-        if (live) gk[pp] = (GT)(GridCodes<GT>::kAgent | (uint32_t)al);
-        rq[al] = kNoReq;
+        if (live) gk[pp] = (GT)(DirCodes::kAgent | (uint32_t)al | (DirCodes::kNoDir << 8));
         nx[al] = (uint16_t)(live ? pp : 0);
         wave_sync();
         STAMP(1);
 
         // ---- decide (model/ffm_core.py:40-88) --------------------------------------
-        uint32_t r = kNoReq;
+        uint32_t slot = kNoReq;
         if (live && !(FFM_ABLATE & 1)) {
             if (MT) {
-                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawPending{}), pp, PW);
+                slot = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawPending{});
             } else if (FFM_ABLATE & 256) {   // diagnostic: cheap hash instead of Philox
                 const uint32_t hsh = (genv * 2654435761u) ^ ((uint32_t)al * 40503u) ^ (a.t * 97u);
-                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
-                                          DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)}), pp, PW);
+                slot = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
+                                             DrawFixed{(double)(hsh >> 8) * (1.0 / 16777216.0)});
             } else {
                 const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
                 // words 2, 3 feed the friction draw if this agent owns a contested target
                 reinterpret_cast<uint2*>(wbase + cv.u)[lane] = make_uint2(pb.z, pb.w);
-                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
-                                          DrawFixed{u53(pb.x, pb.y)}), pp, PW);
+                slot = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64,
+                                             DrawFixed{u53(pb.x, pb.y)});
             }
         }
         if (MT) {
             double* su = reinterpret_cast<double*>(wbase + cv.u) + sub * AL;
-            const unsigned long long pend = __ballot(r == kPending);
+            const unsigned long long pend = __ballot(slot == kPending);
             if (al == 0 && env_ok) {
                 uint32_t* mt_np = a.mt_np + (e0 + sub) * 625;
                 unsigned long long mk = (pend >> (sub * AL)) & (AL == 64 ? ~0ull : ((1ull << AL) - 1ull));
@@ -372,11 +311,16 @@ void core_wave_kernel(CoreStepArgs a) {
                 }
             }
             wave_sync();
-            if (r == kPending)
-                r = slot_cell<NB>(decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]}), pp, PW);
+            if (slot == kPending)
+                slot = decide<NB, false, GT>(pp, PW, gk, psff, nullptr, dk, dd0, kDWS, a.kS32, a.kD32, a.kS64, DrawFixed{su[al]});
         }
         STAMP(2);
-        if (live) rq[al] = (uint16_t)r;
+        // The request goes into the agent's own grid cell (resolve reads it there).
+        // Other lanes may still be reading this cell for validity: they only test
+        // the agent bit, which does not change.
+        const uint32_t r = live ? slot_cell<NB>(slot, pp, PW) : kNoReq;
+        if (live)   // the high byte of the agent's u16 cell: its chosen slot
+            reinterpret_cast<uint8_t*>(gk)[2 * pp + 1] = (uint8_t)(slot <= (uint32_t)NB ? slot : DirCodes::kNoDir);
         wave_sync();
         STAMP(3);
 
@@ -390,7 +334,7 @@ void core_wave_kernel(CoreStepArgs a) {
             int m = 0, s0 = -1;
             bool owner = false;
             if (moving) {
-                m = requesters<NB, GT>((int)r, PW, gk, rq, who, is);
+                m = requesters_dir<NB>((int)r, PW, gk, who, is);
                 s0 = kth_slot<NB>(who, is, 0);
                 owner = s0 >= 0 && who[s0] == al;
             }
