@@ -146,11 +146,12 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     const int A = d.agent_capacity;
     const bool reset_lds = !e->mt && d.auto_reset;
     const int EW = A <= 32 ? 2 : 1;
-    // envs_per_block: 0 = auto, > 0 = block kernel with that many envs per
-    // workgroup, -1 = wave kernel (diagnostic / tests).
-    e->pack = d.envs_per_block == 0 && !e->mt && !e->f64 && A <= 64 && W % 4 == 0 && HW <= 256 &&
+    // envs_per_block: 0 = auto (wave kernel where it fits, else block kernel),
+    // > 0 = block kernel with that many envs per workgroup, -1 = wave kernel,
+    // -2 = packed-bundle kernel (measured slower at C2: 49.9 vs 46.0 us).
+    e->pack = d.envs_per_block == -2 && !e->mt && !e->f64 && A <= 64 && W % 4 == 0 && HW <= 256 &&
               ffm::core_pack_smem_bytes(H, W, A, e->F, 4, reset_lds, 4) <= 64 * 1024;
-    e->wave = !e->pack && d.envs_per_block <= 0 && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
+    e->wave = !e->pack && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
               ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
     int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);

@@ -81,7 +81,7 @@ typedef struct {
     int64_t env_base;         /* global id of env 0 (multi-GPU sharding keys RNG by global id) */
     int32_t device;           /* HIP device ordinal */
     int32_t envs_per_block;   /* 0 = auto, > 0 = block kernel with that many envs per workgroup,
-                                 -1 = wave kernel (no env packing; diagnostics and tests) */
+                                 -1 = wave kernel, -2 = packed-bundle kernel (diagnostics, tests) */
 } ffm_engine_desc;
 
 typedef struct {
