@@ -1,0 +1,84 @@
+/*
+ * ffm_learn_oracle.h -- CPU restatement of SoraKurihara/FFM's learning
+ * variants: model/ffm_ac_core.py, model/ffm_unified.py (critic_only /
+ * actor_only / both) and model/ffm_actor_only.py.
+ *
+ * TEST INFRASTRUCTURE ONLY (like ffm_oracle.h): used by tests/ and by
+ * bench.py's cpu_baseline leg, never by the product.
+ *
+ * Two semantics:
+ *  * MT ("exact"): one env, the reference's two global MT19937 streams, the
+ *    tables read and written in agent order exactly as the reference's dicts
+ *    (Gauss-Seidel).  Pinned by tests/golden/learn_*.npz, recorded from the
+ *    reference itself (tests/golden/gen_golden_learn.py).
+ *  * Philox ("batched"): every env of a batch steps against
+ *    the tables as they were at the start of the step; the TD and actor
+ *    increments of all envs are summed in 2^-32 fixed point (order-free, so
+ *    deterministic) and applied once per step.  This is the GPU's production
+ *    semantics; GPU == this code bit for bit.
+ *
+ * State keys are packed u64 (ffm_amd/learn_keys.py): 2 bits per cell / rank
+ * in [0,26), bx in [26,45), by in [45,64).
+ */
+#ifndef FFM_LEARN_ORACLE_H
+#define FFM_LEARN_ORACLE_H
+
+#include <stdint.h>
+#include "ffm_oracle.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { FFO_VAR_AC = 1, FFO_VAR_UNIFIED = 2, FFO_VAR_ACTOR_ONLY = 3 };
+enum { FFO_MODE_CRITIC = 0, FFO_MODE_ACTOR = 1, FFO_MODE_BOTH = 2 };
+
+typedef struct {
+    int32_t H, W;
+    const uint8_t* map;       /* raw map values 0..3 (state maps use them as-is) */
+    const float* sff32;       /* raw SFF (inf on walls) or NULL */
+    const double* sff64;      /* used when sff32 == NULL */
+    int32_t variant, mode;
+    double k_S, k_D, k_A, diffuse, decay;
+    double alpha_v, alpha_h, gamma, exit_reward, step_penalty, collision_penalty;
+    double epsilon;
+    double v_default;         /* value of a V entry created by a read (0.0; -1.0 after set_v_table, ac) */
+    int32_t block_size;
+} ffo_learn_cfg;
+
+typedef struct ffo_tab ffo_tab;
+
+ffo_tab* ffo_tab_new(int32_t width, int32_t log2_cap);
+void ffo_tab_free(ffo_tab* t);
+int64_t ffo_tab_size(const ffo_tab* t);
+/* entries in insertion order (the reference dict's order in MT mode) */
+void ffo_tab_export(const ffo_tab* t, uint64_t* keys, double* vals);
+/* insert/overwrite in the given order */
+int ffo_tab_import(ffo_tab* t, const uint64_t* keys, const double* vals, int64_t n);
+
+/* Reference-exact step of one env (MT streams).  pos: int32 cells x*W+y. */
+int ffo_learn_step_mt(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int32_t* pos, int32_t* n,
+                      float* dff, ffo_mt* np_rng, ffo_mt* py_rng);
+
+/* Batched Philox step of E envs (see header comment).  pos [E][A_cap] u16,
+ * counts [E], dff [E][H*W], episodes [E], ep_steps [E] (steps in the current
+ * episode).  An env is re-placed (N_reset agents, DFF zeroed) at the end of a
+ * step that empties it or that reaches max_steps (> 0). */
+int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E,
+                                int32_t A_cap, uint16_t* pos, int32_t* counts, float* dff,
+                                int32_t* episodes, int32_t* ep_steps, uint64_t seed, uint32_t t,
+                                int32_t auto_reset, int32_t N_reset, int32_t max_steps,
+                                int64_t env_base, uint64_t* agent_steps, int nthreads);
+
+/* Deterministic float64 exp (fdlibm's algorithm, +,*,/ only): the f64
+ * softmax of the actor modes on CPU and GPU alike. */
+double ffo_det_exp(double x);
+
+/* State encoders (exposed for unit tests). sm = state map [H*W]. */
+uint64_t ffo_encode_rank(const uint8_t* sm, int H, int W, int x, int y, int bs);
+uint64_t ffo_encode_cells13(const uint8_t* sm, int H, int W, int x, int y, int bs, int oob);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

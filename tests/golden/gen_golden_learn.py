@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Golden vectors of the reference's learning variants (container only).
+
+    python tests/golden/gen_golden_learn.py [--ref /root/reference]
+
+Imports the reference's own classes (SoraKurihara/FFM):
+  * model/ffm_ac_core.py      FloorFieldModel            (critic, 13-cell keys)
+  * model/ffm_unified.py      FloorFieldModelUnified     (critic_only / actor_only / both)
+  * model/ffm_actor_only.py   FloorFieldModelActorOnly   (config-4 actor, 13-cell keys)
+seeds NumPy's and CPython's global generators, and records several episodes
+per seed with the tables carried across episodes (``reset()`` between them,
+like the training drivers, e.g. run_unified_actor_training.py:270-300).
+Only recorded arrays leave this container, as ``learn_*.npz`` fixtures.
+
+Per case: map, sff, params (json), variant, mode, N, seeds, episodes per
+seed, epsilon per episode; per step: counts / cells (as in gen_golden.py) and
+a DFF hash; per seed: the V table and H table at the end, in dict insertion
+order, keys packed by ffm_amd/learn_keys.py, and the RNG tails.  One case also
+calls ``set_v_table(get_v_table())`` between episodes (model/ffm_ac_core.py:335-343:
+missing states then default to -1.0).
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import os
+import random
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+from golden_util import dff_hash  # noqa: E402
+from ffm_amd import learn_keys as K  # noqa: E402
+
+
+def pack_key(variant, k):
+    if variant == "unified":
+        return K.from_rank_tuple(k)
+    if isinstance(k, (bytes, bytearray)):
+        return K.from_cells_bytes(bytes(k))
+    return K.from_cells_tuple(k)
+
+
+def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_steps, mode=None,
+             eps_sched=None, reload_v=False):
+    H, W = map_array.shape
+    init, nsteps, counts, cells, hashes = [], [], [], [], []
+    vk, vv, vn, hk, hv, hn, np_tail, py_tail, eps_list = [], [], [], [], [], [], [], [], []
+    with tempfile.TemporaryDirectory() as td:
+        sff_path = os.path.join(td, "sff.npy")
+        np.save(sff_path, sff)
+        for seed in seeds:
+            np.random.seed(seed)
+            random.seed(seed)
+            with contextlib.redirect_stdout(io.StringIO()):
+                if variant == "unified":
+                    model = cls(map_array, sff_path, N, learning_mode=mode, params=dict(params))
+                else:
+                    model = cls(map_array, sff_path, N, params=dict(params))
+            for ep in range(n_ep):
+                if ep > 0:
+                    if reload_v:
+                        model.set_v_table(model.get_v_table())
+                    model.reset()
+                e = 0.0 if eps_sched is None else float(eps_sched[ep])
+                if eps_sched is not None:
+                    model.set_epsilon(e)
+                eps_list.append(e)
+                p0 = model.positions
+                init.append((p0[:, 0] * W + p0[:, 1]).astype(np.int16))
+                steps = 0
+                while model.positions.shape[0] > 0 and steps < max_steps:
+                    model.step()
+                    steps += 1
+                    p = model.positions
+                    counts.append(p.shape[0])
+                    cells.extend((p[:, 0] * W + p[:, 1]).astype(np.int16).tolist())
+                    hashes.append(dff_hash(model.dff))
+                nsteps.append(steps)
+            V = model.get_v_table()
+            vk.extend(pack_key(variant, k) for k in V.keys())
+            vv.extend(float(v) for v in V.values())
+            vn.append(len(V))
+            Ht = model.get_h_table() if hasattr(model, "get_h_table") else None
+            if Ht:
+                hk.extend(pack_key(variant, k) for k in Ht.keys())
+                hv.extend(list(map(float, r)) for r in Ht.values())
+                hn.append(len(Ht))
+            else:
+                hn.append(0)
+            bg = np.random.mtrand._rand._bit_generator
+            np_tail.append(np.asarray(bg.random_raw(4), dtype=np.uint32))
+            py_tail.append(np.asarray([random.getrandbits(32) for _ in range(4)], dtype=np.uint32))
+    out = dict(
+        map=map_array.astype(np.uint8), sff=sff, params=json.dumps(params), variant=variant,
+        mode=mode or "", N=np.int32(N), seeds=np.asarray(seeds, np.int64), n_ep=np.int32(n_ep),
+        max_steps=np.int32(max_steps), reload_v=np.int32(reload_v), eps=np.asarray(eps_list),
+        init=np.concatenate(init).astype(np.int16), init_n=np.asarray([len(i) for i in init], np.int32),
+        nsteps=np.asarray(nsteps, np.int32), counts=np.asarray(counts, np.int16),
+        cells=np.asarray(cells, np.int16), dff_hash=np.asarray(hashes, np.uint64),
+        v_keys=np.asarray(vk, np.uint64), v_vals=np.asarray(vv, np.float64), v_n=np.asarray(vn, np.int64),
+        h_keys=np.asarray(hk, np.uint64), h_vals=np.asarray(hv, np.float64).reshape(-1, 5),
+        h_n=np.asarray(hn, np.int64), np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
+    )
+    path = os.path.join(HERE, f"learn_{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: seeds={len(seeds)} episodes={len(nsteps)} steps={sum(nsteps)} |V|={vn} |H|={hn} "
+          f"-> {os.path.getsize(path)} B")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+    sys.path.insert(0, args.ref)
+    from model.ffm_ac_core import FloorFieldModel as AC
+    from model.ffm_unified import FloorFieldModelUnified as UNI
+    from model.ffm_actor_only import FloorFieldModelActorOnly as AO
+
+    z = np.load(os.path.join(HERE, "room_12x12_reference.npz"))
+    m12, s12 = z["map"], z["sff"]
+    # ffm_ac_core with its class defaults (k_S 10, block 3), then the set_v_table quirk.
+    run_case("ac_12x12_N8", "ac", AC, m12, s12, {}, 8, [0, 1, 2], 3, 400)
+    run_case("ac_12x12_N32_reload", "ac", AC, m12, s12, {"k_S": 3, "block_size": 5}, 32, [3, 4], 3, 400,
+             reload_v=True)
+    # ffm_unified, run_unified_*_training.py parameters (block 1) and class defaults (block 5)
+    uni_p = {"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99,
+             "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0,
+             "neighborhood": "neumann", "block_size": 1}
+    run_case("unified_critic_12x12_N16", "unified", UNI, m12, s12, uni_p, 16, [5, 6], 3, 300,
+             mode="critic_only")
+    run_case("unified_critic_12x12_N40_bs5", "unified", UNI, m12, s12, {}, 40, [7], 2, 300,
+             mode="critic_only")
+    eps = np.linspace(0.2, 0.01, 4)
+    run_case("unified_actor_12x12_N16", "unified", UNI, m12, s12, uni_p, 16, [8, 9], 4, 300,
+             mode="actor_only", eps_sched=eps)
+    run_case("unified_both_12x12_N24", "unified", UNI, m12, s12, dict(uni_p, block_size=5), 24, [10], 4, 300,
+             mode="both", eps_sched=eps)
+    run_case("unified_actor_12x12_N30_eps0", "unified", UNI, m12, s12, uni_p, 30, [11], 3, 300,
+             mode="actor_only")
+    # ffm_actor_only, run_actor_only_training.py parameters (no pretrained critic)
+    ao_p = {"k_D": 1, "k_A": 10, "alpha_v": 0.1, "alpha_h": 0.1, "gamma": 0.95, "exit_reward": 100.0,
+            "step_penalty": 0.0, "collision_penalty": -1.0, "neighborhood": "neumann"}
+    run_case("actoronly_12x12_N16", "actor_only", AO, m12, s12, ao_p, 16, [12, 13], 4, 300,
+             eps_sched=eps)
+    run_case("actoronly_12x12_N32_eps0", "actor_only", AO, m12, s12, ao_p, 32, [14], 2, 300)
+
+
+if __name__ == "__main__":
+    main()
