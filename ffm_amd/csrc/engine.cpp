@@ -20,13 +20,20 @@
 #include "kernels.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const std::string& msg) {
+namespace ffm {
+// Shared with learn_engine.cpp: records the calling thread's last error.
+int set_error(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+}  // namespace ffm
+
+namespace {
+
+int fail(int code, const std::string& msg) { return ffm::set_error(code, msg); }
 
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \

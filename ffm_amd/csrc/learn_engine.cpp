@@ -1,0 +1,551 @@
+// learn_engine.cpp -- C ABI (include/ffm_amd.h, ffm_learner_*) over the
+// learning-variant kernels of learn_step.hip.
+//
+// Mirrors the reference's learning classes: model/ffm_ac_core.py
+// FloorFieldModel, model/ffm_unified.py FloorFieldModelUnified and
+// model/ffm_actor_only.py FloorFieldModelActorOnly.  One learner holds E envs
+// and one V table and one H table shared by all of them (the drivers run one
+// env and keep the tables across episodes, e.g.
+// run_unified_actor_training.py:270-300).
+#include "../../include/ffm_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "learn_kernels.h"
+
+namespace ffm {
+int set_error(int code, const std::string& msg);
+}
+
+namespace {
+
+int fail(int code, const std::string& msg) { return ffm::set_error(code, msg); }
+
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(FFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+struct DevTable {
+    ffm::LearnTable t{};
+    int width = 1;
+    size_t cap = 0;
+};
+
+}  // namespace
+
+struct ffm_learner {
+    ffm_engine_desc d{};
+    ffm_learn_desc L{};
+    bool mt = false, f64 = false, actor = false, post_update = false;
+    int HW = 0, F = 0, D = 1;
+    float smin = 0, smax = 0;
+    uint32_t t = 0;
+    int cur = 0;                       // which DFF buffer is current
+    uint8_t* d_map = nullptr;
+    void* d_sff = nullptr;
+    uint16_t* d_free_cells = nullptr;
+    uint16_t* d_pos = nullptr;
+    int32_t* d_cnt = nullptr;
+    float* d_dff[2] = {nullptr, nullptr};
+    int32_t* d_eps = nullptr;
+    int32_t* d_ep_steps = nullptr;
+    int32_t* d_done = nullptr;
+    int32_t* d_nstart = nullptr;
+    unsigned long long* d_ctr = nullptr;
+    double* d_hstat = nullptr;
+    double* d_hpart = nullptr;
+    ffm::LearnRec* d_recs = nullptr;
+    int32_t* d_overflow = nullptr;
+    uint32_t* d_mt_np = nullptr;
+    uint32_t* d_mt_py = nullptr;
+    unsigned char* d_scratch = nullptr;
+    DevTable V, H;
+};
+
+static void free_table(DevTable& T) {
+    (void)hipFree(T.t.keys);
+    (void)hipFree(T.t.vals);
+    (void)hipFree(T.t.acc);
+    (void)hipFree(T.t.order);
+    (void)hipFree(T.t.n);
+}
+
+static void release(ffm_learner* l) {
+    if (!l) return;
+    void* bufs[] = {l->d_map, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
+                    l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
+                    l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch};
+    for (void* p : bufs) (void)hipFree(p);
+    free_table(l->V);
+    free_table(l->H);
+    delete l;
+}
+
+static hipError_t alloc_table(DevTable& T, int log2cap, int width) {
+    T.width = width;
+    T.cap = (size_t)1 << log2cap;
+    T.t.mask = (uint32_t)(T.cap - 1);
+    hipError_t e;
+    if ((e = hipMalloc((void**)&T.t.keys, T.cap * 8)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&T.t.vals, T.cap * width * 8)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&T.t.acc, T.cap * width * 8)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&T.t.order, T.cap * 4)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&T.t.n, 4)) != hipSuccess) return e;
+    return hipSuccess;
+}
+
+static ffm::LearnArgs make_args(ffm_learner* l) {
+    ffm::LearnArgs a{};
+    const ffm_engine_desc& d = l->d;
+    a.H = d.H; a.W = d.W; a.HW = l->HW; a.A = d.agent_capacity; a.N = d.n_agents; a.F = l->F;
+    a.E = d.n_envs; a.env_base = d.env_base;
+    a.variant = d.variant; a.mode = l->L.mode; a.bs = d.variant == FFM_VARIANT_ACTOR_ONLY ? 5 : l->L.block_size;
+    a.D = l->D;
+    a.map = l->d_map;
+    a.sff32 = l->f64 ? nullptr : reinterpret_cast<const float*>(l->d_sff);
+    a.sff64 = l->f64 ? reinterpret_cast<const double*>(l->d_sff) : nullptr;
+    a.smin = l->smin; a.smax = l->smax;
+    // NumPy weak-scalar promotion (NEP 50): python numbers become float32 next to
+    // a float32 array (model/ffm_unified.py:361-364, 442-445).
+    a.kS32 = (float)(-d.k_S); a.kD32 = (float)d.k_D; a.kS64 = -d.k_S; a.nkA = -l->L.k_A;
+    a.c0 = (float)((1.0 - d.decay) * (1.0 - d.diffuse));
+    a.c1 = (float)(d.decay * (1.0 - d.diffuse) / 4.0);
+    a.alpha_v = l->L.alpha_v; a.alpha_h = l->L.alpha_h; a.gamma = l->L.gamma;
+    a.exit_reward = l->L.exit_reward; a.step_penalty = l->L.step_penalty;
+    a.collision_penalty = l->L.collision_penalty; a.epsilon = l->L.epsilon; a.v_default = l->L.v_default;
+    a.pos = l->d_pos; a.cnt = l->d_cnt;
+    a.dff_in = l->d_dff[l->cur]; a.dff_out = l->d_dff[l->cur ^ 1];
+    a.episodes = l->d_eps; a.ep_steps = l->d_ep_steps; a.done = l->d_done; a.nstart = l->d_nstart;
+    a.counters = l->d_ctr;
+    a.V = l->V.t; a.Ht = l->H.t;
+    a.hstat = l->d_hstat; a.hpart = l->d_hpart; a.recs = l->d_recs; a.overflow = l->d_overflow;
+    a.key0 = (uint32_t)d.seed; a.key1 = (uint32_t)(d.seed >> 32); a.t = l->t;
+    a.auto_reset = d.auto_reset && !l->mt; a.max_steps = l->L.max_steps;
+    a.mt_np = l->d_mt_np; a.mt_py = l->d_mt_py; a.scratch = l->d_scratch;
+    a.free_cells = l->d_free_cells;
+    return a;
+}
+
+static int check_overflow(ffm_learner* l, hipStream_t s) {
+    int32_t ov = 0;
+    HIP_TRY(hipMemcpyAsync(&ov, l->d_overflow, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ov & 1) return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
+    if (ov & 2) return fail(FFM_E_HIP, "placement candidate list out of range (reset)");
+    return FFM_OK;
+}
+
+static hipError_t clear_table(ffm_learner* l, DevTable& T, double dflt, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(T.t.keys, 0xFF, T.cap * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(T.t.vals, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(T.t.n, 0, 4, s)) != hipSuccess) return e;
+    if (T.width == 1 && dflt != 0.0) {
+        ffm::LearnArgs a = make_args(l);
+        a.v_default = dflt;
+        return ffm::launch_learn_fill_default(a, s);
+    }
+    return hipSuccess;
+}
+
+extern "C" {
+
+int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn, ffm_learner** out) {
+    if (!desc || !learn || !out) return fail(FFM_E_INVALID, "null argument");
+    *out = nullptr;
+    const ffm_engine_desc& d = *desc;
+    if (d.abi_version != FFM_ABI_VERSION) return fail(FFM_E_INVALID, "abi_version mismatch");
+    if (d.variant != FFM_VARIANT_AC && d.variant != FFM_VARIANT_UNIFIED && d.variant != FFM_VARIANT_ACTOR_ONLY)
+        return fail(FFM_E_INVALID, "learner variant must be AC, UNIFIED or ACTOR_ONLY");
+    if (d.variant == FFM_VARIANT_UNIFIED && (learn->mode < 0 || learn->mode > 2))
+        return fail(FFM_E_INVALID, "learning_mode must be one of ['critic_only', 'actor_only', 'both']");
+    // Cells are u16 indices and 0xFFFF marks "none": up to 256 x 256 cells, the
+    // last one a wall (the border must be walls anyway).
+    if (d.H < 3 || d.W < 3 || (long long)d.H * d.W > 65536)
+        return fail(FFM_E_INVALID, "map must be at least 3x3 and at most 65536 cells");
+    if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
+    if ((long long)d.H * d.W == 65536 && (d.map[65535] == 0 || d.map[65535] == 3))
+        return fail(FFM_E_UNSUPPORTED, "the last cell of a 65536-cell map must be blocked");
+    if (d.neighborhood != 4) return fail(FFM_E_UNSUPPORTED, "learning variants are built for neighborhood 'neumann'");
+    if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
+    if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
+    if (d.agent_capacity < 1 || d.agent_capacity > 16384) return fail(FFM_E_INVALID, "agent_capacity");
+    if (d.n_agents < 0 || d.n_agents > d.agent_capacity) return fail(FFM_E_INVALID, "n_agents > agent_capacity");
+    if (d.rng_mode != FFM_RNG_PHILOX && d.rng_mode != FFM_RNG_MT) return fail(FFM_E_INVALID, "rng_mode");
+    if (learn->block_size < 1 && d.variant != FFM_VARIANT_ACTOR_ONLY) return fail(FFM_E_INVALID, "block_size");
+    const int H = d.H, W = d.W, HW = H * W;
+    std::vector<uint16_t> fl;
+    for (int i = 0; i < HW; i++) {
+        if (d.map[i] > 3) return fail(FFM_E_UNSUPPORTED, "learning variants need map values in 0..3 (state keys)");
+        const int x = i / W, y = i % W;
+        const bool border = x == 0 || y == 0 || x == H - 1 || y == W - 1;
+        if (d.map[i] == 0) {
+            if (border) return fail(FFM_E_INVALID, "free cell on the map border (walls must enclose the room)");
+            fl.push_back((uint16_t)i);
+        }
+    }
+    if (d.n_agents > (int)fl.size())
+        return fail(FFM_E_INVALID, "Cannot take a larger sample than population when 'replace=False'");
+    // On-device placement sorts <= 16384 candidates in LDS (learn_reset_kernel).
+    if (d.rng_mode == FFM_RNG_PHILOX && d.n_agents > 12288 && (int)fl.size() > 16384)
+        return fail(FFM_E_UNSUPPORTED, "on-device placement supports n_agents <= 12288 on maps with > 16384 free cells");
+
+    ffm_learner* l = new ffm_learner();
+    l->d = d;
+    l->d.map = nullptr;
+    l->d.sff = nullptr;
+    l->L = *learn;
+    if (l->L.log2_v_capacity <= 0) l->L.log2_v_capacity = 21;
+    if (l->L.log2_h_capacity <= 0) l->L.log2_h_capacity = 21;
+    l->L.log2_v_capacity = std::min(std::max(l->L.log2_v_capacity, 8), 30);
+    l->L.log2_h_capacity = std::min(std::max(l->L.log2_h_capacity, 8), 28);
+    l->mt = d.rng_mode == FFM_RNG_MT;
+    l->f64 = d.sff_dtype == FFM_SFF_F64;
+    l->HW = HW;
+    l->F = (int)fl.size();
+    l->D = d.variant == FFM_VARIANT_ACTOR_ONLY ? 4 : 1;
+    l->actor = d.variant == FFM_VARIANT_ACTOR_ONLY || (d.variant == FFM_VARIANT_UNIFIED && learn->mode != FFM_LEARN_CRITIC_ONLY);
+    l->post_update = d.variant == FFM_VARIANT_UNIFIED && learn->mode == FFM_LEARN_ACTOR_ONLY;
+    if (!l->mt && !ffm::learn_batch_supported(HW, d.agent_capacity, l->D)) {
+        release(l);
+        return fail(FFM_E_UNSUPPORTED, "env does not fit the batched learner's LDS budget");
+    }
+    // min / max of the inf->0 float32 SFF (model/ffm_unified.py:74-76, 425-426)
+    {
+        float mn = INFINITY, mx = -INFINITY;
+        for (int i = 0; i < HW; i++) {
+            const double raw = l->f64 ? reinterpret_cast<const double*>(d.sff)[i]
+                                      : (double)reinterpret_cast<const float*>(d.sff)[i];
+            const float v = std::isinf(raw) ? 0.0f : (float)raw;
+            mn = std::min(mn, v);
+            mx = std::max(mx, v);
+        }
+        l->smin = mn;
+        l->smax = mx;
+    }
+    auto cleanup = [&](int rc) {
+        release(l);
+        return rc;
+    };
+    hipError_t he = hipSetDevice(d.device);
+    if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(he)));
+    const size_t E = (size_t)d.n_envs, A = (size_t)d.agent_capacity;
+#define ALLOC(p, n)                                                                                   \
+    do {                                                                                              \
+        he = hipMalloc((void**)&(p), (n));                                                            \
+        if (he != hipSuccess) return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he))); \
+    } while (0)
+    ALLOC(l->d_map, (size_t)HW);
+    ALLOC(l->d_sff, (size_t)HW * (l->f64 ? 8 : 4));
+    ALLOC(l->d_free_cells, std::max<size_t>(1, fl.size()) * 2);
+    ALLOC(l->d_pos, E * A * 2);
+    ALLOC(l->d_cnt, E * 4);
+    ALLOC(l->d_dff[0], E * HW * 4);
+    if (!l->mt) ALLOC(l->d_dff[1], E * HW * 4);
+    ALLOC(l->d_eps, E * 4);
+    ALLOC(l->d_ep_steps, E * 4);
+    ALLOC(l->d_done, E * 4);
+    ALLOC(l->d_nstart, E * 4);
+    ALLOC(l->d_ctr, E * 32);
+    ALLOC(l->d_hstat, 4 * 8);
+    ALLOC(l->d_hpart, (size_t)ffm::kHstatBlocks * 4 * 8);
+    if (l->post_update && !l->mt) ALLOC(l->d_recs, E * A * sizeof(ffm::LearnRec));
+    ALLOC(l->d_overflow, 4);
+    if (l->mt) {
+        ALLOC(l->d_mt_np, E * 625 * 4);
+        ALLOC(l->d_mt_py, E * 625 * 4);
+        ALLOC(l->d_scratch, ffm::learn_exact_scratch_bytes(HW, (int)A));
+    }
+#undef ALLOC
+    if ((he = alloc_table(l->V, l->L.log2_v_capacity, 1)) != hipSuccess ||
+        (he = alloc_table(l->H, l->actor ? l->L.log2_h_capacity : 8, 5)) != hipSuccess)
+        return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
+    he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemcpy(l->d_sff, d.sff, (size_t)HW * (l->f64 ? 8 : 4), hipMemcpyHostToDevice);
+    if (he == hipSuccess && !fl.empty()) he = hipMemcpy(l->d_free_cells, fl.data(), fl.size() * 2, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemset(l->d_pos, 0xFF, E * A * 2);
+    if (he == hipSuccess) he = hipMemset(l->d_cnt, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(l->d_dff[0], 0, E * HW * 4);
+    if (he == hipSuccess && l->d_dff[1]) he = hipMemset(l->d_dff[1], 0, E * HW * 4);
+    if (he == hipSuccess) he = hipMemset(l->d_eps, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(l->d_ep_steps, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(l->d_done, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(l->d_nstart, 0, E * 4);
+    if (he == hipSuccess) he = hipMemset(l->d_ctr, 0, E * 32);
+    if (he == hipSuccess) he = hipMemset(l->d_hstat, 0, 32);
+    if (he == hipSuccess) he = hipMemset(l->d_overflow, 0, 4);
+    if (he == hipSuccess && l->mt) he = hipMemset(l->d_mt_np, 0, E * 625 * 4);
+    if (he == hipSuccess && l->mt) he = hipMemset(l->d_mt_py, 0, E * 625 * 4);
+    if (he == hipSuccess) he = clear_table(l, l->V, l->L.v_default, nullptr);
+    if (he == hipSuccess) he = clear_table(l, l->H, 0.0, nullptr);
+    if (he == hipSuccess) he = hipDeviceSynchronize();
+    if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, std::string("init: ") + hipGetErrorString(he)));
+    *out = l;
+    return FFM_OK;
+}
+
+int ffm_learner_destroy(ffm_learner* l) {
+    if (!l) return FFM_OK;
+    (void)hipSetDevice(l->d.device);
+    (void)hipDeviceSynchronize();
+    release(l);
+    return FFM_OK;
+}
+
+int ffm_learner_reset(ffm_learner* l, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t E = (size_t)l->d.n_envs;
+    HIP_TRY(hipMemsetAsync(l->d_dff[l->cur], 0, E * l->HW * 4, s));
+    HIP_TRY(hipMemsetAsync(l->d_cnt, 0, E * 4, s));
+    HIP_TRY(hipMemsetAsync(l->d_ep_steps, 0, E * 4, s));
+    HIP_TRY(hipMemsetAsync(l->d_pos, 0xFF, E * l->d.agent_capacity * 2, s));
+    if (l->mt) return FFM_OK;
+    HIP_TRY(ffm::launch_learn_reset(make_args(l), true, s));
+    l->t++;
+    return check_overflow(l, s);
+}
+
+int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
+    if (!l || n_steps < 0) return fail(FFM_E_INVALID, "bad learner/n_steps");
+    hipStream_t s = (hipStream_t)stream;
+    for (int i = 0; i < n_steps; i++) {
+        if (l->mt) {
+            HIP_TRY(ffm::launch_learn_exact(make_args(l), s));
+            l->t++;
+            continue;
+        }
+        if (l->actor) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
+        HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
+        HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
+        if (l->post_update) HIP_TRY(ffm::launch_learn_post(make_args(l), s));
+        if (l->actor) HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
+        l->cur ^= 1;
+        if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
+        l->t++;
+    }
+    return FFM_OK;
+}
+
+static int check_range(ffm_learner* l, int64_t env0, int64_t n) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (env0 < 0 || n < 0 || env0 + n > l->d.n_envs) return fail(FFM_E_INVALID, "env range out of bounds");
+    return FFM_OK;
+}
+
+int ffm_learner_set_state(ffm_learner* l, int64_t env0, int64_t n, const uint16_t* positions,
+                          const int32_t* counts, const float* dff, void* stream) {
+    int rc = check_range(l, env0, n);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int A = l->d.agent_capacity;
+    if (counts)
+        for (int64_t i = 0; i < n; i++)
+            if (counts[i] < 0 || counts[i] > A) return fail(FFM_E_INVALID, "count out of [0, agent_capacity]");
+    if (positions && counts) {
+        std::vector<uint8_t> map(l->HW);
+        HIP_TRY(hipMemcpy(map.data(), l->d_map, l->HW, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> seen(l->HW, 0);
+        for (int64_t i = 0; i < n; i++) {
+            for (int j = 0; j < counts[i]; j++) {
+                const uint16_t c = positions[i * A + j];
+                if (c >= l->HW || !(map[c] == 0)) return fail(FFM_E_INVALID, "agent on a non-free cell");
+                if (seen[c]) return fail(FFM_E_INVALID, "two agents on one cell");
+                seen[c] = 1;
+            }
+            for (int j = 0; j < counts[i]; j++) seen[positions[i * A + j]] = 0;
+        }
+    }
+    if (positions)
+        HIP_TRY(hipMemcpyAsync(l->d_pos + env0 * A, positions, (size_t)n * A * 2, hipMemcpyHostToDevice, s));
+    if (counts) HIP_TRY(hipMemcpyAsync(l->d_cnt + env0, counts, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    if (dff)
+        HIP_TRY(hipMemcpyAsync(l->d_dff[l->cur] + env0 * l->HW, dff, (size_t)n * l->HW * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_learner_get_state(ffm_learner* l, int64_t env0, int64_t n, uint16_t* positions, int32_t* counts,
+                          float* dff, void* stream) {
+    int rc = check_range(l, env0, n);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int A = l->d.agent_capacity;
+    if (positions)
+        HIP_TRY(hipMemcpyAsync(positions, l->d_pos + env0 * A, (size_t)n * A * 2, hipMemcpyDeviceToHost, s));
+    if (counts) HIP_TRY(hipMemcpyAsync(counts, l->d_cnt + env0, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (dff)
+        HIP_TRY(hipMemcpyAsync(dff, l->d_dff[l->cur] + env0 * l->HW, (size_t)n * l->HW * 4, hipMemcpyDeviceToHost, s));
+    return check_overflow(l, s);
+}
+
+int ffm_learner_get_episodes(ffm_learner* l, int64_t env0, int64_t n, int32_t* episodes, int32_t* ep_steps,
+                             void* stream) {
+    int rc = check_range(l, env0, n);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (episodes) HIP_TRY(hipMemcpyAsync(episodes, l->d_eps + env0, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (ep_steps) HIP_TRY(hipMemcpyAsync(ep_steps, l->d_ep_steps + env0, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_learner_set_mt_state(ffm_learner* l, int64_t env, const uint32_t* np_key, int32_t np_pos,
+                             const uint32_t* py_key, int32_t py_pos, void* stream) {
+    int rc = check_range(l, env, 1);
+    if (rc) return rc;
+    if (!l->mt) return fail(FFM_E_INVALID, "learner is not in MT mode");
+    if (np_pos < 0 || np_pos > 624 || py_pos < 0 || py_pos > 624) return fail(FFM_E_INVALID, "MT position");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t buf[1250];
+    std::memcpy(buf, np_key, 624 * 4);
+    buf[624] = (uint32_t)np_pos;
+    std::memcpy(buf + 625, py_key, 624 * 4);
+    buf[1249] = (uint32_t)py_pos;
+    HIP_TRY(hipMemcpyAsync(l->d_mt_np + env * 625, buf, 625 * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(l->d_mt_py + env * 625, buf + 625, 625 * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_learner_get_mt_state(ffm_learner* l, int64_t env, uint32_t* np_key, int32_t* np_pos, uint32_t* py_key,
+                             int32_t* py_pos, void* stream) {
+    int rc = check_range(l, env, 1);
+    if (rc) return rc;
+    if (!l->mt) return fail(FFM_E_INVALID, "learner is not in MT mode");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t buf[1250];
+    HIP_TRY(hipMemcpyAsync(buf, l->d_mt_np + env * 625, 625 * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(buf + 625, l->d_mt_py + env * 625, 625 * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(np_key, buf, 624 * 4);
+    *np_pos = (int32_t)buf[624];
+    std::memcpy(py_key, buf + 625, 624 * 4);
+    *py_pos = (int32_t)buf[1249];
+    return FFM_OK;
+}
+
+int ffm_learner_get_counters(ffm_learner* l, uint64_t* counters, void* stream) {
+    if (!l || !counters) return fail(FFM_E_INVALID, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<unsigned long long> c((size_t)l->d.n_envs * 4);
+    HIP_TRY(hipMemcpyAsync(c.data(), l->d_ctr, c.size() * 8, hipMemcpyDeviceToHost, s));
+    int rc = check_overflow(l, s);
+    if (rc) return rc;
+    for (int i = 0; i < 4; i++) counters[i] = 0;
+    for (size_t j = 0; j < (size_t)l->d.n_envs; j++)
+        for (int i = 0; i < 3; i++) counters[i] += c[j * 4 + i];
+    counters[3] = l->d.n_envs ? c[3] : 0;     // steps: every env steps every time
+    return FFM_OK;
+}
+
+int ffm_learner_set_epsilon(ffm_learner* l, double epsilon) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    l->L.epsilon = std::min(std::max(epsilon, 0.0), 1.0);      // np.clip (model/ffm_unified.py:867)
+    return FFM_OK;
+}
+
+int ffm_learner_set_v_default(ffm_learner* l, double v_default, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    l->L.v_default = v_default;
+    ffm::LearnArgs a = make_args(l);
+    HIP_TRY(ffm::launch_learn_fill_default(a, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return FFM_OK;
+}
+
+static DevTable* pick(ffm_learner* l, int32_t which) {
+    if (which == FFM_TABLE_V) return &l->V;
+    if (which == FFM_TABLE_H && l->actor) return &l->H;
+    return nullptr;
+}
+
+int ffm_learner_table_size(ffm_learner* l, int32_t which, int64_t* n, void* stream) {
+    if (!l || !n) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = pick(l, which);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpyAsync(&v, T->t.n, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    *n = (int64_t)v;
+    return FFM_OK;
+}
+
+int ffm_learner_export_table(ffm_learner* l, int32_t which, uint64_t* keys, double* vals, int64_t cap,
+                             int64_t* n, void* stream) {
+    if (!l || !n) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = pick(l, which);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = check_overflow(l, s);
+    if (rc) return rc;
+    uint32_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, T->t.n, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n = cnt;
+    if ((int64_t)cnt > cap) return fail(FFM_E_INVALID, "export buffer too small");
+    if (cnt == 0) return FFM_OK;
+    std::vector<uint32_t> order(cnt);
+    std::vector<unsigned long long> k(T->cap);
+    std::vector<double> v(T->cap * T->width);
+    HIP_TRY(hipMemcpyAsync(order.data(), T->t.order, (size_t)cnt * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(k.data(), T->t.keys, T->cap * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(v.data(), T->t.vals, T->cap * T->width * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (uint32_t i = 0; i < cnt; i++) {
+        const size_t slot = order[i];
+        if (keys) keys[i] = k[slot];
+        if (vals) std::memcpy(vals + (size_t)i * T->width, v.data() + slot * T->width, 8 * (size_t)T->width);
+    }
+    return FFM_OK;
+}
+
+int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys, const double* vals, int64_t n,
+                             void* stream) {
+    if (!l || (n > 0 && (!keys || !vals))) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = pick(l, which);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if ((size_t)n > T->cap - T->cap / 8) return fail(FFM_E_NOMEM, "table capacity too small for import");
+    for (int64_t i = 0; i < n; i++)
+        if (keys[i] == ~0ull) return fail(FFM_E_INVALID, "invalid key");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(clear_table(l, *T, which == FFM_TABLE_V ? l->L.v_default : 0.0, s));
+    if (n > 0) {
+        unsigned long long* dk = nullptr;
+        double* dv = nullptr;
+        HIP_TRY(hipMalloc((void**)&dk, (size_t)n * 8));
+        hipError_t he = hipMalloc((void**)&dv, (size_t)n * T->width * 8);
+        if (he == hipSuccess) he = hipMemcpyAsync(dk, keys, (size_t)n * 8, hipMemcpyHostToDevice, s);
+        if (he == hipSuccess) he = hipMemcpyAsync(dv, vals, (size_t)n * T->width * 8, hipMemcpyHostToDevice, s);
+        if (he == hipSuccess) he = ffm::launch_learn_import(T->t, T->width, dk, dv, n, l->d_overflow, s);
+        if (he == hipSuccess) he = hipStreamSynchronize(s);
+        (void)hipFree(dk);
+        (void)hipFree(dv);
+        if (he != hipSuccess) return fail(FFM_E_HIP, std::string("import: ") + hipGetErrorString(he));
+    }
+    return check_overflow(l, s);
+}
+
+int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t) {
+    if (!l || !t) return fail(FFM_E_INVALID, "null argument");
+    *t = l->t;
+    return FFM_OK;
+}
+
+int ffm_learner_set_step_index(ffm_learner* l, uint32_t t) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    l->t = t;
+    return FFM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// learn_kernels.h -- host-side launch interface of the learning-variant
+// kernels (internal): ffm_ac_core, ffm_unified, ffm_actor_only of
+// SoraKurihara/FFM.  See learn_step.hip and DESIGN.md section 9.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ffm {
+
+enum : int { kVarAC = 1, kVarUnified = 2, kVarActorOnly = 3 };
+enum : int { kModeCritic = 0, kModeActor = 1, kModeBoth = 2 };
+
+// Per-agent record kept between the step kernel and the post-update actor
+// kernel of ffm_unified's actor_only mode (TD error with the updated V).
+struct LearnRec {
+    double r;              // reward
+    int32_t sv, snv;       // V slots of s and s' (-1 = terminal)
+    int32_t hslot;         // H slot of s
+    int32_t k;             // chosen action, -1 = none / invalid
+};
+
+struct LearnTable {
+    unsigned long long* keys;   // [cap], ~0 = empty
+    double* vals;               // [cap * width]; empty slots hold the default
+    long long* acc;             // [cap * width] fixed-point (2^-32) increments of the batched step
+    uint32_t* order;            // [cap] slot of the i-th inserted key
+    uint32_t* n;                // [1] keys inserted
+    uint32_t mask;              // cap - 1
+};
+
+struct LearnArgs {
+    int H, W, HW, A, N, F;
+    long long E, env_base;
+    int variant, mode, bs;      // bs: block size of the state keys
+    int D;                      // decisions per agent: 4 for ffm_actor_only, else 1
+    const uint8_t* map;         // [HW] raw map values (0 free, 1/2 blocked, 3 exit)
+    const float* sff32;         // [HW] raw SFF or nullptr
+    const double* sff64;        // [HW] (when sff32 == nullptr)
+    float smin, smax;           // min/max of the inf->0 SFF (model/ffm_unified.py:425-426)
+    float kS32, kD32;           // f32(-k_S), f32(k_D)
+    double kS64, nkA;           // -k_S, -k_A
+    float c0, c1;               // DFF coefficients (model/ffm_unified.py:779-798)
+    double alpha_v, alpha_h, gamma, exit_reward, step_penalty, collision_penalty, epsilon, v_default;
+    uint16_t* pos;              // [E][A]
+    int* cnt;                   // [E]
+    float* dff_in;              // [E][HW] current DFF (deposits land here)
+    float* dff_out;             // [E][HW] next DFF (stencil output)
+    int* episodes;              // [E]
+    int* ep_steps;              // [E]
+    int* done;                  // [E] re-place at the end of this step
+    int* nstart;                // [E] live agents at step start
+    unsigned long long* counters;  // [E][4] agent_steps, exits, resets, steps
+    LearnTable V, Ht;
+    double* hstat;              // [4] has, nonfinite, min, max of H (step start)
+    double* hpart;              // [2 * kHstatBlocks * 4] partials
+    LearnRec* recs;             // [E][A]
+    int* overflow;              // [1] table full / reset capacity exceeded
+    uint32_t key0, key1, t;
+    int auto_reset, max_steps;
+    uint32_t* mt_np;            // [E][625] (exact mode)
+    uint32_t* mt_py;
+    unsigned char* scratch;     // exact mode scratch
+    const uint16_t* free_cells;    // [F] x*W+y of the free cells, row-major (np.argwhere(map == 0))
+};
+
+constexpr int kHstatBlocks = 120;
+
+size_t learn_exact_scratch_bytes(int HW, int A);
+int learn_batch_block_size(int A);
+size_t learn_batch_smem_bytes(int HW, int A, int D);
+bool learn_batch_supported(int HW, int A, int D);
+hipError_t launch_learn_hstat(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_exact(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s);
+hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
+hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_import(const LearnTable& T, int width, const unsigned long long* keys, const double* vals,
+                              long long n, int* overflow, hipStream_t s);
+
+}  // namespace ffm

@@ -1,0 +1,1188 @@
+// learn_step.hip -- the learning variants of SoraKurihara/FFM on CDNA4:
+//   model/ffm_ac_core.py       critic (TD(0)) over 13-cell state keys
+//   model/ffm_unified.py       critic_only / actor_only / both over rank keys
+//   model/ffm_actor_only.py    the config-4 actor (13-cell keys, inner-loop quirk)
+//
+// Two executions of the same step:
+//  * learn_exact_kernel -- the reference's semantics bit for bit: the two
+//    MT19937 streams, targets and table updates in the reference's order.  It
+//    is inherently sequential (every agent's TD update can change the value the
+//    next agent reads), so one lane runs it; it serves the drop-in classes
+//    (one env) and the golden replays.
+//  * learn_batch_kernel -- the production step: one workgroup per env, agents
+//    on lanes, occupancy grid and requests in LDS, Philox draws keyed
+//    (t, env, seq), the V / H tables in HBM as open-addressing hash tables
+//    shared by all envs.  Every env reads the tables as they were at the start
+//    of the step; TD and actor increments are summed in 2^-32 fixed point
+//    (integer atomics: order-free, so the result is deterministic) and applied
+//    once per step by learn_apply_kernel.
+// All translation units are built with -ffp-contract=off.
+#include "device_common.h"
+#include "learn_kernels.h"
+
+namespace ffm {
+namespace {
+
+constexpr unsigned long long kEmptyKey = ~0ull;
+constexpr double kFxOne = 4294967296.0;
+constexpr uint16_t kNone16 = 0xFFFF;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z ^= z >> 33; z *= 0xff51afd7ed558ccdULL;
+    z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ULL;
+    z ^= z >> 33;
+    return z;
+}
+
+// Deterministic float64 exp (fdlibm e_exp.c reduction + rational correction),
+// the same code as oracle/ffm_learn_oracle.c: GPU == CPU bit for bit.
+__device__ double det_exp(double x) {
+    if (x != x) return x;
+    if (x > 709.782712893383973096) return __builtin_inf();
+    if (x < -745.13321910194110842) return 0.0;
+    const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    const double kd = __builtin_rint(x * invln2);
+    const double hi = x - kd * ln2HI;
+    const double lo = kd * ln2LO;
+    const double r = hi - lo;
+    const double t = r * r;
+    const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+    return __builtin_ldexp(y, (int)kd);
+}
+
+__device__ __forceinline__ long long fx(double v) {
+    double q = __builtin_rint(v * kFxOne);
+    q = q > 4.0e18 ? 4.0e18 : q;
+    q = q < -4.0e18 ? -4.0e18 : q;
+    return (long long)q;
+}
+
+__device__ __forceinline__ void acc_add(long long* p, long long q) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)q);
+}
+
+// ---- hash tables ------------------------------------------------------------
+// Slot of `key`, inserting it when absent (a defaultdict read inserts,
+// model/ffm_unified.py:658).  Empty slots already hold the default value, so
+// an inserter never has to publish a value.  -1 only when the table is full.
+__device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflow) {
+    uint32_t h = (uint32_t)mix64(key) & T.mask;
+    for (uint32_t probe = 0; probe <= T.mask; probe++) {
+        const unsigned long long k = __hip_atomic_load(&T.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key) return (int)h;
+        if (k == kEmptyKey) {
+            const unsigned long long old = atomicCAS(&T.keys[h], kEmptyKey, key);
+            if (old == kEmptyKey) {
+                const uint32_t idx = atomicAdd(T.n, 1u);
+                T.order[idx] = h;
+                if (idx >= T.mask - (T.mask >> 3)) atomicOr(overflow, 1);   // > 7/8 full
+                return (int)h;
+            }
+            if (old == key) return (int)h;
+        }
+        h = (h + 1) & T.mask;
+    }
+    atomicOr(overflow, 1);
+    return -1;
+}
+
+// ---- state maps and encoders ------------------------------------------------
+struct SmArray {                 // exact kernel: explicit state map
+    const uint8_t* sm;
+    __device__ int operator()(int c) const { return sm[c]; }
+};
+struct SmGrid {                  // batch kernel, current positions: agent grid in LDS
+    const uint8_t* map;
+    const uint16_t* grid;
+    __device__ int operator()(int c) const { return grid[c] != kNone16 ? 1 : map[c]; }
+};
+struct SmBits {                  // batch kernel, next positions (exit cells excluded)
+    const uint8_t* map;
+    const uint32_t* bits;
+    __device__ int operator()(int c) const { return ((bits[c >> 5] >> (c & 31)) & 1u) ? 1 : map[c]; }
+};
+
+__device__ __forceinline__ unsigned long long pack_key(unsigned long long cells, int bx, int by) {
+    return cells | ((unsigned long long)bx << 26) | ((unsigned long long)by << 45);
+}
+
+__constant__ int kNBx[4] = {-1, 1, 0, 0};   // U, D, L, R (model/ffm_unified.py:174-175)
+__constant__ int kNBy[4] = {0, 0, -1, 1};
+
+// model/ffm_unified.py:188-269
+template <class SM>
+__device__ unsigned long long enc_rank(const SM& sm, int H, int W, int x, int y, int bs) {
+    unsigned long long cells = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int dx = d == 0 ? -1 : d == 1 ? 1 : 0, dy = d == 2 ? -1 : d == 3 ? 1 : 0;
+        int rank = 3;
+        const int nx1 = x + dx, ny1 = y + dy;
+        if (nx1 >= 0 && nx1 < H && ny1 >= 0 && ny1 < W) {
+            const int v1 = sm(nx1 * W + ny1);
+            if (v1 == 2 || v1 == 1) {
+                rank = 0;
+            } else {
+                const int ax = dx != 0 ? nx1 : nx1 - 1, ay = dx != 0 ? ny1 - 1 : ny1;
+                const int bx = dx != 0 ? nx1 : nx1 + 1, by = dx != 0 ? ny1 + 1 : ny1;
+                bool diag = ax >= 0 && ax < H && ay >= 0 && ay < W && sm(ax * W + ay) == 1;
+                diag = diag || (bx >= 0 && bx < H && by >= 0 && by < W && sm(bx * W + by) == 1);
+                if (diag) {
+                    rank = 1;
+                } else {
+                    const int nx2 = x + 2 * dx, ny2 = y + 2 * dy;
+                    if (nx2 >= 0 && nx2 < H && ny2 >= 0 && ny2 < W) {
+                        const int v2 = sm(nx2 * W + ny2);
+                        if (v2 == 2 || v2 == 1) rank = 2;
+                    } else {
+                        rank = 2;
+                    }
+                }
+            }
+        } else {
+            rank = 0;
+        }
+        cells |= (unsigned long long)rank << (2 * d);
+    }
+    return pack_key(cells, x / bs, y / bs);
+}
+
+// model/ffm_ac_core.py:62-109 (oob 2) and model/ffm_actor_only.py:102-147 (oob 0)
+template <class SM>
+__device__ unsigned long long enc13(const SM& sm, int H, int W, int x, int y, int bs, int oob) {
+    unsigned long long cells = 0;
+    int i = 0;
+#pragma unroll
+    for (int dx = -1; dx <= 1; dx++)
+#pragma unroll
+        for (int dy = -1; dy <= 1; dy++, i++) {
+            const int nx = x + dx, ny = y + dy;
+            const int v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? sm(nx * W + ny) : oob;
+            cells |= (unsigned long long)(v & 3) << (2 * i);
+        }
+#pragma unroll
+    for (int d = 0; d < 4; d++, i++) {
+        const int nx = x + 2 * (d == 0 ? -1 : d == 1 ? 1 : 0), ny = y + 2 * (d == 2 ? -1 : d == 3 ? 1 : 0);
+        const int v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? sm(nx * W + ny) : oob;
+        cells |= (unsigned long long)(v & 3) << (2 * i);
+    }
+    return pack_key(cells, x / bs, y / bs);
+}
+
+template <class SM>
+__device__ unsigned long long encode(const LearnArgs& a, const SM& sm, int x, int y) {
+    if (a.variant == kVarUnified) return enc_rank(sm, a.H, a.W, x, y, a.bs);
+    if (a.variant == kVarAC) return enc13(sm, a.H, a.W, x, y, a.bs, 2);
+    return enc13(sm, a.H, a.W, x, y, 5, 0);                    // block 5 hard-coded, :143
+}
+
+// ---- random draws -----------------------------------------------------------
+__device__ uint32_t mt_interval(uint32_t* mt, uint32_t max) {     // NumPy legacy randint(max + 1)
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    while ((v = (mt_next(mt) & mask)) > max) {}
+    return v;
+}
+
+struct DrawMT {                  // the reference's global streams
+    uint32_t* np;
+    uint32_t* py;
+    __device__ double coin() { return mt_u53(py); }            // random.random()
+    __device__ double u() { return mt_u53(np); }               // np.random.choice(p)
+    __device__ uint32_t randint(uint32_t n) { return mt_interval(np, n - 1); }
+};
+
+struct DrawPh {                  // one keyed Philox stream per decision
+    PhiloxStream ps;
+    __device__ DrawPh(const LearnArgs& a, uint32_t genv, uint32_t seq)
+        : ps(a.key0, a.key1, a.t, genv, seq, kPurDecide) {}
+    __device__ double coin() { return ps.next_u53(); }
+    __device__ double u() { return ps.next_u53(); }
+    __device__ uint32_t randint(uint32_t n) {
+        const uint32_t max = n - 1;
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+        uint32_t v;
+        while ((v = (ps.next() & mask)) > max) {}
+        return v;
+    }
+};
+
+__device__ __forceinline__ int choice_cdf(const double* p, int n, double u) {
+    double cdf[5], acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if (k < n) { acc += p[k]; cdf[k] = acc; }
+    }
+    const double last = cdf[n - 1];
+    for (int k = 0; k < n; k++)
+        if (cdf[k] / last > u) return k;
+    return n - 1;
+}
+
+__device__ __forceinline__ double np_max5(const double* s, int n) {
+    double m = s[0];
+    for (int k = 1; k < n; k++) {
+        if (s[k] != s[k]) return s[k];
+        if (m != m) return m;
+        m = s[k] > m ? s[k] : m;
+    }
+    return m;
+}
+
+__device__ __forceinline__ double sum_seq(const double* e, int n) {   // NumPy add.reduce, n < 8
+    double s = -0.0;
+    for (int k = 0; k < n; k++) s += e[k];
+    return s;
+}
+__device__ __forceinline__ float sum_seqf(const float* e, int n) {
+    float s = -0.0f;
+    for (int k = 0; k < n; k++) s += e[k];
+    return s;
+}
+
+struct HStat {
+    int has, nonfinite;
+    double mn, mx;
+};
+
+// Actor policy: model/ffm_unified.py:394-499 (compat = false) and
+// model/ffm_actor_only.py:241-340 (compat = true: invalid -> -inf -> uniform).
+template <class R>
+__device__ int actor_choose(const LearnArgs& a, const double* hrow, const int* coord, const int* valid,
+                            const float* dff, const HStat& hs, bool compat, R& rng) {
+    double h[5], score[5], e[5], p[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = hrow[k];
+    if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
+        const double smin = (double)a.smin, smax = (double)a.smax;
+#pragma unroll
+        for (int k = 0; k < 5; k++) h[k] = ((hs.mx - h[k]) / (hs.mx - hs.mn)) * (smax - smin) + smin;
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const float d = a.kD32 * dff[coord[k]];
+        score[k] = a.nkA * h[k] + (double)d;
+        if (compat && !valid[k]) score[k] = -__builtin_inf();
+        bad = bad || !__builtin_isfinite(score[k]);
+    }
+    if (bad) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) score[k] = valid[k] ? 1.0 : 0.0;
+    }
+    double mx;
+    if (compat) {
+        double vs[5];
+        int nv = 0;
+        for (int k = 0; k < 5; k++)
+            if (valid[k]) vs[nv++] = score[k];
+        mx = nv ? np_max5(vs, nv) : 0.0;
+    } else {
+        mx = np_max5(score, 5);
+    }
+    int nvalid = 0, vidx[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        e[k] = valid[k] ? det_exp(score[k] - mx) : 0.0;
+        if (valid[k]) vidx[nvalid++] = k;
+    }
+    const double sum = sum_seq(e, 5);
+    if (__builtin_isfinite(sum) && sum > 0) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = e[k] / sum;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
+    }
+    if (a.epsilon > 0 && rng.coin() < a.epsilon) {
+        if (nvalid > 0) return vidx[rng.randint((uint32_t)nvalid)];
+        return 4;
+    }
+    return choice_cdf(p, 5, rng.u());
+}
+
+// Critic-only policy of ffm_unified (:353-392): raw SFF over all five moves.
+template <class R>
+__device__ int critic_choose(const LearnArgs& a, const int* coord, const int* valid, const float* dff, R& rng) {
+    double p[5];
+    int nvalid = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) nvalid += valid[k];
+    if (a.sff32) {
+        float s[5], e[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float x = a.kS32 * a.sff32[coord[k]];
+            const float y = a.kD32 * dff[coord[k]];
+            s[k] = x + y;
+        }
+        float mx = s[0];
+        for (int k = 1; k < 5; k++) {
+            if (s[k] != s[k]) { mx = s[k]; break; }
+            mx = s[k] > mx ? s[k] : mx;
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) e[k] = valid[k] ? np_expf(s[k] - mx) : 0.0f;
+        const float sum = sum_seqf(e, 5);
+        if (__builtin_isfinite(sum) && sum > 0) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) p[k] = (double)(e[k] / sum);
+        } else {
+            const float u = (float)(1.0 / (double)nvalid);
+#pragma unroll
+            for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)u : 0.0;
+        }
+    } else {
+        double s[5], e[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float y = a.kD32 * dff[coord[k]];
+            s[k] = a.kS64 * a.sff64[coord[k]] + (double)y;
+        }
+        const double mx = np_max5(s, 5);
+#pragma unroll
+        for (int k = 0; k < 5; k++) e[k] = valid[k] ? det_exp(s[k] - mx) : 0.0;
+        const double sum = sum_seq(e, 5);
+        if (__builtin_isfinite(sum) && sum > 0) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) p[k] = e[k] / sum;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
+        }
+    }
+    return choice_cdf(p, 5, rng.u());
+}
+
+// ffm_ac_core decide == ffm_core decide (model/ffm_ac_core.py:126-199).
+// `occ(cell)`: another agent stands there.  Returns the target or -1.
+template <class OCC, class R>
+__device__ int ac_decide(const LearnArgs& a, int x, int y, const OCC& occ, const float* dff, int& wexit, R& rng) {
+    const int W = a.W;
+    int cand[5], nc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int cell = (x + kNBx[k]) * W + (y + kNBy[k]);
+        const int m = a.map[cell];
+        if (!(m == 0 || m == 3)) continue;
+        if (occ(cell)) continue;
+        cand[nc++] = cell;
+    }
+    if (nc == 0) return -1;
+    cand[nc++] = x * W + y;
+    for (int k = 0; k < nc; k++)
+        if (a.map[cand[k]] == 3) { wexit = 1; return cand[k]; }
+    double p[5];
+    if (a.sff32) {
+        float s[5], e[5];
+        for (int k = 0; k < nc; k++) {
+            const float u = a.kS32 * a.sff32[cand[k]];
+            const float v = a.kD32 * dff[cand[k]];
+            s[k] = u + v;
+        }
+        float mx = s[0];
+        for (int k = 1; k < nc; k++) mx = s[k] > mx ? s[k] : mx;
+        for (int k = 0; k < nc; k++) e[k] = np_expf(s[k] - mx);
+        const float sum = sum_seqf(e, nc);
+        if (!(__builtin_isfinite(sum) && sum != 0.0f)) return -1;
+        for (int k = 0; k < nc; k++) p[k] = (double)(e[k] / sum);
+    } else {
+        double s[5], e[5];
+        for (int k = 0; k < nc; k++) {
+            const float v = a.kD32 * dff[cand[k]];
+            s[k] = a.kS64 * a.sff64[cand[k]] + (double)v;
+        }
+        double mx = s[0];
+        for (int k = 1; k < nc; k++) mx = s[k] > mx ? s[k] : mx;
+        for (int k = 0; k < nc; k++) e[k] = det_exp(s[k] - mx);
+        const double sum = sum_seq(e, nc);
+        if (!(__builtin_isfinite(sum) && sum != 0.0)) return -1;
+        for (int k = 0; k < nc; k++) p[k] = e[k] / sum;
+    }
+    return cand[choice_cdf(p, nc, rng.u())];
+}
+
+// The five moves of agent (x, y) (neighbours U, D, L, R, then stay) with the
+// reference's validity mask (model/ffm_unified.py:296-323).
+template <class OCC>
+__device__ __forceinline__ void moves5(const LearnArgs& a, int x, int y, const OCC& occ, int* coord, int* valid,
+                                       int* inb) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const int nx = k < 4 ? x + kNBx[k] : x, ny = k < 4 ? y + kNBy[k] : y;
+        inb[k] = nx >= 0 && nx < a.H && ny >= 0 && ny < a.W;
+        coord[k] = inb[k] ? nx * a.W + ny : x * a.W + y;
+        const int m = inb[k] ? a.map[coord[k]] : 2;
+        valid[k] = inb[k] && (m == 0 || m == 3) && (k == 4 || !occ(coord[k]));
+    }
+    valid[4] = 1;
+}
+
+__device__ void update_dff_seq(const LearnArgs& a, float* dff, float* B) {
+    const int H = a.H, W = a.W, HW = a.HW;
+    for (int i = 0; i < HW; i++) B[i] = a.c0 * dff[i];
+    for (int x = 0; x < H; x++)
+        for (int y = 0; y < W; y++) {
+            float acc = B[x * W + y];
+            for (int k = 0; k < 4; k++) {
+                const int nx = x + kNBx[k], ny = y + kNBy[k];
+                const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? B[nx * W + ny] : 0.0f;
+                const float t = a.c1 * v;
+                acc = acc + t;
+            }
+            dff[x * W + y] = acc < 1e-4f ? 0.0f : acc;
+        }
+}
+
+__device__ void h_stats_seq(const LearnArgs& a, HStat& hs) {
+    const uint32_t n = *a.Ht.n;
+    hs.has = n > 0;
+    hs.nonfinite = 0;
+    hs.mn = __builtin_inf();
+    hs.mx = -__builtin_inf();
+    for (uint32_t i = 0; i < n; i++) {
+        const double* v = a.Ht.vals + (size_t)a.Ht.order[i] * 5;
+        for (int k = 0; k < 5; k++) {
+            if (!__builtin_isfinite(v[k])) hs.nonfinite = 1;
+            hs.mn = v[k] < hs.mn ? v[k] : hs.mn;
+            hs.mx = v[k] > hs.mx ? v[k] : hs.mx;
+        }
+    }
+}
+
+struct ExactScratch {
+    int *occ, *rq_tgt, *rq_agent, *list, *nxt, *coll, *act, *avalid, *wexit;
+    uint8_t *sm, *smn, *done;
+    float* B;
+    unsigned long long* skey;
+    double* td;
+};
+
+__host__ __device__ inline size_t exact_carve(unsigned char* base, int HW, int A, ExactScratch* s) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        unsigned char* p = base ? base + o : nullptr;
+        o += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    const size_t R = (size_t)A * 4 + 1;
+    ExactScratch t;
+    t.occ = (int*)take((size_t)HW * 4);
+    t.rq_tgt = (int*)take(R * 4);
+    t.rq_agent = (int*)take(R * 4);
+    t.list = (int*)take(R * 4);
+    t.nxt = (int*)take((size_t)A * 4 + 4);
+    t.coll = (int*)take((size_t)A * 4 + 4);
+    t.act = (int*)take((size_t)A * 4 + 4);
+    t.avalid = (int*)take((size_t)A * 4 + 4);
+    t.wexit = (int*)take((size_t)A * 4 + 4);
+    t.sm = (uint8_t*)take((size_t)HW);
+    t.smn = (uint8_t*)take((size_t)HW);
+    t.done = (uint8_t*)take(R);
+    t.B = (float*)take((size_t)HW * 4);
+    t.skey = (unsigned long long*)take((size_t)A * 8 + 8);
+    t.td = (double*)take((size_t)A * 8 + 8);
+    if (s) *s = t;
+    return o;
+}
+
+// ===========================================================================
+// Reference-exact step (one lane, envs in order, MT streams).  Restates
+// model/ffm_ac_core.py:111-236, model/ffm_unified.py:271-606 and
+// model/ffm_actor_only.py:149-409 statement by statement.
+// ===========================================================================
+__global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
+    if (threadIdx.x != 0) return;
+    ExactScratch S;
+    exact_carve(a.scratch, a.HW, a.A, &S);
+    const int W = a.W, HW = a.HW, A = a.A;
+    const int D = a.D;
+    const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
+    const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
+    for (int i = 0; i < HW; i++) S.occ[i] = -1;
+    for (long long e = 0; e < a.E; e++) {
+        uint16_t* pe = a.pos + e * A;
+        float* dff = a.dff_in + e * (long long)HW;
+        DrawMT rng{a.mt_np + e * 625, a.mt_py + e * 625};
+        const int n = a.cnt[e];
+        HStat hs{};
+        if (actor) h_stats_seq(a, hs);
+        for (int c = 0; c < HW; c++) S.sm[c] = a.map[c];
+        for (int i = 0; i < n; i++) { S.sm[pe[i]] = 1; S.occ[pe[i]] = i; }
+        auto occ = [&](int c) { return S.occ[c] >= 0; };
+        int nrq = 0;
+        // ---- decide -------------------------------------------------------
+        for (int i = 0; i < n; i++) {
+            const int x = pe[i] / W, y = pe[i] % W;
+            S.skey[i] = encode(a, SmArray{S.sm}, x, y);
+            S.nxt[i] = pe[i];
+            S.coll[i] = -1; S.act[i] = -1; S.avalid[i] = 0; S.wexit[i] = 0;
+            if (a.variant == kVarAC) {
+                const int T = ac_decide(a, x, y, occ, dff, S.wexit[i], rng);
+                if (T >= 0) { S.rq_tgt[nrq] = T; S.rq_agent[nrq++] = i; }
+                continue;
+            }
+            int coord[5], valid[5], inb[5];
+            moves5(a, x, y, occ, coord, valid, inb);
+            if (a.variant == kVarUnified) {
+                int ex = -1;
+                for (int k = 0; k < 4; k++)
+                    if (inb[k] && a.map[coord[k]] == 3) { ex = k; break; }
+                int k;
+                if (ex >= 0) {
+                    S.wexit[i] = 1;
+                    k = ex;
+                } else if (!actor) {
+                    k = critic_choose(a, coord, valid, dff, rng);
+                } else {
+                    const uint32_t before = *a.Ht.n;
+                    const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
+                    if (hsl < 0) return;
+                    if (*a.Ht.n > before) {                   // a zero row joins min/max (:414-423)
+                        hs.has = 1;
+                        hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
+                        hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
+                    }
+                    k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, false, rng);
+                }
+                S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
+                S.act[i] = k; S.avalid[i] = valid[k];
+            } else {
+                // ffm_actor_only: exit test and decision inside the neighbour loop (:214-355)
+                int ex = -1;
+                for (int j = 0; j < 4; j++) {
+                    if (ex < 0 && inb[j] && a.map[coord[j]] == 3) ex = j;
+                    int k;
+                    if (ex >= 0) {
+                        S.wexit[i] = 1;
+                        k = ex;
+                    } else {
+                        const uint32_t before = *a.Ht.n;
+                        const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
+                        if (hsl < 0) return;
+                        if (*a.Ht.n > before) {
+                            hs.has = 1;
+                            hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
+                            hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
+                        }
+                        k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, true, rng);
+                    }
+                    S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
+                    S.act[i] = k; S.avalid[i] = valid[k];
+                }
+            }
+        }
+        // ---- resolve: dict order, always a winner (random.choice) ---------
+        for (int q = 0; q < nrq; q++) S.done[q] = 0;
+        for (int q = 0; q < nrq; q++) {
+            if (S.done[q]) continue;
+            const int T = S.rq_tgt[q];
+            int m = 0;
+            for (int q2 = q; q2 < nrq; q2++)
+                if (S.rq_tgt[q2] == T) { S.list[m++] = S.rq_agent[q2]; S.done[q2] = 1; }
+            int w;
+            if (m == 1) {
+                w = S.list[0];
+                S.coll[w] = 0;
+            } else {
+                w = S.list[mt_randbelow(rng.py, (uint32_t)m)];
+                for (int z = 0; z < m; z++) S.coll[S.list[z]] = m - 1;
+            }
+            S.nxt[w] = T;
+            dff[pe[w]] += 1.0f;
+        }
+        // ---- learning --------------------------------------------------------
+        for (int c = 0; c < HW; c++) S.smn[c] = a.map[c];
+        for (int i = 0; i < n; i++)
+            if (a.map[S.nxt[i]] != 3) S.smn[S.nxt[i]] = 1;
+        for (int i = 0; i < n; i++) {
+            double r = a.step_penalty;
+            if (S.wexit[i]) r = r + a.exit_reward;
+            if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
+            double vn = 0.0;
+            if (!S.wexit[i]) {
+                const int sn = tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow);
+                if (sn < 0) return;
+                vn = a.V.vals[sn];
+            }
+            const int sv = tab_get(a.V, S.skey[i], a.overflow);
+            if (sv < 0) return;
+            const double v = a.V.vals[sv];
+            const double td = (r + a.gamma * vn) - v;
+            S.td[i] = td;
+            a.V.vals[sv] = v + a.alpha_v * td;
+        }
+        if (post_update) {        // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
+            for (int i = 0; i < n; i++) {
+                double r = a.step_penalty;
+                if (S.wexit[i]) r = r + a.exit_reward;
+                if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
+                double vn = 0.0;
+                if (!S.wexit[i])
+                    vn = a.V.vals[tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow)];
+                const double v = a.V.vals[tab_get(a.V, S.skey[i], a.overflow)];
+                S.td[i] = (r + a.gamma * vn) - v;
+            }
+        }
+        if (actor) {
+            for (int i = 0; i < n; i++) {
+                if (S.act[i] < 0) continue;
+                const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);    // :769-773
+                if (hsl < 0) return;
+                if (!S.avalid[i]) continue;
+                double* hv = a.Ht.vals + (size_t)hsl * 5 + S.act[i];
+                *hv = *hv + a.alpha_h * S.td[i];
+            }
+        }
+        // ---- exit removal, DFF -------------------------------------------------
+        for (int i = 0; i < n; i++) S.occ[pe[i]] = -1;
+        int nn = 0;
+        for (int i = 0; i < n; i++)
+            if (a.map[S.nxt[i]] != 3) pe[nn++] = (uint16_t)S.nxt[i];
+        a.cnt[e] = nn;
+        update_dff_seq(a, dff, S.B);
+        unsigned long long* slot = a.counters + 4 * e;
+        slot[0] += (unsigned long long)n;
+        slot[1] += (unsigned long long)(n - nn);
+        slot[3] += 1;
+        (void)D;
+    }
+}
+
+// ===========================================================================
+// Batched step: one workgroup per env.
+// ===========================================================================
+template <int BS>
+__device__ __forceinline__ int block_scan_flag(bool f, int* ws, int& total) {
+    const unsigned long long m = __ballot(f);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (BS == 64) {
+        total = __popcll(m);
+        return pre;
+    }
+    if (lane == 0) ws[wv] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BS / 64; w++) {
+        const int c = ws[w];
+        off += w < wv ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return off + pre;
+}
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+struct BatchCarve {
+    size_t grid, bits, req, ws, total;
+};
+__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D) {
+    BatchCarve c;
+    size_t o = 0;
+    c.grid = o; o += align16((size_t)HW * 2);
+    c.bits = o; o += align16((size_t)((HW + 31) / 32) * 4);
+    c.req = o; o += align16((size_t)A * D * 2);
+    c.ws = o; o += 64;
+    c.total = o;
+    return c;
+}
+
+template <int BS, int APT, int D>
+__global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int H = a.H, W = a.W, HW = a.HW, A = a.A;
+    const BatchCarve cv = batch_carve(HW, A, D);
+    uint16_t* grid = reinterpret_cast<uint16_t*>(smem + cv.grid);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(smem + cv.bits);
+    uint16_t* req = reinterpret_cast<uint16_t*>(smem + cv.req);
+    int* ws = reinterpret_cast<int*>(smem + cv.ws);
+    const long long e = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint32_t genv = (uint32_t)(a.env_base + e);
+    const int n = a.cnt[e];
+    const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
+    const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
+    const float* dff = a.dff_in + e * (long long)HW;
+
+    for (int c = tid; c < HW; c += BS) grid[c] = kNone16;
+    for (int c = tid; c < (HW + 31) / 32; c += BS) bits[c] = 0u;
+    for (int c = tid; c < A * D; c += BS) req[c] = kNone16;
+    __syncthreads();
+    int p[APT];
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = tid + j * BS;
+        p[j] = i < n ? a.pos[e * A + i] : 0;
+        if (i < n) grid[p[j]] = (uint16_t)i;
+    }
+    HStat hs{};
+    if (actor) {
+        hs.has = (int)a.hstat[0];
+        hs.nonfinite = (int)a.hstat[1];
+        hs.mn = a.hstat[2];
+        hs.mx = a.hstat[3];
+    }
+    __syncthreads();
+    const SmGrid smc{a.map, grid};
+    auto occ = [&](int c) { return grid[c] != kNone16; };
+
+    // ---- decide --------------------------------------------------------------
+    unsigned long long skey[APT];
+    int act[APT], avalid[APT], wexit[APT], hsl[APT];
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = tid + j * BS;
+        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
+        if (i >= n) continue;
+        const int x = p[j] / W, y = p[j] - (p[j] / W) * W;
+        skey[j] = encode(a, smc, x, y);
+        if (a.variant == kVarAC) {
+            DrawPh rng(a, genv, (uint32_t)i);
+            const int T = ac_decide(a, x, y, occ, dff, wexit[j], rng);
+            if (T >= 0) req[i] = (uint16_t)T;
+            continue;
+        }
+        int coord[5], valid[5], inb[5];
+        moves5(a, x, y, occ, coord, valid, inb);
+        if (D == 1) {
+            int ex = -1;
+            for (int k = 0; k < 4; k++)
+                if (inb[k] && a.map[coord[k]] == 3) { ex = k; break; }
+            int k;
+            if (ex >= 0) {
+                wexit[j] = 1;
+                k = ex;
+            } else if (!actor) {
+                DrawPh rng(a, genv, (uint32_t)i);
+                k = critic_choose(a, coord, valid, dff, rng);
+            } else {
+                DrawPh rng(a, genv, (uint32_t)i);
+                hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+                if (hsl[j] < 0) { k = 4; }
+                else k = actor_choose(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, false, rng);
+            }
+            req[i] = (uint16_t)coord[k];
+            act[j] = k; avalid[j] = valid[k];
+        } else {
+            int ex = -1;
+            for (int d = 0; d < 4; d++) {
+                if (ex < 0 && inb[d] && a.map[coord[d]] == 3) ex = d;
+                int k;
+                if (ex >= 0) {
+                    wexit[j] = 1;
+                    k = ex;
+                } else {
+                    DrawPh rng(a, genv, (uint32_t)(i * 4 + d));
+                    if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+                    if (hsl[j] < 0) k = 4;
+                    else k = actor_choose(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, true, rng);
+                }
+                req[i * D + d] = (uint16_t)coord[k];
+                act[j] = k; avalid[j] = valid[k];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- resolve -----------------------------------------------------------------
+    // Requesters of a target stand on it or next to it; a target's owner is its
+    // smallest request seq (= the reference's dict order); every member draws
+    // the winner rank from the owner's stream itself.
+    int nxt[APT], coll[APT], wins[APT];
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = tid + j * BS;
+        nxt[j] = p[j]; coll[j] = -1; wins[j] = 0;
+        if (i >= n) continue;
+        int best_owner = -1, best_won_owner = -1;
+        for (int d = 0; d < D; d++) {
+            const int T = req[i * D + d];
+            if (T == kNone16) continue;
+            const int mine = i * D + d;
+            const int tx = T / W, ty = T - (T / W) * W;
+            int m = 0, owner = 0x7FFFFFFF, rank = 0;
+            for (int c5 = 0; c5 < 5; c5++) {
+                const int cx = c5 < 4 ? tx + kNBx[c5] : tx, cy = c5 < 4 ? ty + kNBy[c5] : ty;
+                if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
+                const int b = grid[cx * W + cy];
+                if (b == kNone16) continue;
+                for (int d2 = 0; d2 < D; d2++) {
+                    if (req[b * D + d2] != T) continue;
+                    const int sq = b * D + d2;
+                    m++;
+                    owner = sq < owner ? sq : owner;
+                    rank += sq < mine ? 1 : 0;
+                }
+            }
+            int w = 0;
+            if (m > 1) {
+                PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)owner, kPurFriction);
+                w = (int)ps.randbelow((uint32_t)m);
+            }
+            if (owner > best_owner) { best_owner = owner; coll[j] = m == 1 ? 0 : m - 1; }
+            if (rank == w) {
+                wins[j]++;
+                if (owner > best_won_owner) { best_won_owner = owner; nxt[j] = T; }
+            }
+        }
+    }
+    // deposits at the winners' own cells (distinct per agent: no races)
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        if (wins[j] == 0) continue;
+        float* c = a.dff_in + e * (long long)HW + p[j];
+        float v = *c;
+        for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
+        *c = v;
+        if (a.map[nxt[j]] != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
+    }
+#pragma unroll
+    for (int j = 0; j < APT; j++) {        // non-movers keep their cells in the next state map
+        const int i = tid + j * BS;
+        if (i < n && wins[j] == 0 && a.map[nxt[j]] != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
+    }
+    __syncthreads();
+
+    // ---- learning (TD(0) critic, actor) --------------------------------------------------
+    const SmBits smn{a.map, bits};
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = tid + j * BS;
+        if (i >= n) continue;
+        double r = a.step_penalty;
+        if (wexit[j]) r = r + a.exit_reward;
+        if (coll[j] >= 0) r = r + (double)coll[j] * a.collision_penalty;
+        int sn = -1;
+        double vn = 0.0;
+        if (!wexit[j]) {
+            const int nx = nxt[j] / W, ny = nxt[j] - (nxt[j] / W) * W;
+            sn = tab_get(a.V, encode(a, smn, nx, ny), a.overflow);
+            vn = sn >= 0 ? a.V.vals[sn] : 0.0;
+        }
+        const int sv = tab_get(a.V, skey[j], a.overflow);
+        if (sv < 0) continue;
+        const double td = (r + a.gamma * vn) - a.V.vals[sv];
+        acc_add(a.V.acc + sv, fx(a.alpha_v * td));
+        if (!actor) continue;
+        if (act[j] < 0) continue;
+        if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+        if (hsl[j] < 0) continue;
+        if (post_update) {
+            LearnRec rc;
+            rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
+            a.recs[e * A + i] = rc;
+        } else if (avalid[j]) {
+            acc_add(a.Ht.acc + (size_t)hsl[j] * 5 + act[j], fx(a.alpha_h * td));
+        }
+    }
+
+    // ---- exit removal (order preserving), counters ---------------------------------------
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = tid + j * BS;
+        const bool keep = i < n && a.map[nxt[j]] != 3;
+        int tot;
+        const int off = block_scan_flag<BS>(keep, ws, tot);
+        if (keep) a.pos[e * A + base + off] = (uint16_t)nxt[j];
+        base += tot;
+    }
+    __syncthreads();     // deposits visible to the whole workgroup before the stencil
+
+    // ---- update_dff (model/ffm_unified.py:779-798) into the other buffer ---------------------
+    float* out = a.dff_out + e * (long long)HW;
+    for (int c = tid; c < HW; c += BS) {
+        const int x = c / W, y = c - (c / W) * W;
+        float acc = a.c0 * dff[c];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int nx = x + kNBx[k], ny = y + kNBy[k];
+            const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? a.c0 * dff[nx * W + ny] : 0.0f;
+            const float t = a.c1 * v;
+            acc = acc + t;
+        }
+        out[c] = acc < 1e-4f ? 0.0f : acc;
+    }
+    if (tid == 0) {
+        a.cnt[e] = base;
+        a.nstart[e] = n;
+        const int st = a.ep_steps[e] + 1;
+        a.ep_steps[e] = st;
+        a.done[e] = a.auto_reset && (base == 0 || (a.max_steps > 0 && st >= a.max_steps)) ? 1 : 0;
+        unsigned long long* slot = a.counters + 4 * e;
+        slot[0] += (unsigned long long)n;
+        slot[1] += (unsigned long long)(n - base);
+        slot[3] += 1;
+    }
+}
+
+// ===========================================================================
+// Table upkeep.
+// ===========================================================================
+__global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
+    __shared__ double smn[4], smx[4];
+    __shared__ int snf[4];
+    const uint32_t n = *a.Ht.n;
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    int nf = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const double* v = a.Ht.vals + (size_t)a.Ht.order[i] * 5;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            nf |= !__builtin_isfinite(v[k]);
+            mn = v[k] < mn ? v[k] : mn;
+            mx = v[k] > mx ? v[k] : mx;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
+        mn = a2 < mn ? a2 : mn;
+        mx = b2 > mx ? b2 : mx;
+        nf |= __shfl_xor(nf, o);
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smn[wv] = mn; smx[wv] = mx; snf[wv] = nf; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            mn = smn[w] < mn ? smn[w] : mn;
+            mx = smx[w] > mx ? smx[w] : mx;
+            nf |= snf[w];
+        }
+        double* o = a.hpart + blockIdx.x * 4;
+        o[0] = n > 0 ? 1.0 : 0.0;
+        o[1] = (double)nf;
+        o[2] = mn;
+        o[3] = mx;
+    }
+}
+
+__global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a) {
+    if (threadIdx.x != 0) return;
+    double mn = __builtin_inf(), mx = -__builtin_inf(), nf = 0.0;
+    for (int b = 0; b < kHstatBlocks; b++) {
+        const double* o = a.hpart + b * 4;
+        mn = o[2] < mn ? o[2] : mn;
+        mx = o[3] > mx ? o[3] : mx;
+        nf = o[1] != 0.0 ? 1.0 : nf;
+    }
+    a.hstat[0] = *a.Ht.n > 0 ? 1.0 : 0.0;
+    a.hstat[1] = nf;
+    a.hstat[2] = mn;
+    a.hstat[3] = mx;
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T) {
+    const uint32_t n = *T.n;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const size_t s = (size_t)T.order[i] * WIDTH;
+#pragma unroll
+        for (int k = 0; k < WIDTH; k++) {
+            const long long q = T.acc[s + k];
+            if (q != 0) {
+                T.vals[s + k] = T.vals[s + k] + (double)q * (1.0 / kFxOne);
+                T.acc[s + k] = 0;
+            }
+        }
+    }
+}
+
+// _get_td_errors with the updated V, then the actor (model/ffm_unified.py:559-598).
+__global__ __launch_bounds__(64) void learn_post_kernel(LearnArgs a) {
+    const long long e = blockIdx.x;
+    const int n = a.nstart[e];
+    for (int i = threadIdx.x; i < n; i += 64) {
+        const LearnRec rc = a.recs[e * a.A + i];
+        if (rc.k < 0) continue;
+        const double vn = rc.snv >= 0 ? a.V.vals[rc.snv] : 0.0;
+        const double td = (rc.r + a.gamma * vn) - a.V.vals[rc.sv];
+        acc_add(a.Ht.acc + (size_t)rc.hslot * 5 + rc.k, fx(a.alpha_h * td));
+    }
+}
+
+__global__ __launch_bounds__(256) void learn_fill_default_kernel(LearnTable T, double v) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i <= T.mask; i += (size_t)gridDim.x * 256)
+        if (T.keys[i] == kEmptyKey) T.vals[i] = v;
+}
+
+// Philox placement: the N free cells with the smallest
+// (key_j, j), in that order.  Candidates (all F, or those under a threshold
+// chosen so that N <= expected count << capacity) are bitonic-sorted in LDS.
+constexpr int kResetBS = 256;
+constexpr int kResetCap = 16384;
+
+__global__ __launch_bounds__(kResetBS) void learn_reset_kernel(LearnArgs a, int all) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
+    __shared__ int cnt;
+    const long long e = blockIdx.x;
+    if (!all && !a.done[e]) return;
+    const int tid = threadIdx.x, F = a.F, N = a.N;
+    const uint32_t genv = (uint32_t)(a.env_base + e);
+    const bool take_all = F <= kResetCap;
+    unsigned long long T = 0xFFFFFFFFull;
+    if (!take_all) {
+        const unsigned long long want = (unsigned long long)N + (unsigned long long)(kResetCap - N) / 2;
+        T = (want << 32) / (unsigned long long)F;
+    }
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    for (int j = tid; j < F; j += kResetBS) {
+        const uint32_t k = philox(make_uint4(a.t, genv, (uint32_t)j, kPurReset << 28), a.key0, a.key1).x;
+        if (take_all) {
+            keys[j] = ((unsigned long long)k << 32) | (unsigned)j;
+        } else if ((unsigned long long)k <= T) {
+            const int slot = atomicAdd(&cnt, 1);
+            if (slot < kResetCap) keys[slot] = ((unsigned long long)k << 32) | (unsigned)j;
+        }
+    }
+    __syncthreads();
+    int C = take_all ? F : cnt;
+    if (C > kResetCap || C < N) {
+        if (tid == 0) atomicOr(a.overflow, 2);
+        C = C > kResetCap ? kResetCap : C;
+    }
+    int P = 1;
+    while (P < C) P <<= 1;
+    for (int j = C + tid; j < P; j += kResetBS) keys[j] = ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = tid; i < P; i += kResetBS) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const unsigned long long x = keys[i], y = keys[l];
+                    const bool up = (i & k) == 0;
+                    if ((x > y) == up) { keys[i] = y; keys[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    const int NN = N < C ? N : C;
+    for (int r = tid; r < NN; r += kResetBS) a.pos[e * a.A + r] = a.free_cells[(int)(keys[r] & 0xFFFFFFFFu)];
+    float* d = a.dff_in + e * (long long)a.HW;
+    for (int c = tid; c < a.HW; c += kResetBS) d[c] = 0.0f;
+    if (tid == 0) {
+        a.cnt[e] = NN;
+        a.ep_steps[e] = 0;
+        a.done[e] = 0;
+        if (!all) {
+            a.episodes[e] += 1;
+            a.counters[4 * e + 2] += 1;
+        }
+    }
+}
+
+// Insert keys in the given order (one lane: the insertion order is the dict
+// order the reference's get_v_table / get_h_table return) and set their values.
+__global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int width, const unsigned long long* keys,
+                                                          const double* vals, long long n, int* overflow) {
+    if (threadIdx.x != 0) return;
+    for (long long i = 0; i < n; i++) {
+        const int s = tab_get(T, keys[i], overflow);
+        if (s < 0) return;
+        for (int k = 0; k < width; k++) T.vals[(size_t)s * width + k] = vals[i * width + k];
+    }
+}
+
+template <int BS, int APT, int D>
+hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
+    const size_t smem = batch_carve(a.HW, a.A, D).total;
+    if (smem > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&learn_batch_kernel<BS, APT, D>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    learn_batch_kernel<BS, APT, D><<<dim3((unsigned)a.E), dim3(BS), smem, s>>>(a);
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
+    const int A = a.A;
+    if (A <= 64) return launch_batch_t<64, 1, D>(a, s);
+    if (A <= 256) return launch_batch_t<256, 1, D>(a, s);
+    if (A <= 1024) return launch_batch_t<1024, 1, D>(a, s);
+    if (A <= 2048) return launch_batch_t<1024, 2, D>(a, s);
+    if (A <= 4096) return launch_batch_t<1024, 4, D>(a, s);
+    if (A <= 8192) return launch_batch_t<1024, 8, D>(a, s);
+    return launch_batch_t<1024, 16, D>(a, s);
+}
+
+}  // namespace
+
+size_t learn_exact_scratch_bytes(int HW, int A) { return exact_carve(nullptr, HW, A, nullptr); }
+
+int learn_batch_block_size(int A) { return A <= 64 ? 64 : A <= 256 ? 256 : 1024; }
+
+size_t learn_batch_smem_bytes(int HW, int A, int D) { return batch_carve(HW, A, D).total; }
+
+bool learn_batch_supported(int HW, int A, int D) {
+    return A <= 16384 && learn_batch_smem_bytes(HW, A, D) <= 160 * 1024;
+}
+
+hipError_t launch_learn_hstat(const LearnArgs& a, hipStream_t s) {
+    learn_hstat_partial<<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a);
+    learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_exact(const LearnArgs& a, hipStream_t s) {
+    learn_exact_kernel<<<dim3(1), dim3(64), 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s) {
+    return a.D == 4 ? launch_batch_d<4>(a, s) : launch_batch_d<1>(a, s);
+}
+
+hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s) {
+    if (v) learn_apply_kernel<1><<<dim3(512), dim3(256), 0, s>>>(a.V);
+    if (h) learn_apply_kernel<5><<<dim3(512), dim3(256), 0, s>>>(a.Ht);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s) {
+    learn_post_kernel<<<dim3((unsigned)a.E), dim3(64), 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
+    int P = 1;
+    while (P < (a.F < kResetCap ? a.F : kResetCap)) P <<= 1;
+    const size_t smem = (size_t)P * 8;
+    if (smem > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&learn_reset_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    learn_reset_kernel<<<dim3((unsigned)a.E), dim3(kResetBS), smem, s>>>(a, all ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_import(const LearnTable& T, int width, const unsigned long long* keys, const double* vals,
+                              long long n, int* overflow, hipStream_t s) {
+    learn_import_kernel<<<dim3(1), dim3(64), 0, s>>>(T, width, keys, vals, n, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s) {
+    learn_fill_default_kernel<<<dim3(1024), dim3(256), 0, s>>>(a.V, a.v_default);
+    return hipGetLastError();
+}
+
+}  // namespace ffm

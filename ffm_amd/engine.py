@@ -16,7 +16,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FFM_LIB_PATH") or os.path.join(_HERE, "_lib", "libffm_amd.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, E_INVALID, E_HIP, E_NOMEM, E_UNSUPPORTED = 0, -1, -2, -3, -4
 VARIANT_CORE = 0
 RNG_PHILOX, RNG_MT = 0, 1
@@ -28,7 +28,17 @@ EXPORTED = [
     "ffm_engine_get_state", "ffm_engine_set_mt_state", "ffm_engine_get_mt_state",
     "ffm_engine_get_counters", "ffm_engine_device_buffers", "ffm_engine_get_step_index",
     "ffm_engine_set_step_index", "ffm_np_expf_device",
+    "ffm_learner_create", "ffm_learner_destroy", "ffm_learner_reset", "ffm_learner_step",
+    "ffm_learner_set_state", "ffm_learner_get_state", "ffm_learner_get_episodes",
+    "ffm_learner_set_mt_state", "ffm_learner_get_mt_state", "ffm_learner_get_counters",
+    "ffm_learner_set_epsilon", "ffm_learner_set_v_default", "ffm_learner_table_size",
+    "ffm_learner_export_table", "ffm_learner_import_table", "ffm_learner_get_step_index",
+    "ffm_learner_set_step_index",
 ]
+
+VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY = 1, 2, 3
+LEARN_MODES = {"critic_only": 0, "actor_only": 1, "both": 2}
+TABLE_V, TABLE_H = 0, 1
 
 
 class EngineDesc(C.Structure):
@@ -41,6 +51,17 @@ class EngineDesc(C.Structure):
         ("n_envs", C.c_int64), ("agent_capacity", C.c_int32), ("n_agents", C.c_int32),
         ("rng_mode", C.c_int32), ("auto_reset", C.c_int32), ("seed", C.c_uint64),
         ("env_base", C.c_int64), ("device", C.c_int32), ("envs_per_block", C.c_int32),
+    ]
+
+
+class LearnDesc(C.Structure):
+    _fields_ = [
+        ("mode", C.c_int32), ("k_A", C.c_double),
+        ("alpha_v", C.c_double), ("alpha_h", C.c_double), ("gamma", C.c_double),
+        ("exit_reward", C.c_double), ("step_penalty", C.c_double), ("collision_penalty", C.c_double),
+        ("epsilon", C.c_double), ("v_default", C.c_double),
+        ("block_size", C.c_int32), ("max_steps", C.c_int32),
+        ("log2_v_capacity", C.c_int32), ("log2_h_capacity", C.c_int32),
     ]
 
 
@@ -82,6 +103,23 @@ def load_library():
     L.ffm_engine_get_step_index.argtypes = [P, C.POINTER(C.c_uint32)]
     L.ffm_engine_set_step_index.argtypes = [P, C.c_uint32]
     L.ffm_np_expf_device.argtypes = [P, P, i64, P]
+    L.ffm_learner_create.argtypes = [C.POINTER(EngineDesc), C.POINTER(LearnDesc), C.POINTER(P)]
+    L.ffm_learner_destroy.argtypes = [P]
+    L.ffm_learner_reset.argtypes = [P, P]
+    L.ffm_learner_step.argtypes = [P, i32, P]
+    L.ffm_learner_set_state.argtypes = [P, i64, i64, P, P, P, P]
+    L.ffm_learner_get_state.argtypes = [P, i64, i64, P, P, P, P]
+    L.ffm_learner_get_episodes.argtypes = [P, i64, i64, P, P, P]
+    L.ffm_learner_set_mt_state.argtypes = [P, i64, P, i32, P, i32, P]
+    L.ffm_learner_get_mt_state.argtypes = [P, i64, P, C.POINTER(i32), P, C.POINTER(i32), P]
+    L.ffm_learner_get_counters.argtypes = [P, P, P]
+    L.ffm_learner_set_epsilon.argtypes = [P, C.c_double]
+    L.ffm_learner_set_v_default.argtypes = [P, C.c_double, P]
+    L.ffm_learner_table_size.argtypes = [P, i32, C.POINTER(i64), P]
+    L.ffm_learner_export_table.argtypes = [P, i32, P, P, i64, C.POINTER(i64), P]
+    L.ffm_learner_import_table.argtypes = [P, i32, P, P, i64, P]
+    L.ffm_learner_get_step_index.argtypes = [P, C.POINTER(C.c_uint32)]
+    L.ffm_learner_set_step_index.argtypes = [P, C.c_uint32]
     for name in EXPORTED:
         if name != "ffm_last_error":
             getattr(L, name).restype = C.c_int
@@ -294,3 +332,234 @@ class Engine:
 def np_expf_device(x_dev_ptr: int, y_dev_ptr: int, n: int, stream=None):
     L = load_library()
     _check(L.ffm_np_expf_device(x_dev_ptr, y_dev_ptr, n, _stream_handle(stream)))
+
+
+# ---------------------------------------------------------------------------
+# Learning variants: ffm_ac_core, ffm_unified, ffm_actor_only
+# ---------------------------------------------------------------------------
+# Class defaults of the reference, merged under the caller's params the way
+# the reference merges them ({**defaults, **params}).
+LEARN_DEFAULTS = {
+    # model/ffm_ac_core.py:10-23
+    "ac": {"k_S": 10, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann", "alpha_v": 0.1,
+           "gamma": 0.95, "exit_reward": 100.0, "step_penalty": 0.0, "collision_penalty": -1.0,
+           "block_size": 3},
+    # model/ffm_unified.py:36-53
+    "unified": {"k_S": 10, "k_D": 1, "k_A": 10, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann",
+                "alpha_v": 0.1, "gamma": 0.95, "exit_reward": 100.0, "step_penalty": 0.0,
+                "collision_penalty": -1.0, "block_size": 5, "alpha_h": 0.1, "epsilon": 0.0},
+    # model/ffm_actor_only.py:24-40 (block size 5 is hard-coded at :143)
+    "actor_only": {"k_D": 1, "k_A": 10, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann",
+                   "alpha_v": 0.1, "gamma": 0.95, "exit_reward": 100.0, "step_penalty": 0.0,
+                   "collision_penalty": -1.0, "alpha_h": 0.1, "epsilon": 0.0},
+}
+_LEARN_VARIANTS = {"ac": VARIANT_AC, "unified": VARIANT_UNIFIED, "actor_only": VARIANT_ACTOR_ONLY}
+
+
+class Learner:
+    """E environments of one learning model class plus its shared V / H tables.
+
+    variant: "ac" (model/ffm_ac_core.py), "unified" (model/ffm_unified.py, with
+    ``mode`` critic_only / actor_only / both) or "actor_only"
+    (model/ffm_actor_only.py).  rng="mt" reproduces the reference bit for bit
+    (per-env MT19937 streams, agents and table updates in the reference's
+    order); rng="philox" is the batched production step.
+    Table keys are packed u64 (ffm_amd/learn_keys.py).
+    """
+
+    def __init__(self, map_array, sff, variant: str, n_envs: int, n_agents: int,
+                 agent_capacity: int | None = None, mode: str | None = None, params: dict | None = None,
+                 rng: str = "philox", seed: int = 42, auto_reset: bool = True, max_steps: int = 0,
+                 env_base: int = 0, device: int = 0, log2_v_capacity: int = 0, log2_h_capacity: int = 0):
+        L = load_library()
+        if variant not in _LEARN_VARIANTS:
+            raise ValueError(f"variant must be one of {sorted(_LEARN_VARIANTS)}")
+        p = {**LEARN_DEFAULTS[variant], **(params or {})}
+        self.params, self.variant = p, variant
+        self.mode = mode or ("actor_only" if variant == "actor_only" else "critic_only")
+        if variant == "unified" and self.mode not in LEARN_MODES:
+            raise ValueError(f"learning_mode must be one of {list(LEARN_MODES)}")
+        self.map = np.ascontiguousarray(map_array, dtype=np.uint8)
+        if self.map.ndim != 2:
+            raise ValueError("map must be 2-D")
+        self.H, self.W = self.map.shape
+        sff = np.asarray(sff)
+        if sff.shape != self.map.shape:
+            raise ValueError("sff shape must equal map shape")
+        if sff.dtype == np.float32:
+            self.sff, sdt = np.ascontiguousarray(sff), SFF_F32
+        else:
+            self.sff, sdt = np.ascontiguousarray(sff, dtype=np.float64), SFF_F64
+        self.n_envs, self.n_agents = int(n_envs), int(n_agents)
+        self.A = int(agent_capacity if agent_capacity is not None else max(1, n_agents))
+        self.rng = rng
+        d = EngineDesc()
+        d.abi_version = ABI_VERSION
+        d.variant = _LEARN_VARIANTS[variant]
+        d.H, d.W = self.H, self.W
+        d.map, d.sff, d.sff_dtype = self.map.ctypes.data, self.sff.ctypes.data, sdt
+        d.neighborhood = 4 if p.get("neighborhood", "neumann") == "neumann" else 8
+        d.k_S, d.k_D = float(p.get("k_S", 0.0)), float(p["k_D"])
+        d.diffuse, d.decay = float(p["diffuse"]), float(p["decay"])
+        d.n_envs, d.agent_capacity, d.n_agents = self.n_envs, self.A, self.n_agents
+        d.rng_mode = {"philox": RNG_PHILOX, "mt": RNG_MT}[rng]
+        d.auto_reset = int(bool(auto_reset))
+        d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        d.env_base, d.device = int(env_base), int(device)
+        ld = LearnDesc()
+        ld.mode = LEARN_MODES.get(self.mode, 1) if variant == "unified" else (1 if variant == "actor_only" else 0)
+        ld.k_A = float(p.get("k_A", 0.0))
+        ld.alpha_v, ld.alpha_h, ld.gamma = float(p["alpha_v"]), float(p.get("alpha_h", 0.0)), float(p["gamma"])
+        ld.exit_reward, ld.step_penalty = float(p["exit_reward"]), float(p["step_penalty"])
+        ld.collision_penalty = float(p["collision_penalty"])
+        ld.epsilon = float(min(max(float(p.get("epsilon", 0.0)), 0.0), 1.0))
+        ld.v_default = 0.0
+        ld.block_size = int(p.get("block_size", 5))
+        ld.max_steps = int(max_steps)
+        ld.log2_v_capacity, ld.log2_h_capacity = int(log2_v_capacity), int(log2_h_capacity)
+        h = C.c_void_p()
+        _check(L.ffm_learner_create(C.byref(d), C.byref(ld), C.byref(h)))
+        self._h, self._L = h, L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ffm_learner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- stepping ------------------------------------------------------------------
+    def reset(self, stream=None):
+        _check(self._L.ffm_learner_reset(self._h, _stream_handle(stream)))
+
+    def step(self, n_steps: int = 1, stream=None):
+        _check(self._L.ffm_learner_step(self._h, int(n_steps), _stream_handle(stream)))
+
+    def set_epsilon(self, eps: float):
+        _check(self._L.ffm_learner_set_epsilon(self._h, float(eps)))
+
+    def set_v_default(self, v: float, stream=None):
+        _check(self._L.ffm_learner_set_v_default(self._h, float(v), _stream_handle(stream)))
+
+    # -- state -----------------------------------------------------------------------
+    def get_state(self, env0: int = 0, n: int | None = None, stream=None):
+        n = self.n_envs - env0 if n is None else n
+        pos = np.empty((n, self.A), np.uint16)
+        cnt = np.empty(n, np.int32)
+        dff = np.empty((n, self.H, self.W), np.float32)
+        _check(self._L.ffm_learner_get_state(self._h, env0, n, _ptr(pos), _ptr(cnt), _ptr(dff),
+                                             _stream_handle(stream)))
+        return pos, cnt, dff
+
+    def set_state(self, env0: int = 0, positions=None, counts=None, dff=None, stream=None):
+        n = None
+        arrs = []
+        for a, dt in ((positions, np.uint16), (counts, np.int32), (dff, np.float32)):
+            if a is None:
+                arrs.append(None)
+                continue
+            a = np.ascontiguousarray(a, dtype=dt)
+            n = a.shape[0] if n is None else n
+            if a.shape[0] != n:
+                raise ValueError("inconsistent env counts")
+            arrs.append(a)
+        if n is None:
+            return
+        if arrs[0] is not None and arrs[0].shape[1:] != (self.A,):
+            raise ValueError(f"positions must be [n, {self.A}]")
+        if arrs[2] is not None and arrs[2].reshape(n, -1).shape[1] != self.H * self.W:
+            raise ValueError("dff must be [n, H, W]")
+        _check(self._L.ffm_learner_set_state(self._h, env0, n, _ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]),
+                                             _stream_handle(stream)))
+
+    def episodes(self, env0: int = 0, n: int | None = None, stream=None):
+        n = self.n_envs - env0 if n is None else n
+        eps = np.empty(n, np.int32)
+        st = np.empty(n, np.int32)
+        _check(self._L.ffm_learner_get_episodes(self._h, env0, n, _ptr(eps), _ptr(st), _stream_handle(stream)))
+        return eps, st
+
+    def set_mt_state(self, env: int, np_key, np_pos: int, py_key, py_pos: int, stream=None):
+        nk = np.ascontiguousarray(np_key, dtype=np.uint32)
+        pk = np.ascontiguousarray(py_key, dtype=np.uint32)
+        if nk.size != 624 or pk.size != 624:
+            raise ValueError("MT19937 keys must have 624 words")
+        _check(self._L.ffm_learner_set_mt_state(self._h, env, _ptr(nk), int(np_pos), _ptr(pk), int(py_pos),
+                                                _stream_handle(stream)))
+
+    def get_mt_state(self, env: int, stream=None):
+        nk = np.empty(624, np.uint32)
+        pk = np.empty(624, np.uint32)
+        npos, ppos = C.c_int32(), C.c_int32()
+        _check(self._L.ffm_learner_get_mt_state(self._h, env, _ptr(nk), C.byref(npos), _ptr(pk), C.byref(ppos),
+                                                _stream_handle(stream)))
+        return nk, int(npos.value), pk, int(ppos.value)
+
+    def load_rng_from(self, env: int, np_rs: np.random.RandomState | None = None,
+                      py_r: _pyrandom.Random | None = None):
+        st = (np_rs if np_rs is not None else np.random.mtrand._rand).get_state(legacy=True)
+        ps = (py_r if py_r is not None else _pyrandom._inst).getstate()
+        self.set_mt_state(env, st[1], st[2], np.asarray(ps[1][:624], np.uint32), ps[1][624])
+
+    def store_rng_to(self, env: int, np_rs: np.random.RandomState | None = None,
+                     py_r: _pyrandom.Random | None = None):
+        nk, npos, pk, ppos = self.get_mt_state(env)
+        rs = np_rs if np_rs is not None else np.random.mtrand._rand
+        st = rs.get_state(legacy=True)
+        rs.set_state(("MT19937", nk, npos, st[3], st[4]))
+        r = py_r if py_r is not None else _pyrandom._inst
+        ps = r.getstate()
+        r.setstate((ps[0], tuple(int(w) for w in pk) + (ppos,), ps[2]))
+
+    # -- tables ------------------------------------------------------------------------
+    def table_size(self, which: str = "V", stream=None) -> int:
+        n = C.c_int64()
+        _check(self._L.ffm_learner_table_size(self._h, TABLE_V if which == "V" else TABLE_H, C.byref(n),
+                                              _stream_handle(stream)))
+        return int(n.value)
+
+    def export_table(self, which: str = "V", stream=None):
+        """(keys u64 [n], values f64 [n] or [n, 5]) in insertion order."""
+        w = TABLE_V if which == "V" else TABLE_H
+        width = 1 if w == TABLE_V else 5
+        cap = self.table_size(which, stream)
+        keys = np.empty(max(cap, 1), np.uint64)
+        vals = np.empty((max(cap, 1), width), np.float64)
+        n = C.c_int64()
+        _check(self._L.ffm_learner_export_table(self._h, w, _ptr(keys), _ptr(vals), cap, C.byref(n),
+                                                _stream_handle(stream)))
+        n = int(n.value)
+        return keys[:n], (vals[:n, 0] if width == 1 else vals[:n])
+
+    def import_table(self, which: str, keys, vals, stream=None):
+        w = TABLE_V if which == "V" else TABLE_H
+        width = 1 if w == TABLE_V else 5
+        k = np.ascontiguousarray(keys, dtype=np.uint64)
+        v = np.ascontiguousarray(vals, dtype=np.float64).reshape(len(k), width)
+        _check(self._L.ffm_learner_import_table(self._h, w, _ptr(k), _ptr(v), len(k), _stream_handle(stream)))
+
+    # -- telemetry -----------------------------------------------------------------------
+    def counters(self, stream=None) -> dict:
+        c = np.zeros(4, np.uint64)
+        _check(self._L.ffm_learner_get_counters(self._h, _ptr(c), _stream_handle(stream)))
+        return {"agent_steps": int(c[0]), "exits": int(c[1]), "resets": int(c[2]), "steps": int(c[3])}
+
+    @property
+    def step_index(self) -> int:
+        t = C.c_uint32()
+        _check(self._L.ffm_learner_get_step_index(self._h, C.byref(t)))
+        return int(t.value)
+
+    @step_index.setter
+    def step_index(self, t: int):
+        _check(self._L.ffm_learner_set_step_index(self._h, int(t) & 0xFFFFFFFF))

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FFM_ABI_VERSION 1
+#define FFM_ABI_VERSION 2
 
 enum {
     FFM_OK = 0,
@@ -50,7 +50,10 @@ enum {
 
 /* Which model class the engine steps. */
 enum {
-    FFM_VARIANT_CORE = 0      /* model/ffm_core.py FloorFieldModel */
+    FFM_VARIANT_CORE = 0,      /* model/ffm_core.py FloorFieldModel              (ffm_engine_*)  */
+    FFM_VARIANT_AC = 1,        /* model/ffm_ac_core.py FloorFieldModel           (ffm_learner_*) */
+    FFM_VARIANT_UNIFIED = 2,   /* model/ffm_unified.py FloorFieldModelUnified    (ffm_learner_*) */
+    FFM_VARIANT_ACTOR_ONLY = 3 /* model/ffm_actor_only.py FloorFieldModelActorOnly (ffm_learner_*) */
 };
 
 /* Where the random draws come from. */
@@ -135,6 +138,82 @@ int ffm_engine_device_buffers(ffm_engine* eng, ffm_device_buffers* out);
 /* Step counter (Philox key component); settable for replay. */
 int ffm_engine_get_step_index(ffm_engine* eng, uint32_t* t);
 int ffm_engine_set_step_index(ffm_engine* eng, uint32_t t);
+
+/* ---- learning variants (ffm_ac_core / ffm_unified / ffm_actor_only) ----
+ *
+ * A learner owns E envs of one learning model class plus its V (state value)
+ * and H (action preference) tables, shared by all E envs.  Reference entry
+ * points each function replaces:
+ *   ffm_learner_create        <- __init__   model/ffm_ac_core.py:9-38, model/ffm_unified.py:27-129,
+ *                                           model/ffm_actor_only.py:21-79
+ *   ffm_learner_reset         <- reset()    model/ffm_ac_core.py:319-325, model/ffm_unified.py:800-812
+ *   ffm_learner_step          <- step()     model/ffm_ac_core.py:111-236, model/ffm_unified.py:271-606,
+ *                                           model/ffm_actor_only.py:149-409
+ *   ffm_learner_{export,import}_table <- get_v_table / set_v_table / get_h_table and the
+ *                                        pretrained-critic loaders (model/ffm_unified.py:84-110)
+ *   ffm_learner_table_size    <- get_v_table_size / get_h_table_size
+ *   ffm_learner_set_epsilon   <- set_epsilon (model/ffm_unified.py:859-867)
+ *
+ * rng_mode FFM_RNG_MT: the reference's semantics bit for bit (per-env NumPy +
+ * CPython streams, agents and table updates in the reference's order; envs are
+ * stepped one after another).  FFM_RNG_PHILOX: the batched production step
+ * (DESIGN.md section 9): all envs in parallel against the tables as they were at
+ * the start of the step, increments summed in 2^-32 fixed point, on-device
+ * episode ends (emptied or max_steps) with Philox placement.
+ * Learning variants require neighborhood 4 (all of the reference's learning
+ * drivers use "neumann") and map values in 0..3.  Table keys are packed u64
+ * (ffm_amd/learn_keys.py): 2 bits per cell / rank in [0,26), bx in [26,45),
+ * by in [45,64).
+ */
+enum { FFM_LEARN_CRITIC_ONLY = 0, FFM_LEARN_ACTOR_ONLY = 1, FFM_LEARN_BOTH = 2 };
+enum { FFM_TABLE_V = 0, FFM_TABLE_H = 1 };
+
+typedef struct {
+    int32_t mode;             /* FFM_LEARN_* (ffm_unified learning_mode; ignored otherwise) */
+    double k_A;               /* actor logit scale */
+    double alpha_v, alpha_h, gamma;
+    double exit_reward, step_penalty, collision_penalty;
+    double epsilon;           /* eps-greedy (actor modes) */
+    double v_default;         /* value a V read inserts: 0.0 (-1.0 after ffm_ac_core.set_v_table) */
+    int32_t block_size;       /* state-key block size (ffm_actor_only: always 5) */
+    int32_t max_steps;        /* Philox mode: an episode also ends after this many steps (0 = never) */
+    int32_t log2_v_capacity;  /* hash-table slots (0 = 21) */
+    int32_t log2_h_capacity;
+} ffm_learn_desc;
+
+typedef struct ffm_learner ffm_learner;
+
+int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn, ffm_learner** out);
+int ffm_learner_destroy(ffm_learner* l);
+/* Philox: place n_agents in every env (keyed by the step counter, which advances)
+ * and zero the DFF.  MT: zero the DFF and counts only (the caller uploads
+ * positions drawn from its own generators, like ffm_engine_reset). */
+int ffm_learner_reset(ffm_learner* l, void* stream);
+int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream);
+int ffm_learner_set_state(ffm_learner* l, int64_t env0, int64_t n, const uint16_t* positions,
+                          const int32_t* counts, const float* dff, void* stream);
+int ffm_learner_get_state(ffm_learner* l, int64_t env0, int64_t n, uint16_t* positions, int32_t* counts,
+                          float* dff, void* stream);
+/* episodes[n]: completed episodes per env; ep_steps[n]: steps into the current one. */
+int ffm_learner_get_episodes(ffm_learner* l, int64_t env0, int64_t n, int32_t* episodes, int32_t* ep_steps,
+                             void* stream);
+int ffm_learner_set_mt_state(ffm_learner* l, int64_t env, const uint32_t* np_key, int32_t np_pos,
+                             const uint32_t* py_key, int32_t py_pos, void* stream);
+int ffm_learner_get_mt_state(ffm_learner* l, int64_t env, uint32_t* np_key, int32_t* np_pos,
+                             uint32_t* py_key, int32_t* py_pos, void* stream);
+int ffm_learner_get_counters(ffm_learner* l, uint64_t* counters, void* stream);
+int ffm_learner_set_epsilon(ffm_learner* l, double epsilon);
+int ffm_learner_set_v_default(ffm_learner* l, double v_default, void* stream);
+int ffm_learner_table_size(ffm_learner* l, int32_t which, int64_t* n, void* stream);
+/* Entries in insertion order (= the reference dict's order in MT mode).
+ * vals: [cap][1] (V) or [cap][5] (H).  *n receives the entry count; fails if > cap. */
+int ffm_learner_export_table(ffm_learner* l, int32_t which, uint64_t* keys, double* vals, int64_t cap,
+                             int64_t* n, void* stream);
+/* Replace the table by these entries, inserted in the given order. */
+int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys, const double* vals,
+                             int64_t n, void* stream);
+int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t);
+int ffm_learner_set_step_index(ffm_learner* l, uint32_t t);
 
 /* ---- numerics probes (used by the parity tests) ---------------------- */
 /* y[i] = NumPy-exact float32 exp(x[i]) computed on the device; device pointers. */

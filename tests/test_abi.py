@@ -34,7 +34,8 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.ffm_abi_version() == 1
+    from ffm_amd.engine import ABI_VERSION
+    assert lib.ffm_abi_version() == ABI_VERSION == 2
 
 
 def test_engine_fails_loudly_without_gpu(lib):
@@ -60,6 +61,39 @@ def test_engine_validation_before_device(lib):
         Engine(bad, l1_sff(m), n_envs=1, n_agents=1)
     with pytest.raises(ValueError):
         Engine(m, l1_sff(m)[:5], n_envs=1, n_agents=1)
+
+
+def test_learner_fails_loudly_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Learner
+    m = make_room(12, 12)
+    for variant, mode in (("ac", None), ("unified", "both"), ("actor_only", None)):
+        with pytest.raises((RuntimeError, MemoryError)):
+            Learner(m, l1_sff(m), variant, n_envs=4, n_agents=8, mode=mode)
+
+
+def test_learner_validation_before_device(lib):
+    """The reference's ValueErrors (model/ffm_unified.py:59-63; np.random.choice at
+    model/ffm_unified.py:146) come before any device work."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Learner
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    with pytest.raises(ValueError):
+        Learner(m, s, "unified", n_envs=1, n_agents=4, mode="greedy")
+    with pytest.raises(ValueError):
+        Learner(m, s, "nope", n_envs=1, n_agents=4)
+    with pytest.raises(ValueError):
+        Learner(m, s, "ac", n_envs=1, n_agents=101)
+    with pytest.raises(NotImplementedError):
+        Learner(m, s, "ac", n_envs=1, n_agents=4, params={"neighborhood": "moore"})
+    bad = m.copy()
+    bad[5, 0] = 0
+    with pytest.raises(ValueError):
+        Learner(bad, s, "unified", n_envs=1, n_agents=4)
 
 
 def test_missing_library_raises(monkeypatch, tmp_path):

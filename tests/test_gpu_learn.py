@@ -1,0 +1,258 @@
+"""GPU parity of the learning variants (ffm_ac_core, ffm_unified critic_only /
+actor_only / both, ffm_actor_only) through the C ABI (ffm_learner_*).
+
+* MT mode against the golden vectors recorded from the reference itself
+  (tests/golden/learn_*.npz): positions, DFF bits, both RNG streams and the final
+  V / H tables (keys, dict order, value bits) must all be equal.
+* Philox (batched) mode against the CPU restatement of the same batched
+  semantics (oracle/ffm_learn_oracle.c) at sizes it finishes in seconds:
+  positions, counts, episode ends, DFF bits and the V / H tables bit for bit.
+* Size-independent properties at BASELINE config-4 / config-5 scale.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN_DIR, dff_hash
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+CASES = sorted(os.path.basename(p)[6:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "learn_*.npz")))
+VARIANTS = [("ac", None), ("unified", "critic_only"), ("unified", "actor_only"), ("unified", "both"),
+            ("actor_only", None)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+
+
+def _learner(*a, **kw):
+    from ffm_amd.engine import Learner
+    return Learner(*a, **kw)
+
+
+def _mt_words(m):
+    return np.ctypeslib.as_array(m.mt).copy(), int(m.pos)
+
+
+# ---------------------------------------------------------------------------
+# MT mode: every golden episode of every seed
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", CASES)
+def test_learner_replays_reference_goldens(name):
+    from oracle import oracle as O
+    z = np.load(os.path.join(GOLDEN_DIR, f"learn_{name}.npz"), allow_pickle=False)
+    z = {k: z[k] for k in z.files}
+    params = json.loads(str(z["params"]))
+    variant, mode = str(z["variant"]), str(z["mode"]) or None
+    H, W = z["map"].shape
+    N, n_ep = int(z["N"]), int(z["n_ep"])
+    core = O.Core(z["map"], z["sff"], {"neighborhood": "neumann"})
+    ep_i = step_i = cell_i = 0
+    v_off = h_off = 0
+    for si, seed in enumerate(z["seeds"]):
+        L = _learner(z["map"], z["sff"], variant, n_envs=1, n_agents=0, agent_capacity=max(N, 1), mode=mode,
+                     params=params, rng="mt", auto_reset=False)
+        np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
+        for ep in range(n_ep):
+            if ep > 0 and int(z["reload_v"]):
+                L.set_v_default(-1.0)           # model/ffm_ac_core.py:343
+            L.set_epsilon(float(z["eps"][ep_i]))
+            pos = core.init_agents_mt(N, np_rng)
+            ni = int(z["init_n"][ep_i])
+            init = z["init"][sum(z["init_n"][:ep_i]):sum(z["init_n"][:ep_i]) + ni]
+            assert np.array_equal(pos, init), f"seed {seed} ep {ep}: initial placement"
+            cells = np.full((1, max(N, 1)), 0xFFFF, np.uint16)
+            cells[0, :len(pos)] = pos
+            L.set_state(0, positions=cells, counts=np.array([len(pos)], np.int32),
+                        dff=np.zeros((1, H, W), np.float32))
+            nk, npos = _mt_words(np_rng)
+            pk, ppos = _mt_words(py_rng)
+            L.set_mt_state(0, nk, npos, pk, ppos)
+            for t in range(int(z["nsteps"][ep_i])):
+                L.step(1)
+                gp, gc, gd = L.get_state()
+                c = int(z["counts"][step_i])
+                assert int(gc[0]) == c, f"seed {seed} ep {ep} step {t}: count {gc[0]} != {c}"
+                assert np.array_equal(gp[0, :c], z["cells"][cell_i:cell_i + c]), f"seed {seed} ep {ep} step {t}"
+                assert dff_hash(gd[0]) == int(z["dff_hash"][step_i]), f"seed {seed} ep {ep} step {t}: DFF"
+                cell_i += c
+                step_i += 1
+            nk, npos, pk, ppos = L.get_mt_state(0)
+            np.ctypeslib.as_array(np_rng.mt)[:] = nk
+            np_rng.pos = npos
+            np.ctypeslib.as_array(py_rng.mt)[:] = pk
+            py_rng.pos = ppos
+            ep_i += 1
+        vk, vv = L.export_table("V")
+        nv = int(z["v_n"][si])
+        assert len(vk) == nv, f"seed {seed}: |V| {len(vk)} != {nv}"
+        assert np.array_equal(vk, z["v_keys"][v_off:v_off + nv]), f"seed {seed}: V keys / order"
+        assert np.array_equal(vv.view(np.uint64), z["v_vals"][v_off:v_off + nv].view(np.uint64)), \
+            f"seed {seed}: V values"
+        v_off += nv
+        nh = int(z["h_n"][si])
+        if nh:
+            hk, hv = L.export_table("H")
+            assert len(hk) == nh, f"seed {seed}: |H| {len(hk)} != {nh}"
+            assert np.array_equal(hk, z["h_keys"][h_off:h_off + nh]), f"seed {seed}: H keys / order"
+            assert np.array_equal(hv.view(np.uint64), z["h_vals"][h_off:h_off + nh].view(np.uint64)), \
+                f"seed {seed}: H values"
+            h_off += nh
+        tails = [O.lib().ffo_mt_next(np_rng) for _ in range(4)]
+        assert tails == [int(x) for x in z["np_tail"][si]], "NumPy stream position"
+        tails = [O.lib().ffo_mt_next(py_rng) for _ in range(4)]
+        assert tails == [int(x) for x in z["py_tail"][si]], "CPython stream position"
+        L.close()
+
+
+# ---------------------------------------------------------------------------
+# Philox (batched) mode: GPU == CPU restatement
+# ---------------------------------------------------------------------------
+def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
+                    nthreads=16, sff_dtype=np.float32):
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import learn as LO
+    from oracle import oracle as O
+    m = make_room(H, W)
+    s = l1_sff(m).astype(sff_dtype)
+    A = A or N
+    L = _learner(m, s, variant, n_envs=E, n_agents=N, agent_capacity=A, mode=mode, params=params,
+                 rng="philox", seed=seed, auto_reset=True, max_steps=max_steps, env_base=env_base)
+    cpu = LO.Learn(m, s, variant, mode, params, log2_cap=22)
+    core = O.Core(m, s, {"neighborhood": "neumann"})
+    pos = np.full((E, A), 0xFFFF, np.uint16)
+    for e in range(E):
+        pos[e, :N] = core.reset_philox(N, seed, 0, env_base + e)
+    counts = np.full(E, N, np.int32)
+    dff = np.zeros((E, H, W), np.float32)
+    eps = np.zeros(E, np.int32)
+    ep_steps = np.zeros(E, np.int32)
+    L.reset()
+    gp, gc, _ = L.get_state()
+    assert np.array_equal(gc, counts)
+    assert np.array_equal(gp[:, :N], pos[:, :N]), "reset placement"
+    tot = 0
+    for t in range(1, T + 1):
+        tot += cpu.step_philox_batch(pos, counts, dff, eps, ep_steps, seed, t, True, N, max_steps, env_base,
+                                     nthreads)
+    L.step(T)
+    gp, gc, gd = L.get_state()
+    geps, gst = L.episodes()
+    assert np.array_equal(gc, counts), "counts"
+    assert np.array_equal(geps, eps), "episodes"
+    assert np.array_equal(gst, ep_steps), "steps into the episode"
+    for e in range(E):
+        assert np.array_equal(gp[e, :counts[e]], pos[e, :counts[e]]), f"env {e} positions"
+    assert np.array_equal(gd.view(np.uint32), dff.view(np.uint32)), "DFF bits"
+    for which, tab in (("V", cpu.V), ("H", cpu.Ht)):
+        if which == "H" and variant != "actor_only" and mode in (None, "critic_only"):
+            continue
+        ck, cv = tab.export()
+        gk, gv = L.export_table(which)
+        assert len(gk) == len(ck), f"|{which}|"
+        oc, og = np.argsort(ck), np.argsort(gk)
+        assert np.array_equal(ck[oc], gk[og]), f"{which} keys"
+        assert np.array_equal(np.asarray(cv)[oc].view(np.uint64), np.asarray(gv)[og].view(np.uint64)), \
+            f"{which} values"
+    c = L.counters()
+    assert c["agent_steps"] == tot
+    assert c["resets"] == int(eps.sum())
+    assert c["steps"] == T
+    L.close()
+    return counts, eps
+
+
+@pytest.mark.parametrize("variant,mode", VARIANTS)
+def test_learner_philox_12x12_matches_cpu(variant, mode):
+    """12x12, 32 agents (configs 2/4 geometry), epsilon > 0 (exercises randint), 2,048 envs."""
+    p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    _, eps = _philox_compare(variant, mode, p, 12, 12, 32, 2048, 120)
+    assert eps.sum() > 0
+
+
+@pytest.mark.parametrize("variant,mode", VARIANTS)
+def test_learner_philox_odd_shapes_and_f64_sff(variant, mode):
+    """Non-square room, block size 2, f64 SFF (main.py's data path), spare agent capacity,
+    env ids offset (a later shard)."""
+    p = {"epsilon": 0.05, "block_size": 2, "k_S": 4} if variant != "ac" else {"block_size": 2}
+    _philox_compare(variant, mode, p, 11, 17, 20, 333, 90, A=24, max_steps=40, seed=9, env_base=1 << 20,
+                    sff_dtype=np.float64)
+
+
+@pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None), ("ac", None)])
+def test_learner_philox_large_rooms(variant, mode):
+    """Workgroup-per-env kernel at 256 and 1,024 agent lanes (40x40 / 200 agents; 64x64 / 600)."""
+    p = {"block_size": 5}
+    _philox_compare(variant, mode, p, 40, 40, 200, 64, 40, max_steps=30, seed=3)
+    _philox_compare(variant, mode, p, 64, 64, 600, 16, 25, max_steps=20, seed=4)
+
+
+def test_learner_philox_config5_geometry():
+    """256x256 room, 8,192 agents (BASELINE config 5, ffm_unified actor_only): thresholded
+    on-device placement (> 16,384 free cells) and the 8-agents-per-lane kernel."""
+    _philox_compare("unified", "actor_only", {"block_size": 5}, 256, 256, 8192, 4, 6, max_steps=300, seed=5)
+
+
+def test_learner_table_import_export_roundtrip():
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd import learn_keys as K
+    m = make_room(12, 12)
+    L = _learner(m, l1_sff(m), "unified", n_envs=4, n_agents=8, mode="both", params={"block_size": 1})
+    rs = np.random.RandomState(0)
+    keys = np.array(sorted({K.pack(rs.randint(0, 4, 4), rs.randint(0, 12), rs.randint(0, 12))
+                            for _ in range(500)}), np.uint64)
+    rs.shuffle(keys)
+    vv = rs.standard_normal(len(keys))
+    hv = rs.standard_normal((len(keys), 5))
+    L.import_table("V", keys, vv)
+    L.import_table("H", keys[::-1], hv[::-1])
+    k1, v1 = L.export_table("V")
+    k2, v2 = L.export_table("H")
+    assert np.array_equal(k1, keys) and np.array_equal(v1.view(np.uint64), vv.view(np.uint64))
+    assert np.array_equal(k2, keys[::-1]) and np.array_equal(v2.view(np.uint64), hv[::-1].view(np.uint64))
+    assert L.table_size("V") == len(keys)
+    L.close()
+
+
+@pytest.mark.parametrize("variant,mode", [("actor_only", None), ("unified", "actor_only")])
+def test_learner_full_size_invariants(variant, mode):
+    """BASELINE config-4 geometry (12x12, 32 agents, 65,536 envs per GPU): determinism over
+    two runs, valid occupancy, finite tables, episodes truncated at max_steps."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"epsilon": 0.2, "block_size": 1}
+    outs = []
+    for _ in range(2):
+        L = _learner(m, s, variant, n_envs=65536, n_agents=32, mode=mode, params=p, seed=8, max_steps=100)
+        L.reset()
+        L.step(120)
+        outs.append((*L.get_state(), *L.episodes(), *L.export_table("V"), *L.export_table("H")))
+        c = L.counters()
+        L.close()
+    a, b = outs
+    for x, y in zip(a[:5], b[:5]):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    for i in (5, 7):       # tables: same entries (insertion order may differ), same bits
+        oa, ob = np.argsort(a[i]), np.argsort(b[i])
+        assert np.array_equal(a[i][oa], b[i][ob])
+        assert np.array_equal(a[i + 1][oa].view(np.uint64), b[i + 1][ob].view(np.uint64))
+        assert np.isfinite(a[i + 1]).all()
+    pos, cnt, dff, eps, st = a[:5]
+    assert (cnt >= 0).all() and (cnt <= 32).all() and (st < 100).all()
+    assert eps.sum() >= 65536        # every env ended at least one episode in 120 steps
+    flat = m.reshape(-1)
+    for e in range(0, 65536, 101):
+        cells = pos[e, :cnt[e]]
+        assert len(set(cells.tolist())) == len(cells) and (flat[cells] == 0).all()
+    assert (dff >= 0).all() and np.isfinite(dff).all()
+    assert c["steps"] == 120 and c["agent_steps"] > 0
