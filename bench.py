@@ -7,8 +7,15 @@ recipe), 32 agents per env, 65,536 envs per GPU, default_config.yaml params
 on-device auto-reset.  One bench "step" = one FloorFieldModel.step() of every
 env = one launch of the fused HIP kernel over inputs resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--config picks a BASELINE.json workload: 2 (default, the headline line),
+3 (64x64 room, 512 agents, 8,192 envs), 4 (ffm_actor_only learning step,
+12x12, 32 agents, 65,536 envs per GPU, run_actor_only_training.py params) or
+5 (ffm_unified actor_only learning step, 256x256, 8,192 agents, 512 envs per
+GPU, run_unified_actor_training.py params).  Configs 4 and 5 step the
+learner (ffm_learner_*): its V / H tables are shared by all envs of a GPU.
 
 Multi-GPU: envs are sharded by global id (weak scaling, 65,536 per GPU); the
 only collective is the final reduction of counters and times (RCCL).
@@ -40,11 +47,12 @@ METRIC = "agent-steps/sec (whole node), 12×12 grid × 64k envs, 1/2/4/8 GPU"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--size", type=int, default=12)
-    ap.add_argument("--agents", type=int, default=32)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
+    ap.add_argument("--steps", type=int, default=None, help="default 500 (configs 2-4), 50 (config 5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 50 (configs 2-4), 5 (config 5)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    ap.add_argument("--size", type=int, default=None)
+    ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--neighborhood", default="neumann")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--envs-per-block", type=int, default=0)
@@ -53,7 +61,15 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_config2.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    size, agents, envs, steps, warmup = {2: (12, 32, 65536, 500, 50), 3: (64, 512, 8192, 200, 20),
+                                         4: (12, 32, 65536, 300, 30), 5: (256, 8192, 512, 50, 5)}[a.config]
+    a.size = a.size or size
+    a.agents = a.agents or agents
+    a.envs = a.envs or envs
+    a.steps = a.steps if a.steps is not None else steps
+    a.warmup = a.warmup if a.warmup is not None else warmup
+    return a
 
 
 def main():
@@ -69,6 +85,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+
+    if args.config in (4, 5):
+        return bench_learner(args, world, rank, torch, dist)
 
     from ffm_amd.data import make_room, l1_sff
     from ffm_amd.engine import Engine
@@ -171,6 +190,153 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+# run_actor_only_training.py:47-58 (epsilon = EPSILON_START, :40) and
+# run_unified_actor_training.py:58-70 (epsilon = EPSILON_START, :51).
+LEARN_CONFIGS = {
+    4: dict(variant="actor_only", mode=None, max_steps=1000,      # run_actor_only_training.py:37
+            params={"k_D": 1, "k_A": 10, "alpha_v": 0.1, "alpha_h": 0.1, "gamma": 0.95, "exit_reward": 100.0,
+                    "step_penalty": 0.0, "collision_penalty": -1.0, "neighborhood": "neumann", "epsilon": 0.2}),
+    5: dict(variant="unified", mode="actor_only", max_steps=300,  # run_unified_actor_training.py:47
+            params={"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99,
+                    "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0,
+                    "neighborhood": "neumann", "block_size": 1, "epsilon": 0.2}),
+}
+
+
+def learner_bytes_per_env_step(H, W, A, D):
+    """Algorithmic HBM bytes of one learning step of one env at full occupancy
+    (DESIGN.md section 9.4): the ffm_core state round trip, 2*(2A + 4HW + 4),
+    plus per agent two V reads (key + value, 16 B each) and one fixed-point
+    increment (8 B read + 8 B write), and for actor variants the H row (8 B key +
+    40 B values) and its increment (16 B)."""
+    per_agent = 2 * 16 + 16 + (8 + 40 + 16)
+    return 2 * (2 * A + 4 * H * W + 4) + A * per_agent
+
+
+def bench_learner(args, world, rank, torch, dist):
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Learner
+    cfg = LEARN_CONFIGS[args.config]
+    H = W = args.size
+    A, E = args.agents, args.envs
+    m = make_room(H, W)
+    s = l1_sff(m)
+    L = Learner(m, s, cfg["variant"], n_envs=E, n_agents=A, mode=cfg["mode"], params=cfg["params"],
+                rng="philox", seed=args.seed, auto_reset=True, max_steps=cfg["max_steps"], env_base=rank * E,
+                device=torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    L.reset(stream)
+    L.step(args.warmup, stream)
+    torch.cuda.synchronize()
+    c0 = L.counters(stream)
+    print(f"[bench] config {args.config}: warmup done", file=sys.stderr, flush=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    L.step(args.steps, stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    c1 = L.counters(stream)
+    elapsed = t1 - t0
+    agent_steps = c1["agent_steps"] - c0["agent_steps"]
+    print(f"[bench] timed region {elapsed:.3f} s", file=sys.stderr, flush=True)
+    nk = min(args.steps, 100)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    L.step(nk, stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    step_ms = ev0.elapsed_time(ev1) / nk
+    v_size, h_size = L.table_size("V"), L.table_size("H")
+    if world > 1:
+        from ffm_amd.dist import reduce_counters, reduce_max
+        elapsed = reduce_max(elapsed, device="cuda")
+        agent_steps = reduce_counters({"agent_steps": agent_steps}, device="cuda")["agent_steps"]
+    if rank == 0:
+        D = 4 if cfg["variant"] == "actor_only" else 1
+        bpe = learner_bytes_per_env_step(H, W, A, D)
+        achieved = E * bpe / (step_ms / 1e3) / 1e9
+        out = {
+            "metric": METRIC, "value": agent_steps / elapsed, "unit": "agent-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+f64",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"config {args.config}: {cfg['variant']}"
+                             f"{'/' + cfg['mode'] if cfg['mode'] else ''} learning step, {H}x{W} room, "
+                             f"{A} agents/env, {E} envs/GPU, epsilon {cfg['params']['epsilon']}, "
+                             f"max_steps {cfg['max_steps']}, Philox seed {args.seed}, on-device auto-reset"),
+                "map": f"{H}x{W}", "agents_per_env": A, "envs_per_gpu": E, "global_envs": E * world,
+                "parallelism": f"env-sharded x{world}",
+            },
+            "env_steps_per_s": E * world * args.steps / elapsed,
+            "step_ms_events": step_ms,
+            "tables": {"V": v_size, "H": h_size},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "bytes_per_launch_algorithmic": E * bpe,
+                         "note": "whole learning step (all kernels) timed with HIP events"},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline_learner(args, cfg, m, s)
+        print(json.dumps(out), flush=True)
+    L.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_learner(args, cfg, m, s):
+    """The batched learning restatement (oracle/ffm_learn_oracle.c) on a bounded
+    sample; its state after the sample is checked bit-exactly against a fresh
+    GPU learner stepped the same number of steps."""
+    from oracle import learn as LO
+    from oracle import oracle as O
+    from ffm_amd.engine import Learner
+    H, W = m.shape
+    A = args.agents
+    E = min(args.cpu_envs, 1024) if args.config == 4 else 2
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    cpu = LO.Learn(m, s, cfg["variant"], cfg["mode"], cfg["params"], log2_cap=22 if args.config == 4 else 24)
+    core = O.Core(m, s, {"neighborhood": "neumann"})
+    pos = np.full((E, A), 0xFFFF, np.uint16)
+    for e in range(E):
+        pos[e] = core.reset_philox(A, args.seed, 0, e)
+    cnt = np.full(E, A, np.int32)
+    dff = np.zeros((E, H, W), np.float32)
+    eps = np.zeros(E, np.int32)
+    est = np.zeros(E, np.int32)
+    t, total = 1, 0
+    tb = time.perf_counter()
+    while time.perf_counter() - tb < 12.0 or t <= 3:
+        total += cpu.step_philox_batch(pos, cnt, dff, eps, est, args.seed, t, True, A, cfg["max_steps"], 0,
+                                       threads)
+        t += 1
+    elapsed = time.perf_counter() - tb
+    g = Learner(m, s, cfg["variant"], n_envs=E, n_agents=A, mode=cfg["mode"], params=cfg["params"],
+                rng="philox", seed=args.seed, auto_reset=True, max_steps=cfg["max_steps"])
+    g.reset()
+    g.step(t - 1)
+    gp, gc, gd = g.get_state()
+    gk, gv = g.export_table("V")
+    g.close()
+    ck, cv = cpu.V.export()
+    ok = bool(np.array_equal(gc, cnt) and np.array_equal(gd.view(np.uint32), dff.view(np.uint32))
+              and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(E))
+              and np.array_equal(np.sort(gk), np.sort(ck))
+              and np.array_equal(gv[np.argsort(gk)].view(np.uint64), cv[np.argsort(ck)].view(np.uint64)))
+    return {
+        "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle/ffm_learn_oracle.c batched Philox mode, {E} envs x {t - 1} steps of the same "
+                   f"workload (OpenMP {threads} threads); state and V table bit-exact vs GPU: {ok}"),
+        "seconds": elapsed, "bit_exact_vs_gpu": ok,
+    }
 
 
 def copy_bandwidth(torch, stream, nbytes, reps=50):

@@ -35,14 +35,32 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
-    """Compile the library; `out`/`defines` make diagnostic variants (tools/ablate.sh)."""
+    """Compile the library; `out`/`defines` make diagnostic variants (tools/ablate.sh).
+
+    Each source compiles to its own object in parallel (the kernels' translation
+    units are independent), then hipcc links the shared library."""
+    from concurrent.futures import ThreadPoolExecutor
     target = out or LIB_PATH
     if out is None and not force and not _stale():
         return LIB_PATH
     os.makedirs(os.path.dirname(target), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    objdir = target + ".obj"
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != "-shared"] + [f"-D{d}" for d in defines]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, src + ".o")
+        cmd = [hipcc, *cflags, "-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = target + ".tmp"
-    cmd = [hipcc, *FLAGS, *[f"-D{d}" for d in defines], "-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)

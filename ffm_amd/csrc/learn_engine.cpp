@@ -68,6 +68,8 @@ struct ffm_learner {
     uint32_t* d_mt_np = nullptr;
     uint32_t* d_mt_py = nullptr;
     unsigned char* d_scratch = nullptr;
+    uint32_t dense_bx = 0;             // dense tables: x blocks (import validation)
+    bool hstat_valid = false;          // d_hstat holds the H statistics of the current table
     DevTable V, H;
 };
 
@@ -90,10 +92,19 @@ static void release(ffm_learner* l) {
     delete l;
 }
 
-static hipError_t alloc_table(DevTable& T, int log2cap, int width) {
+// dense_by > 0: ffm_unified's rank keys map injectively onto
+// ranks | (bx * dense_by + by) << 8 (learn_step.hip dense_slot); the capacity is
+// the next power of two >= 256 * Bx * By and the table can never fill.
+static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dense_by = 0, size_t dense_n = 0) {
     T.width = width;
+    if (dense_by) {
+        log2cap = 8;
+        while (((size_t)1 << log2cap) < dense_n) log2cap++;
+    }
     T.cap = (size_t)1 << log2cap;
     T.t.mask = (uint32_t)(T.cap - 1);
+    T.t.dense_by = dense_by;
+    T.t.limit = (uint32_t)(T.cap - T.cap / 8);
     hipError_t e;
     if ((e = hipMalloc((void**)&T.t.keys, T.cap * 8)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.vals, T.cap * width * 8)) != hipSuccess) return e;
@@ -267,8 +278,20 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         ALLOC(l->d_scratch, ffm::learn_exact_scratch_bytes(HW, (int)A));
     }
 #undef ALLOC
-    if ((he = alloc_table(l->V, l->L.log2_v_capacity, 1)) != hipSuccess ||
-        (he = alloc_table(l->H, l->actor ? l->L.log2_h_capacity : 8, 5)) != hipSuccess)
+    // ffm_unified: dense tables over 256 rank codes x Bx x By blocks (at most 2^28 slots).
+    uint32_t dense_by = 0;
+    size_t dense_n = 0;
+    if (d.variant == FFM_VARIANT_UNIFIED) {
+        const size_t bs = (size_t)learn->block_size;
+        const size_t bx = (size_t)(H - 1) / bs + 1, by = (size_t)(W - 1) / bs + 1;
+        if (256 * bx * by <= ((size_t)1 << 28)) {
+            dense_by = (uint32_t)by;
+            dense_n = 256 * bx * by;
+        }
+    }
+    l->dense_bx = dense_by ? (uint32_t)((H - 1) / learn->block_size + 1) : 0;
+    if ((he = alloc_table(l->V, l->L.log2_v_capacity, 1, dense_by, dense_n)) != hipSuccess ||
+        (he = alloc_table(l->H, l->actor ? l->L.log2_h_capacity : 8, 5, l->actor ? dense_by : 0, dense_n)) != hipSuccess)
         return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(l->d_sff, d.sff, (size_t)HW * (l->f64 ? 8 : 4), hipMemcpyHostToDevice);
@@ -325,11 +348,14 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             l->t++;
             continue;
         }
-        if (l->actor) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
+        // H statistics of the step-start table: produced by the previous step's H
+        // apply, recomputed only after the table was replaced (create / import)
+        if (l->actor && !l->hstat_valid) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
         HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
         HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
         if (l->post_update) HIP_TRY(ffm::launch_learn_post(make_args(l), s));
         if (l->actor) HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
+        l->hstat_valid = l->actor;
         l->cur ^= 1;
         if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
         l->t++;
@@ -515,10 +541,17 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
     if (!l || (n > 0 && (!keys || !vals))) return fail(FFM_E_INVALID, "null argument");
     DevTable* T = pick(l, which);
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
-    if ((size_t)n > T->cap - T->cap / 8) return fail(FFM_E_NOMEM, "table capacity too small for import");
-    for (int64_t i = 0; i < n; i++)
+    if ((size_t)n > T->t.limit) return fail(FFM_E_NOMEM, "table capacity too small for import");
+    for (int64_t i = 0; i < n; i++) {
         if (keys[i] == ~0ull) return fail(FFM_E_INVALID, "invalid key");
+        if (T->t.dense_by) {     // rank keys: 8 bits of ranks, blocks inside the map
+            const uint64_t bx = (keys[i] >> 26) & 0x7FFFF, by = (keys[i] >> 45) & 0x7FFFF;
+            if ((keys[i] & 0x3FFFF00ull) || bx >= l->dense_bx || by >= T->t.dense_by)
+                return fail(FFM_E_INVALID, "key is not a rank state of this map / block size");
+        }
+    }
     hipStream_t s = (hipStream_t)stream;
+    if (which == FFM_TABLE_H) l->hstat_valid = false;
     HIP_TRY(clear_table(l, *T, which == FFM_TABLE_V ? l->L.v_default : 0.0, s));
     if (n > 0) {
         unsigned long long* dk = nullptr;

@@ -27,7 +27,14 @@ struct LearnTable {
     uint32_t* order;            // [cap] slot of the i-th inserted key
     uint32_t* n;                // [1] keys inserted
     uint32_t mask;              // cap - 1
+    // Dense layout (ffm_unified's rank keys): slot = ranks | (bx * dense_by + by) << 8,
+    // injective, so no probing and never full.  0 = hashed (13-cell keys).
+    uint32_t dense_by;
+    uint32_t limit;             // hashed: insertions refused beyond this many keys (7/8 load)
 };
+
+// Longest probe sequence a hashed lookup walks before reporting the table full.
+constexpr uint32_t kMaxProbe = 4096;
 
 struct LearnArgs {
     int H, W, HW, A, N, F;
@@ -64,7 +71,7 @@ struct LearnArgs {
     const uint16_t* free_cells;    // [F] x*W+y of the free cells, row-major (np.argwhere(map == 0))
 };
 
-constexpr int kHstatBlocks = 120;
+constexpr int kHstatBlocks = 512;
 
 size_t learn_exact_scratch_bytes(int HW, int A);
 int learn_batch_block_size(int A);

@@ -70,17 +70,24 @@ __device__ __forceinline__ void acc_add(long long* p, long long q) {
 // Slot of `key`, inserting it when absent (a defaultdict read inserts,
 // model/ffm_unified.py:658).  Empty slots already hold the default value, so
 // an inserter never has to publish a value.  -1 only when the table is full.
+__device__ __forceinline__ uint32_t dense_slot(unsigned long long key, uint32_t by_count) {
+    const uint32_t bx = (uint32_t)(key >> 26) & 0x7FFFFu, by = (uint32_t)(key >> 45) & 0x7FFFFu;
+    return (uint32_t)(key & 0xFFu) | ((bx * by_count + by) << 8);
+}
+
 __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflow) {
-    uint32_t h = (uint32_t)mix64(key) & T.mask;
-    for (uint32_t probe = 0; probe <= T.mask; probe++) {
+    uint32_t h = T.dense_by ? dense_slot(key, T.dense_by) : (uint32_t)mix64(key) & T.mask;
+    for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
         const unsigned long long k = __hip_atomic_load(&T.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == key) return (int)h;
         if (k == kEmptyKey) {
+            // A hashed table past 7/8 load refuses new keys (probe chains would grow
+            // without bound); the host reports FFM_E_NOMEM.
+            if (!T.dense_by && __hip_atomic_load(T.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= T.limit) break;
             const unsigned long long old = atomicCAS(&T.keys[h], kEmptyKey, key);
             if (old == kEmptyKey) {
                 const uint32_t idx = atomicAdd(T.n, 1u);
                 T.order[idx] = h;
-                if (idx >= T.mask - (T.mask >> 3)) atomicOr(overflow, 1);   // > 7/8 full
                 return (int)h;
             }
             if (old == key) return (int)h;
@@ -658,23 +665,241 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
     }
 }
 
+// Diagnostic builds only (tools/learn_ablate.sh): FFM_LABLATE bits drop parts of the
+// batched step to time them.  1: table increments, 2: learning phase,
+// 4: policy (agents stay; no H lookup), 8: DFF stencil.
+#ifndef FFM_LABLATE
+#define FFM_LABLATE 0
+#endif
+
 // ===========================================================================
-// Batched step: one workgroup per env.
+// Batched step: EPB envs per workgroup, LPE = BS / EPB lanes per env, APT
+// agents per lane.  Small rooms (A <= 32) pack two envs onto one wavefront.
 // ===========================================================================
-template <int BS>
-__device__ __forceinline__ int block_scan_flag(bool f, int* ws, int& total) {
-    const unsigned long long m = __ballot(f);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (BS == 64) {
-        total = __popcll(m);
-        return pre;
+
+// A decision's policy, computed once per agent: the normalised cdf of
+// np.random.choice (cdf / cdf[-1], model/ffm_unified.py:497) over the five
+// moves (U, D, L, R, stay; invalid moves carry zero mass) and the valid-move
+// mask for the epsilon branch (:478-495).  ffm_actor_only repeats the same
+// decision up to four times per agent (the inner-loop quirk,
+// model/ffm_actor_only.py:214-355): within a batched step the table, DFF and
+// statistics it reads are fixed, so only the draws differ.
+struct Policy {
+    double cn[5];
+    int vmask;            // bit k: move k valid
+    int none;             // ffm_ac_core: no request (softmax sum not finite / zero, :187)
+};
+
+__device__ __forceinline__ int kth_set_bit(int mask, int r) {
+    int k = 4;
+#pragma unroll
+    for (int j = 4; j >= 0; j--) {
+        const int below = __builtin_popcount(mask & ((1 << j) - 1));
+        if (((mask >> j) & 1) && below == r) k = j;
     }
+    return k;
+}
+
+__device__ __forceinline__ void finish_cdf(Policy& P, const double* p) {
+    double acc = 0.0, cdf[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) { acc += p[k]; cdf[k] = acc; }
+#pragma unroll
+    for (int k = 0; k < 5; k++) P.cn[k] = cdf[k] / acc;
+}
+
+template <class R>
+__device__ __forceinline__ int policy_draw(const Policy& P, double eps, R& rng) {
+    if (eps > 0 && rng.coin() < eps)
+        return kth_set_bit(P.vmask, (int)rng.randint((uint32_t)__builtin_popcount(P.vmask)));
+    const double u = rng.u();
+    int k = 4;
+#pragma unroll
+    for (int j = 3; j >= 0; j--) k = P.cn[j] > u ? j : k;
+    return k;
+}
+
+// Actor policy (model/ffm_unified.py:394-476; compat: model/ffm_actor_only.py:257-326,
+// invalid moves -inf then uniform), the same arithmetic as actor_choose.
+__device__ __forceinline__ void actor_policy(const LearnArgs& a, const double* hrow, const int* coord,
+                                             const int* valid, const float* dff, const HStat& hs, bool compat,
+                                             Policy& P) {
+    double h[5], score[5], e[5], p[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = hrow[k];
+    if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
+        const double smin = (double)a.smin, smax = (double)a.smax;
+#pragma unroll
+        for (int k = 0; k < 5; k++) h[k] = ((hs.mx - h[k]) / (hs.mx - hs.mn)) * (smax - smin) + smin;
+    }
+    bool bad = false;
+    int vm = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const float d = a.kD32 * dff[coord[k]];
+        score[k] = a.nkA * h[k] + (double)d;
+        if (compat && !valid[k]) score[k] = -__builtin_inf();
+        bad = bad || !__builtin_isfinite(score[k]);
+        vm |= valid[k] << k;
+    }
+    // after the bad-score fallback every score is finite: np.max is a plain max
+    double mx = -__builtin_inf();
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if (bad) score[k] = valid[k] ? 1.0 : 0.0;
+        const bool in = compat ? valid[k] != 0 : true;
+        mx = in && score[k] > mx ? score[k] : mx;
+    }
+    double sum = -0.0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const double x = det_exp(score[k] - mx);
+        e[k] = valid[k] ? x : 0.0;
+        sum += e[k];
+    }
+    const int nvalid = __builtin_popcount(vm);
+    const bool ok = __builtin_isfinite(sum) && sum > 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) p[k] = ok ? e[k] / sum : (valid[k] ? 1.0 / (double)nvalid : 0.0);
+    P.vmask = vm;
+    P.none = 0;
+    finish_cdf(P, p);
+}
+
+// ffm_unified critic_only policy (:353-392): SFF/DFF softmax over all five moves,
+// invalid ones masked after the exp.
+__device__ __forceinline__ void critic_policy(const LearnArgs& a, const int* coord, const int* valid,
+                                              const float* dff, Policy& P) {
+    double p[5];
+    int vm = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) vm |= valid[k] << k;
+    const int nvalid = __builtin_popcount(vm);
+    if (a.sff32) {
+        float s[5], e[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float x = a.kS32 * a.sff32[coord[k]];
+            const float y = a.kD32 * dff[coord[k]];
+            s[k] = x + y;
+        }
+        float mx = s[0];
+        bool nan = s[0] != s[0];
+#pragma unroll
+        for (int k = 1; k < 5; k++) {
+            if (!nan && s[k] != s[k]) { mx = s[k]; nan = true; }
+            if (!nan) mx = s[k] > mx ? s[k] : mx;
+        }
+        float sum = -0.0f;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float x = np_expf(s[k] - mx);
+            e[k] = valid[k] ? x : 0.0f;
+            sum += e[k];
+        }
+        const bool ok = __builtin_isfinite(sum) && sum > 0;
+        const float u = (float)(1.0 / (double)nvalid);
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = ok ? (double)(e[k] / sum) : (valid[k] ? (double)u : 0.0);
+    } else {
+        double s[5], e[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float y = a.kD32 * dff[coord[k]];
+            s[k] = a.kS64 * a.sff64[coord[k]] + (double)y;
+        }
+        const double mx = np_max5(s, 5);
+        double sum = -0.0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const double x = det_exp(s[k] - mx);
+            e[k] = valid[k] ? x : 0.0;
+            sum += e[k];
+        }
+        const bool ok = __builtin_isfinite(sum) && sum > 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = ok ? e[k] / sum : (valid[k] ? 1.0 / (double)nvalid : 0.0);
+    }
+    P.vmask = vm;
+    P.none = 0;
+    finish_cdf(P, p);
+}
+
+// ffm_ac_core (= ffm_core) policy (model/ffm_ac_core.py:126-199): softmax over the
+// free neighbours + stay.  Slots of blocked / occupied neighbours carry zero mass,
+// which leaves every sum, running cdf and draw exactly as over the compacted list.
+__device__ __forceinline__ void ac_policy(const LearnArgs& a, const int* coord, const int* valid,
+                                          const float* dff, Policy& P) {
+    double p[5];
+    int vm = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) vm |= valid[k] << k;
+    bool fin;
+    if (a.sff32) {
+        float s[5], e[5];
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float x = a.kS32 * a.sff32[coord[k]];
+            const float y = a.kD32 * dff[coord[k]];
+            s[k] = x + y;
+            mx = valid[k] && s[k] > mx ? s[k] : mx;
+        }
+        float sum = -0.0f;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float x = np_expf(s[k] - mx);
+            e[k] = valid[k] ? x : 0.0f;
+            sum = valid[k] ? sum + e[k] : sum;
+        }
+        fin = __builtin_isfinite(sum) && sum != 0.0f;
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)(e[k] / sum) : 0.0;
+    } else {
+        double s[5], e[5];
+        double mx = -__builtin_inf();
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float y = a.kD32 * dff[coord[k]];
+            s[k] = a.kS64 * a.sff64[coord[k]] + (double)y;
+            mx = valid[k] && s[k] > mx ? s[k] : mx;
+        }
+        double sum = -0.0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const double x = det_exp(s[k] - mx);
+            e[k] = valid[k] ? x : 0.0;
+            sum = valid[k] ? sum + e[k] : sum;
+        }
+        fin = __builtin_isfinite(sum) && sum != 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = valid[k] ? e[k] / sum : 0.0;
+    }
+    P.vmask = vm;
+    P.none = !fin;
+    finish_cdf(P, p);
+}
+
+// Segmented exclusive scan of a flag over each env's LPE lanes.
+template <int BS, int LPE>
+__device__ __forceinline__ int env_scan_flag(bool f, int* ws, int& total) {
+    const unsigned long long m = __ballot(f);
+    const int lane = threadIdx.x & 63;
+    if (LPE <= 64) {
+        const int seg = (lane / LPE) * LPE;
+        const unsigned long long sm =
+            (LPE == 64 ? m : (m >> seg) & ((1ull << (LPE & 63)) - 1));
+        const int l = lane - seg;
+        total = __popcll(sm);
+        return __popcll(sm & ((1ull << l) - 1));
+    }
+    const int wv = (threadIdx.x % LPE) >> 6;
+    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     if (lane == 0) ws[wv] = __popcll(m);
     __syncthreads();
     int off = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < BS / 64; w++) {
+    for (int w = 0; w < LPE / 64; w++) {
         const int c = ws[w];
         off += w < wv ? c : 0;
         tot += c;
@@ -700,31 +925,34 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D) {
     return c;
 }
 
-template <int BS, int APT, int D>
+template <int BS, int EPB, int APT, int D>
 __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int LPE = BS / EPB;
     const int H = a.H, W = a.W, HW = a.HW, A = a.A;
     const BatchCarve cv = batch_carve(HW, A, D);
-    uint16_t* grid = reinterpret_cast<uint16_t*>(smem + cv.grid);
-    uint32_t* bits = reinterpret_cast<uint32_t*>(smem + cv.bits);
-    uint16_t* req = reinterpret_cast<uint16_t*>(smem + cv.req);
-    int* ws = reinterpret_cast<int*>(smem + cv.ws);
-    const long long e = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int sub = threadIdx.x / LPE, tid = threadIdx.x % LPE;
+    unsigned char* base = smem + (size_t)sub * cv.total;
+    uint16_t* grid = reinterpret_cast<uint16_t*>(base + cv.grid);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(base + cv.bits);
+    uint16_t* req = reinterpret_cast<uint16_t*>(base + cv.req);
+    int* ws = reinterpret_cast<int*>(base + cv.ws);
+    const long long e = (long long)blockIdx.x * EPB + sub;
+    const bool live = e < a.E;
     const uint32_t genv = (uint32_t)(a.env_base + e);
-    const int n = a.cnt[e];
+    const int n = live ? a.cnt[e] : 0;
     const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
     const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
-    const float* dff = a.dff_in + e * (long long)HW;
+    const float* dff = a.dff_in + (live ? e : 0) * (long long)HW;
 
-    for (int c = tid; c < HW; c += BS) grid[c] = kNone16;
-    for (int c = tid; c < (HW + 31) / 32; c += BS) bits[c] = 0u;
-    for (int c = tid; c < A * D; c += BS) req[c] = kNone16;
+    for (int c = tid; c < HW; c += LPE) grid[c] = kNone16;
+    for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
+    for (int c = tid; c < A * D; c += LPE) req[c] = kNone16;
     __syncthreads();
     int p[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * BS;
+        const int i = tid + j * LPE;
         p[j] = i < n ? a.pos[e * A + i] : 0;
         if (i < n) grid[p[j]] = (uint16_t)i;
     }
@@ -744,55 +972,78 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     int act[APT], avalid[APT], wexit[APT], hsl[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * BS;
+        const int i = tid + j * LPE;
         act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
         if (i >= n) continue;
         const int x = p[j] / W, y = p[j] - (p[j] / W) * W;
         skey[j] = encode(a, smc, x, y);
-        if (a.variant == kVarAC) {
-            DrawPh rng(a, genv, (uint32_t)i);
-            const int T = ac_decide(a, x, y, occ, dff, wexit[j], rng);
-            if (T >= 0) req[i] = (uint16_t)T;
-            continue;
-        }
         int coord[5], valid[5], inb[5];
         moves5(a, x, y, occ, coord, valid, inb);
+        int ex = -1;                               // first exit among the neighbours
+#pragma unroll
+        for (int k = 3; k >= 0; k--) ex = inb[k] && a.map[coord[k]] == 3 ? k : ex;
+        Policy P;
+        if (FFM_LABLATE & 4) {
+            req[i * D] = (uint16_t)p[j];
+            act[j] = 4; avalid[j] = 1;
+            continue;
+        }
+        if (a.variant == kVarAC) {
+            // ffm_core candidates: free neighbours, then stay if any (:126-164)
+            if ((valid[0] | valid[1] | valid[2] | valid[3]) == 0) continue;
+            int exv = -1;
+#pragma unroll
+            for (int k = 3; k >= 0; k--) exv = valid[k] && a.map[coord[k]] == 3 ? k : exv;
+            if (exv >= 0) {
+                wexit[j] = 1;
+                req[i] = (uint16_t)coord[exv];
+                continue;
+            }
+            ac_policy(a, coord, valid, dff, P);
+            if (P.none) continue;
+            DrawPh rng(a, genv, (uint32_t)i);
+            req[i] = (uint16_t)coord[policy_draw(P, 0.0, rng)];
+            continue;
+        }
         if (D == 1) {
-            int ex = -1;
-            for (int k = 0; k < 4; k++)
-                if (inb[k] && a.map[coord[k]] == 3) { ex = k; break; }
             int k;
             if (ex >= 0) {
                 wexit[j] = 1;
                 k = ex;
-            } else if (!actor) {
-                DrawPh rng(a, genv, (uint32_t)i);
-                k = critic_choose(a, coord, valid, dff, rng);
             } else {
+                if (!actor) {
+                    critic_policy(a, coord, valid, dff, P);
+                } else {
+                    hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+                    if (hsl[j] < 0) continue;
+                    actor_policy(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, false, P);
+                }
                 DrawPh rng(a, genv, (uint32_t)i);
-                hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
-                if (hsl[j] < 0) { k = 4; }
-                else k = actor_choose(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, false, rng);
+                k = policy_draw(P, actor ? a.epsilon : 0.0, rng);
             }
             req[i] = (uint16_t)coord[k];
             act[j] = k; avalid[j] = valid[k];
         } else {
-            int ex = -1;
+            // model/ffm_actor_only.py:214-355: decisions for the neighbours before the
+            // first exit, then the exit for the rest; the last one is the agent's action.
+            if (ex != 0) {
+                hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+                if (hsl[j] < 0) continue;
+                actor_policy(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, true, P);
+            }
+            int k = 4;
+#pragma unroll
             for (int d = 0; d < 4; d++) {
-                if (ex < 0 && inb[d] && a.map[coord[d]] == 3) ex = d;
-                int k;
-                if (ex >= 0) {
-                    wexit[j] = 1;
+                if (ex >= 0 && d >= ex) {
                     k = ex;
                 } else {
                     DrawPh rng(a, genv, (uint32_t)(i * 4 + d));
-                    if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
-                    if (hsl[j] < 0) k = 4;
-                    else k = actor_choose(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, true, rng);
+                    k = policy_draw(P, a.epsilon, rng);
                 }
-                req[i * D + d] = (uint16_t)coord[k];
-                act[j] = k; avalid[j] = valid[k];
+                req[i * 4 + d] = (uint16_t)coord[k];
             }
+            wexit[j] = ex >= 0;
+            act[j] = k; avalid[j] = valid[k];
         }
     }
     __syncthreads();
@@ -804,24 +1055,27 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     int nxt[APT], coll[APT], wins[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * BS;
+        const int i = tid + j * LPE;
         nxt[j] = p[j]; coll[j] = -1; wins[j] = 0;
         if (i >= n) continue;
         int best_owner = -1, best_won_owner = -1;
+#pragma unroll
         for (int d = 0; d < D; d++) {
             const int T = req[i * D + d];
             if (T == kNone16) continue;
             const int mine = i * D + d;
             const int tx = T / W, ty = T - (T / W) * W;
             int m = 0, owner = 0x7FFFFFFF, rank = 0;
+#pragma unroll
             for (int c5 = 0; c5 < 5; c5++) {
                 const int cx = c5 < 4 ? tx + kNBx[c5] : tx, cy = c5 < 4 ? ty + kNBy[c5] : ty;
                 if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
                 const int b = grid[cx * W + cy];
                 if (b == kNone16) continue;
+#pragma unroll
                 for (int d2 = 0; d2 < D; d2++) {
-                    if (req[b * D + d2] != T) continue;
                     const int sq = b * D + d2;
+                    if (req[sq] != T) continue;
                     m++;
                     owner = sq < owner ? sq : owner;
                     rank += sq < mine ? 1 : 0;
@@ -839,20 +1093,19 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             }
         }
     }
-    // deposits at the winners' own cells (distinct per agent: no races)
+    // deposits at the winners' own cells (distinct per agent: no races); every
+    // agent's next cell joins the next state map unless it is an exit
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        if (wins[j] == 0) continue;
-        float* c = a.dff_in + e * (long long)HW + p[j];
-        float v = *c;
-        for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
-        *c = v;
+        const int i = tid + j * LPE;
+        if (i >= n) continue;
+        if (wins[j]) {
+            float* c = a.dff_in + e * (long long)HW + p[j];
+            float v = *c;
+            for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
+            *c = v;
+        }
         if (a.map[nxt[j]] != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
-    }
-#pragma unroll
-    for (int j = 0; j < APT; j++) {        // non-movers keep their cells in the next state map
-        const int i = tid + j * BS;
-        if (i < n && wins[j] == 0 && a.map[nxt[j]] != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
     }
     __syncthreads();
 
@@ -860,8 +1113,8 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     const SmBits smn{a.map, bits};
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * BS;
-        if (i >= n) continue;
+        const int i = tid + j * LPE;
+        if (i >= n || (FFM_LABLATE & 2)) continue;
         double r = a.step_penalty;
         if (wexit[j]) r = r + a.exit_reward;
         if (coll[j] >= 0) r = r + (double)coll[j] * a.collision_penalty;
@@ -875,7 +1128,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         const int sv = tab_get(a.V, skey[j], a.overflow);
         if (sv < 0) continue;
         const double td = (r + a.gamma * vn) - a.V.vals[sv];
-        acc_add(a.V.acc + sv, fx(a.alpha_v * td));
+        if (!(FFM_LABLATE & 1)) acc_add(a.V.acc + sv, fx(a.alpha_v * td));
         if (!actor) continue;
         if (act[j] < 0) continue;
         if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
@@ -884,47 +1137,49 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             LearnRec rc;
             rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
             a.recs[e * A + i] = rc;
-        } else if (avalid[j]) {
+        } else if (avalid[j] && !(FFM_LABLATE & 1)) {
             acc_add(a.Ht.acc + (size_t)hsl[j] * 5 + act[j], fx(a.alpha_h * td));
         }
     }
 
     // ---- exit removal (order preserving), counters ---------------------------------------
-    int base = 0;
+    int base_ = 0;
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * BS;
+        const int i = tid + j * LPE;
         const bool keep = i < n && a.map[nxt[j]] != 3;
         int tot;
-        const int off = block_scan_flag<BS>(keep, ws, tot);
-        if (keep) a.pos[e * A + base + off] = (uint16_t)nxt[j];
-        base += tot;
+        const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
+        if (keep) a.pos[e * A + base_ + off] = (uint16_t)nxt[j];
+        base_ += tot;
     }
     __syncthreads();     // deposits visible to the whole workgroup before the stencil
 
     // ---- update_dff (model/ffm_unified.py:779-798) into the other buffer ---------------------
-    float* out = a.dff_out + e * (long long)HW;
-    for (int c = tid; c < HW; c += BS) {
-        const int x = c / W, y = c - (c / W) * W;
-        float acc = a.c0 * dff[c];
+    if (live && !(FFM_LABLATE & 8)) {
+        float* out = a.dff_out + e * (long long)HW;
+        for (int c = tid; c < HW; c += LPE) {
+            const int x = c / W, y = c - (c / W) * W;
+            float acc = a.c0 * dff[c];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int nx = x + kNBx[k], ny = y + kNBy[k];
-            const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? a.c0 * dff[nx * W + ny] : 0.0f;
-            const float t = a.c1 * v;
-            acc = acc + t;
+            for (int k = 0; k < 4; k++) {
+                const int nx = x + kNBx[k], ny = y + kNBy[k];
+                const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? a.c0 * dff[nx * W + ny] : 0.0f;
+                const float t = a.c1 * v;
+                acc = acc + t;
+            }
+            out[c] = acc < 1e-4f ? 0.0f : acc;
         }
-        out[c] = acc < 1e-4f ? 0.0f : acc;
     }
-    if (tid == 0) {
-        a.cnt[e] = base;
+    if (live && tid == 0) {
+        a.cnt[e] = base_;
         a.nstart[e] = n;
         const int st = a.ep_steps[e] + 1;
         a.ep_steps[e] = st;
-        a.done[e] = a.auto_reset && (base == 0 || (a.max_steps > 0 && st >= a.max_steps)) ? 1 : 0;
+        a.done[e] = a.auto_reset && (base_ == 0 || (a.max_steps > 0 && st >= a.max_steps)) ? 1 : 0;
         unsigned long long* slot = a.counters + 4 * e;
         slot[0] += (unsigned long long)n;
-        slot[1] += (unsigned long long)(n - base);
+        slot[1] += (unsigned long long)(n - base_);
         slot[3] += 1;
     }
 }
@@ -932,21 +1187,11 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
 // ===========================================================================
 // Table upkeep.
 // ===========================================================================
-__global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
+// Min / max / non-finite flag of the H values (the actor's global normalisation,
+// model/ffm_unified.py:413-426), reduced per block into hpart[block][4].
+__device__ __forceinline__ void hstat_block_reduce(double mn, double mx, int nf, uint32_t n, double* hpart) {
     __shared__ double smn[4], smx[4];
     __shared__ int snf[4];
-    const uint32_t n = *a.Ht.n;
-    double mn = __builtin_inf(), mx = -__builtin_inf();
-    int nf = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const double* v = a.Ht.vals + (size_t)a.Ht.order[i] * 5;
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            nf |= !__builtin_isfinite(v[k]);
-            mn = v[k] < mn ? v[k] : mn;
-            mx = v[k] > mx ? v[k] : mx;
-        }
-    }
     for (int o = 32; o > 0; o >>= 1) {
         const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
         mn = a2 < mn ? a2 : mn;
@@ -962,7 +1207,7 @@ __global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
             mx = smx[w] > mx ? smx[w] : mx;
             nf |= snf[w];
         }
-        double* o = a.hpart + blockIdx.x * 4;
+        double* o = hpart + blockIdx.x * 4;
         o[0] = n > 0 ? 1.0 : 0.0;
         o[1] = (double)nf;
         o[2] = mn;
@@ -970,48 +1215,86 @@ __global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
+    const uint32_t n = *a.Ht.n;
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    int nf = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const double* v = a.Ht.vals + (size_t)a.Ht.order[i] * 5;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            nf |= !__builtin_isfinite(v[k]);
+            mn = v[k] < mn ? v[k] : mn;
+            mx = v[k] > mx ? v[k] : mx;
+        }
+    }
+    hstat_block_reduce(mn, mx, nf, n, a.hpart);
+}
+
 __global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a) {
-    if (threadIdx.x != 0) return;
-    double mn = __builtin_inf(), mx = -__builtin_inf(), nf = 0.0;
-    for (int b = 0; b < kHstatBlocks; b++) {
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    int nf = 0;
+    for (int b = threadIdx.x; b < kHstatBlocks; b += 64) {
         const double* o = a.hpart + b * 4;
         mn = o[2] < mn ? o[2] : mn;
         mx = o[3] > mx ? o[3] : mx;
-        nf = o[1] != 0.0 ? 1.0 : nf;
+        nf |= o[1] != 0.0;
     }
-    a.hstat[0] = *a.Ht.n > 0 ? 1.0 : 0.0;
-    a.hstat[1] = nf;
-    a.hstat[2] = mn;
-    a.hstat[3] = mx;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
+        mn = a2 < mn ? a2 : mn;
+        mx = b2 > mx ? b2 : mx;
+        nf |= __shfl_xor(nf, o);
+    }
+    if (threadIdx.x == 0) {
+        a.hstat[0] = *a.Ht.n > 0 ? 1.0 : 0.0;
+        a.hstat[1] = nf ? 1.0 : 0.0;
+        a.hstat[2] = mn;
+        a.hstat[3] = mx;
+    }
 }
 
-template <int WIDTH>
-__global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T) {
+// Apply the step's fixed-point increments once; for H also reduce the statistics
+// the next step's actor reads (fusing the separate statistics pass).
+template <int WIDTH, bool STATS>
+__global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* hpart) {
     const uint32_t n = *T.n;
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    int nf = 0;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const size_t s = (size_t)T.order[i] * WIDTH;
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
             const long long q = T.acc[s + k];
+            double v = T.vals[s + k];
             if (q != 0) {
-                T.vals[s + k] = T.vals[s + k] + (double)q * (1.0 / kFxOne);
+                v = v + (double)q * (1.0 / kFxOne);
+                T.vals[s + k] = v;
                 T.acc[s + k] = 0;
+            }
+            if (STATS) {
+                nf |= !__builtin_isfinite(v);
+                mn = v < mn ? v : mn;
+                mx = v > mx ? v : mx;
             }
         }
     }
+    if (STATS) hstat_block_reduce(mn, mx, nf, n, hpart);
 }
 
 // _get_td_errors with the updated V, then the actor (model/ffm_unified.py:559-598).
-__global__ __launch_bounds__(64) void learn_post_kernel(LearnArgs a) {
-    const long long e = blockIdx.x;
-    const int n = a.nstart[e];
-    for (int i = threadIdx.x; i < n; i += 64) {
-        const LearnRec rc = a.recs[e * a.A + i];
-        if (rc.k < 0) continue;
-        const double vn = rc.snv >= 0 ? a.V.vals[rc.snv] : 0.0;
-        const double td = (rc.r + a.gamma * vn) - a.V.vals[rc.sv];
-        acc_add(a.Ht.acc + (size_t)rc.hslot * 5 + rc.k, fx(a.alpha_h * td));
-    }
+// One lane per (env, agent) slot.
+__global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
+    const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (g >= a.E * a.A) return;
+    const long long e = g / a.A;
+    const int i = (int)(g - e * a.A);
+    if (i >= a.nstart[e]) return;
+    const LearnRec rc = a.recs[g];
+    if (rc.k < 0) return;
+    const double vn = rc.snv >= 0 ? a.V.vals[rc.snv] : 0.0;
+    const double td = (rc.r + a.gamma * vn) - a.V.vals[rc.sv];
+    acc_add(a.Ht.acc + (size_t)rc.hslot * 5 + rc.k, fx(a.alpha_h * td));
 }
 
 __global__ __launch_bounds__(256) void learn_fill_default_kernel(LearnTable T, double v) {
@@ -1099,28 +1382,31 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
     }
 }
 
-template <int BS, int APT, int D>
+template <int BS, int EPB, int APT, int D>
 hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
-    const size_t smem = batch_carve(a.HW, a.A, D).total;
+    const size_t smem = batch_carve(a.HW, a.A, D).total * EPB;
     if (smem > 65536) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&learn_batch_kernel<BS, APT, D>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        const hipError_t e = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    learn_batch_kernel<BS, APT, D><<<dim3((unsigned)a.E), dim3(BS), smem, s>>>(a);
+    const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
+    learn_batch_kernel<BS, EPB, APT, D><<<dim3(blocks), dim3(BS), smem, s>>>(a);
     return hipGetLastError();
 }
 
 template <int D>
 hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
     const int A = a.A;
-    if (A <= 64) return launch_batch_t<64, 1, D>(a, s);
-    if (A <= 256) return launch_batch_t<256, 1, D>(a, s);
-    if (A <= 1024) return launch_batch_t<1024, 1, D>(a, s);
-    if (A <= 2048) return launch_batch_t<1024, 2, D>(a, s);
-    if (A <= 4096) return launch_batch_t<1024, 4, D>(a, s);
-    if (A <= 8192) return launch_batch_t<1024, 8, D>(a, s);
-    return launch_batch_t<1024, 16, D>(a, s);
+    if (A <= 32 && 2 * batch_carve(a.HW, A, D).total <= 64 * 1024) return launch_batch_t<64, 2, 1, D>(a, s);
+    if (A <= 64) return launch_batch_t<64, 1, 1, D>(a, s);
+    if (A <= 256) return launch_batch_t<256, 1, 1, D>(a, s);
+    if (A <= 1024) return launch_batch_t<1024, 1, 1, D>(a, s);
+    if (A <= 2048) return launch_batch_t<1024, 1, 2, D>(a, s);
+    if (A <= 4096) return launch_batch_t<1024, 1, 4, D>(a, s);
+    if (A <= 8192) return launch_batch_t<1024, 1, 8, D>(a, s);
+    return launch_batch_t<1024, 1, 16, D>(a, s);
 }
 
 }  // namespace
@@ -1151,13 +1437,17 @@ hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s) {
-    if (v) learn_apply_kernel<1><<<dim3(512), dim3(256), 0, s>>>(a.V);
-    if (h) learn_apply_kernel<5><<<dim3(512), dim3(256), 0, s>>>(a.Ht);
+    if (v) learn_apply_kernel<1, false><<<dim3(512), dim3(256), 0, s>>>(a.V, nullptr);
+    if (h) {     // H increments + the next step's statistics
+        learn_apply_kernel<5, true><<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s) {
-    learn_post_kernel<<<dim3((unsigned)a.E), dim3(64), 0, s>>>(a);
+    const long long slots = a.E * a.A;
+    learn_post_kernel<<<dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s>>>(a);
     return hipGetLastError();
 }
 

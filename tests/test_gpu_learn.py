@@ -256,3 +256,28 @@ def test_learner_full_size_invariants(variant, mode):
         assert len(set(cells.tolist())) == len(cells) and (flat[cells] == 0).all()
     assert (dff >= 0).all() and np.isfinite(dff).all()
     assert c["steps"] == 120 and c["agent_steps"] > 0
+
+
+def test_learner_full_hashed_table_reports_instead_of_hanging():
+    """A hashed table past 7/8 load refuses new keys; the host raises MemoryError."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    L = _learner(m, l1_sff(m), "ac", n_envs=256, n_agents=32, log2_v_capacity=8)
+    L.reset()
+    L.step(10)
+    with pytest.raises(MemoryError):
+        L.counters()
+    L.close()
+
+
+def test_learner_unified_dense_table_rejects_foreign_keys():
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd import learn_keys as K
+    m = make_room(12, 12)
+    L = _learner(m, l1_sff(m), "unified", n_envs=1, n_agents=4, mode="both", params={"block_size": 5})
+    L.import_table("V", [K.pack((1, 2, 3, 0), 2, 2)], [1.5])      # blocks 0..2 exist at bs 5
+    with pytest.raises(ValueError):
+        L.import_table("V", [K.pack((1, 2, 3, 0), 3, 0)], [1.5])
+    with pytest.raises(ValueError):
+        L.import_table("H", [K.pack((1,) * 13, 0, 0)], np.zeros((1, 5)))
+    L.close()
