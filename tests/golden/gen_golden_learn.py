@@ -26,6 +26,7 @@ import contextlib
 import io
 import json
 import os
+import pickle
 import random
 import sys
 import tempfile
@@ -49,21 +50,28 @@ def pack_key(variant, k):
 
 
 def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_steps, mode=None,
-             eps_sched=None, reload_v=False):
+             eps_sched=None, reload_v=False, pretrained=None):
+    """pretrained: (keys, values) of a critic pickled as the drivers' pretrained_v_path
+    (bytes keys, run_actor_only_training.py:24, run_unified_actor_training.py:30)."""
     H, W = map_array.shape
     init, nsteps, counts, cells, hashes = [], [], [], [], []
     vk, vv, vn, hk, hv, hn, np_tail, py_tail, eps_list = [], [], [], [], [], [], [], [], []
     with tempfile.TemporaryDirectory() as td:
         sff_path = os.path.join(td, "sff.npy")
         np.save(sff_path, sff)
+        kw = {}
+        if pretrained is not None:
+            kw["pretrained_v_path"] = os.path.join(td, "v.pkl")
+            with open(kw["pretrained_v_path"], "wb") as f:
+                pickle.dump(dict(zip(pretrained[0], pretrained[1])), f)
         for seed in seeds:
             np.random.seed(seed)
             random.seed(seed)
             with contextlib.redirect_stdout(io.StringIO()):
                 if variant == "unified":
-                    model = cls(map_array, sff_path, N, learning_mode=mode, params=dict(params))
+                    model = cls(map_array, sff_path, N, learning_mode=mode, params=dict(params), **kw)
                 else:
-                    model = cls(map_array, sff_path, N, params=dict(params))
+                    model = cls(map_array, sff_path, N, params=dict(params), **kw)
             for ep in range(n_ep):
                 if ep > 0:
                     if reload_v:
@@ -109,6 +117,11 @@ def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_ste
         h_keys=np.asarray(hk, np.uint64), h_vals=np.asarray(hv, np.float64).reshape(-1, 5),
         h_n=np.asarray(hn, np.int64), np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
     )
+    if pretrained is not None:
+        out["pre_keys"] = np.asarray([pack_key(variant if variant == "unified" else "ac", pickle.loads(k))
+                                      if variant == "unified" else K.from_cells_bytes(k)
+                                      for k in pretrained[0]], np.uint64)
+        out["pre_vals"] = np.asarray(pretrained[1], np.float64)
     path = os.path.join(HERE, f"learn_{name}.npz")
     np.savez_compressed(path, **out)
     print(f"{name}: seeds={len(seeds)} episodes={len(nsteps)} steps={sum(nsteps)} |V|={vn} |H|={hn} "
@@ -118,11 +131,20 @@ def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_ste
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated case names to (re)generate")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
     sys.path.insert(0, args.ref)
     from model.ffm_ac_core import FloorFieldModel as AC
     from model.ffm_unified import FloorFieldModelUnified as UNI
     from model.ffm_actor_only import FloorFieldModelActorOnly as AO
+
+    global run_case
+    _run = run_case
+
+    def run_case(name, *a, **kw):        # noqa: F811 -- filter by --only
+        if not only or name in only:
+            _run(name, *a, **kw)
 
     z = np.load(os.path.join(HERE, "room_12x12_reference.npz"))
     m12, s12 = z["map"], z["sff"]
@@ -151,6 +173,32 @@ def main():
     run_case("actoronly_12x12_N16", "actor_only", AO, m12, s12, ao_p, 16, [12, 13], 4, 300,
              eps_sched=eps)
     run_case("actoronly_12x12_N32_eps0", "actor_only", AO, m12, s12, ao_p, 32, [14], 2, 300)
+
+    # pretrained critics (the drivers' pretrained_v_path): a critic recorded by the
+    # reference itself, pickled with bytes keys like the critic-training scripts
+    # write them; ffm_unified re-keys them to tuples and uses them, ffm_actor_only's
+    # tuple keys never meet its bytes keys (model/ffm_actor_only.py:59-64).
+    np.random.seed(99)
+    random.seed(99)
+    with tempfile.TemporaryDirectory() as td, contextlib.redirect_stdout(io.StringIO()):
+        sp = os.path.join(td, "s.npy")
+        np.save(sp, s12)
+        cu = UNI(m12, sp, 16, learning_mode="critic_only", params=dict(uni_p))
+        for _ in range(3):
+            cu.reset()
+            cu.run(max_steps=300)
+        Vu = cu.get_v_table()
+        ca = AC(m12, sp, 16, params={"k_S": 3, "block_size": 5})
+        for _ in range(3):
+            ca.reset()
+            ca.run(max_steps=300)
+        Va = ca.get_v_table()
+    pre_u = ([pickle.dumps(k) for k in Vu.keys()], [float(v) for v in Vu.values()])
+    pre_a = (list(Va.keys()), [float(v) for v in Va.values()])
+    run_case("unified_actor_pretrained_12x12_N16", "unified", UNI, m12, s12, uni_p, 16, [15], 3, 300,
+             mode="actor_only", eps_sched=eps, pretrained=pre_u)
+    run_case("actoronly_pretrained_12x12_N16", "actor_only", AO, m12, s12, ao_p, 16, [16], 3, 300,
+             eps_sched=eps, pretrained=pre_a)
 
 
 if __name__ == "__main__":

@@ -143,3 +143,38 @@ def test_room_generator_matches_reference_recipe():
     s = l1_sff(make_room(12, 12))
     assert s.dtype == z["sff"].dtype == np.float32
     assert np.array_equal(s, z["sff"])
+
+
+def test_learning_dropin_signatures_match_reference():
+    """Constructor and method signatures of the reference classes:
+    model/ffm_ac_core.py:9, model/ffm_unified.py:27-35, model/ffm_actor_only.py:21-23."""
+    from ffm_amd.model.ffm_ac_core import FloorFieldModel as AC
+    from ffm_amd.model.ffm_actor_only import FloorFieldModelActorOnly as AO
+    from ffm_amd.model.ffm_unified import FloorFieldModelUnified as UNI
+    sig = lambda f: list(inspect.signature(f).parameters)
+    assert sig(AC.__init__) == ["self", "map_array", "sff_path", "N", "params"]
+    assert sig(UNI.__init__) == ["self", "map_array", "sff_path", "N", "learning_mode", "pretrained_v_path", "params"]
+    assert inspect.signature(UNI.__init__).parameters["learning_mode"].default == "critic_only"
+    assert sig(AO.__init__) == ["self", "map_array", "sff_path", "N", "pretrained_v_path", "params"]
+    assert sig(AC.run) == ["self", "save_prefix", "save_interval", "max_steps"]
+    for c in (UNI, AO):
+        assert sig(c.run) == ["self", "save_prefix", "save_interval", "max_steps", "return_trajectory"]
+    assert sig(UNI.reset) == ["self", "exit_pos", "radius"] and sig(UNI.initialize_agents) == sig(UNI.reset)
+    for c, meths in ((AC, ["get_v_table", "set_v_table", "get_v_table_size", "reset", "step", "update_dff"]),
+                     (UNI, ["get_v_table", "set_v_table", "get_v_table_size", "get_h_table", "get_h_table_size",
+                            "set_epsilon", "step", "update_dff"]),
+                     (AO, ["get_v_table", "get_v_table_size", "get_h_table", "get_h_table_size", "set_epsilon",
+                           "reset", "step", "update_dff"])):
+        for m in meths:
+            assert callable(getattr(c, m)), (c, m)
+
+
+def test_unified_dropin_rejects_bad_mode_before_device(tmp_path):
+    """ValueError of model/ffm_unified.py:59-63, raised before any device work."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.model.ffm_unified import FloorFieldModelUnified as UNI
+    m = make_room(12, 12)
+    p = str(tmp_path / "s.npy")
+    np.save(p, l1_sff(m))
+    with pytest.raises(ValueError, match="learning_mode must be one of"):
+        UNI(m, p, 4, learning_mode="greedy")

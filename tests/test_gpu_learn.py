@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 
 from golden_util import GOLDEN_DIR, dff_hash
+from test_learn_oracle import pretrained
 
 pytestmark = pytest.mark.gpu
 
@@ -61,6 +62,7 @@ def test_learner_replays_reference_goldens(name):
     for si, seed in enumerate(z["seeds"]):
         L = _learner(z["map"], z["sff"], variant, n_envs=1, n_agents=0, agent_capacity=max(N, 1), mode=mode,
                      params=params, rng="mt", auto_reset=False)
+        inert_k, inert_v = pretrained(z, variant, lambda k, v: L.import_table("V", k, v))
         np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
         for ep in range(n_ep):
             if ep > 0 and int(z["reload_v"]):
@@ -93,6 +95,7 @@ def test_learner_replays_reference_goldens(name):
             py_rng.pos = ppos
             ep_i += 1
         vk, vv = L.export_table("V")
+        vk, vv = np.concatenate([inert_k, vk]), np.concatenate([inert_v, vv])
         nv = int(z["v_n"][si])
         assert len(vk) == nv, f"seed {seed}: |V| {len(vk)} != {nv}"
         assert np.array_equal(vk, z["v_keys"][v_off:v_off + nv]), f"seed {seed}: V keys / order"

@@ -25,6 +25,20 @@ def load(name):
     return {k: z[k] for k in z.files}
 
 
+def pretrained(z, variant, load):
+    """A fixture's pretrained critic (model/ffm_unified.py:84-110, model/ffm_actor_only.py:55-70).
+    ffm_unified loads it into V; ffm_actor_only keys it by tuples that its bytes keys
+    never match, so it stays inert and only leads get_v_table()'s order.
+    Returns that inert prefix (keys, values)."""
+    none = (np.zeros(0, np.uint64), np.zeros(0, np.float64))
+    if "pre_keys" not in z:
+        return none
+    if variant == "unified":
+        load(z["pre_keys"], z["pre_vals"])
+        return none
+    return z["pre_keys"], z["pre_vals"]
+
+
 def replay(z, make_step):
     """Drive one fixture through `make_step(learn, seed)`; returns per-seed learn objects."""
     params = json.loads(str(z["params"]))
@@ -36,6 +50,7 @@ def replay(z, make_step):
     v_off = h_off = 0
     for si, seed in enumerate(z["seeds"]):
         L = LO.Learn(z["map"], z["sff"], variant, mode, params)
+        inert_k, inert_v = pretrained(z, variant, lambda k, v: L.V.load(k, v))
         np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
         for ep in range(n_ep):
             if ep > 0 and int(z["reload_v"]):
@@ -56,6 +71,7 @@ def replay(z, make_step):
                 step_i += 1
             ep_i += 1
         vk, vv = L.V.export()
+        vk, vv = np.concatenate([inert_k, vk]), np.concatenate([inert_v, vv])
         nv = int(z["v_n"][si])
         assert len(vk) == nv, f"seed {seed}: |V| {len(vk)} != {nv}"
         assert np.array_equal(vk, z["v_keys"][v_off:v_off + nv]), f"seed {seed}: V keys / order"
