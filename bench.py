@@ -228,7 +228,14 @@ def bench_learner(args, world, rank, torch, dist):
                 device=torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     L.reset(stream)
-    L.step(args.warmup, stream)
+    if world > 1:
+        # the ranks share V / H: every step exchanges the table deltas over RCCL
+        from ffm_amd.dist import TableSync
+        sync = TableSync(L, device="cuda", capacity=1 << 18)
+        run = sync.step
+    else:
+        run = lambda k: L.step(k, stream)  # noqa: E731
+    run(args.warmup)
     torch.cuda.synchronize()
     c0 = L.counters(stream)
     print(f"[bench] config {args.config}: warmup done", file=sys.stderr, flush=True)
@@ -236,7 +243,7 @@ def bench_learner(args, world, rank, torch, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    L.step(args.steps, stream)
+    run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -249,7 +256,7 @@ def bench_learner(args, world, rank, torch, dist):
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
-    L.step(nk, stream)
+    run(nk)
     ev1.record(stream)
     torch.cuda.synchronize()
     step_ms = ev0.elapsed_time(ev1) / nk

@@ -70,6 +70,8 @@ struct ffm_learner {
     unsigned char* d_scratch = nullptr;
     uint32_t dense_bx = 0;             // dense tables: x blocks (import validation)
     bool hstat_valid = false;          // d_hstat holds the H statistics of the current table
+    int phase = 0;                     // batched step in phases: 0 idle, 1 local done, 2 V applied
+    unsigned long long* d_count = nullptr;   // delta export record counter
     DevTable V, H;
 };
 
@@ -79,13 +81,14 @@ static void free_table(DevTable& T) {
     (void)hipFree(T.t.acc);
     (void)hipFree(T.t.order);
     (void)hipFree(T.t.n);
+    (void)hipFree(T.t.mark);
 }
 
 static void release(ffm_learner* l) {
     if (!l) return;
     void* bufs[] = {l->d_map, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
-                    l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch};
+                    l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count};
     for (void* p : bufs) (void)hipFree(p);
     free_table(l->V);
     free_table(l->H);
@@ -111,7 +114,8 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     if ((e = hipMalloc((void**)&T.t.acc, T.cap * width * 8)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.order, T.cap * 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.n, 4)) != hipSuccess) return e;
-    return hipSuccess;
+    if ((e = hipMalloc((void**)&T.t.mark, 4)) != hipSuccess) return e;
+    return hipMemset(T.t.mark, 0, 4);
 }
 
 static ffm::LearnArgs make_args(ffm_learner* l) {
@@ -272,6 +276,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     ALLOC(l->d_hpart, (size_t)ffm::kHstatBlocks * 4 * 8);
     if (l->post_update && !l->mt) ALLOC(l->d_recs, E * A * sizeof(ffm::LearnRec));
     ALLOC(l->d_overflow, 4);
+    ALLOC(l->d_count, 8);
     if (l->mt) {
         ALLOC(l->d_mt_np, E * 625 * 4);
         ALLOC(l->d_mt_py, E * 625 * 4);
@@ -339,8 +344,44 @@ int ffm_learner_reset(ffm_learner* l, void* stream) {
     return check_overflow(l, s);
 }
 
+// The batched step in phases (multi-rank runs exchange the table deltas between
+// them, ffm_amd/dist.py TableSync): local -> [exchange V (+H)] -> apply V (+ the
+// post-update actor increments) -> [exchange H] -> apply H -> end.
+static int phase_local(ffm_learner* l, hipStream_t s) {
+    // H statistics of the step-start table: produced by the previous step's H
+    // apply, recomputed only after the table was replaced (create / import)
+    if (l->actor && !l->hstat_valid) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
+    HIP_TRY(hipMemcpyAsync(l->V.t.mark, l->V.t.n, 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(l->H.t.mark, l->H.t.n, 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
+    l->phase = 1;
+    return FFM_OK;
+}
+
+static int phase_apply(ffm_learner* l, int32_t which, hipStream_t s) {
+    if (which == FFM_TABLE_V) {
+        HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
+        if (l->post_update) HIP_TRY(ffm::launch_learn_post(make_args(l), s));
+        l->phase = 2;
+        return FFM_OK;
+    }
+    HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
+    l->hstat_valid = true;
+    l->phase = 3;
+    return FFM_OK;
+}
+
+static int phase_end(ffm_learner* l, hipStream_t s) {
+    l->cur ^= 1;
+    if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
+    l->t++;
+    l->phase = 0;
+    return FFM_OK;
+}
+
 int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
     if (!l || n_steps < 0) return fail(FFM_E_INVALID, "bad learner/n_steps");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
     hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n_steps; i++) {
         if (l->mt) {
@@ -348,18 +389,65 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             l->t++;
             continue;
         }
-        // H statistics of the step-start table: produced by the previous step's H
-        // apply, recomputed only after the table was replaced (create / import)
-        if (l->actor && !l->hstat_valid) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
-        HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
-        HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
-        if (l->post_update) HIP_TRY(ffm::launch_learn_post(make_args(l), s));
-        if (l->actor) HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
-        l->hstat_valid = l->actor;
-        l->cur ^= 1;
-        if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
-        l->t++;
+        int rc = phase_local(l, s);
+        if (!rc) rc = phase_apply(l, FFM_TABLE_V, s);
+        if (!rc && l->actor) rc = phase_apply(l, FFM_TABLE_H, s);
+        if (!rc) rc = phase_end(l, s);
+        if (rc) return rc;
     }
+    return FFM_OK;
+}
+
+int ffm_learner_step_local(ffm_learner* l, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->mt) return fail(FFM_E_INVALID, "phased steps are the batched (Philox) step");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "step_local: previous step not ended");
+    return phase_local(l, (hipStream_t)stream);
+}
+
+int ffm_learner_step_apply(ffm_learner* l, int32_t which, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (which == FFM_TABLE_V && l->phase != 1) return fail(FFM_E_INVALID, "step_apply(V) must follow step_local");
+    if (which == FFM_TABLE_H && (!l->actor || l->phase != 2))
+        return fail(FFM_E_INVALID, "step_apply(H) must follow step_apply(V) (actor variants only)");
+    if (which != FFM_TABLE_V && which != FFM_TABLE_H) return fail(FFM_E_INVALID, "which");
+    return phase_apply(l, which, (hipStream_t)stream);
+}
+
+int ffm_learner_step_end(ffm_learner* l, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->phase != (l->actor ? 3 : 2)) return fail(FFM_E_INVALID, "step_end before the tables were applied");
+    return phase_end(l, (hipStream_t)stream);
+}
+
+int ffm_learner_delta_export(ffm_learner* l, int32_t which, uint64_t* d_keys, int64_t* d_acc, int64_t cap,
+                             int64_t* n, void* stream) {
+    if (!l || !n) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if (l->phase == 0) return fail(FFM_E_INVALID, "delta_export outside a phased step");
+    if (cap > 0 && (!d_keys || !d_acc)) return fail(FFM_E_INVALID, "null record buffers");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(l->d_count, 0, 8, s));
+    HIP_TRY(ffm::launch_learn_delta_export(T->t, T->width, reinterpret_cast<unsigned long long*>(d_keys),
+                                           reinterpret_cast<long long*>(d_acc), cap, l->d_count, s));
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, l->d_count, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n = (int64_t)c;
+    if ((int64_t)c > cap) return fail(FFM_E_INVALID, "delta_export: record buffer too small (*n holds the size)");
+    return FFM_OK;
+}
+
+int ffm_learner_delta_merge(ffm_learner* l, int32_t which, const uint64_t* d_keys, const int64_t* d_acc, int64_t n,
+                            void* stream) {
+    if (!l || n < 0) return fail(FFM_E_INVALID, "bad argument");
+    DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if (l->phase == 0) return fail(FFM_E_INVALID, "delta_merge outside a phased step");
+    HIP_TRY(ffm::launch_learn_delta_merge(T->t, T->width, reinterpret_cast<const unsigned long long*>(d_keys),
+                                          reinterpret_cast<const long long*>(d_acc), n, l->d_overflow,
+                                          (hipStream_t)stream));
     return FFM_OK;
 }
 

@@ -26,6 +26,7 @@ struct LearnTable {
     long long* acc;             // [cap * width] fixed-point (2^-32) increments of the batched step
     uint32_t* order;            // [cap] slot of the i-th inserted key
     uint32_t* n;                // [1] keys inserted
+    uint32_t* mark;             // [1] n at the start of the current batched step (delta export)
     uint32_t mask;              // cap - 1
     // Dense layout (ffm_unified's rank keys): slot = ranks | (bx * dense_by + by) << 8,
     // injective, so no probing and never full.  0 = hashed (13-cell keys).
@@ -84,6 +85,10 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
+                                    long long cap, unsigned long long* count, hipStream_t s);
+hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsigned long long* keys,
+                                   const long long* acc, long long n, int* overflow, hipStream_t s);
 hipError_t launch_learn_import(const LearnTable& T, int width, const unsigned long long* keys, const double* vals,
                               long long n, int* overflow, hipStream_t s);
 

@@ -17,6 +17,8 @@
 //    (integer atomics: order-free, so the result is deterministic) and applied
 //    once per step by learn_apply_kernel.
 // All translation units are built with -ffp-contract=off.
+#include <algorithm>
+
 #include "device_common.h"
 #include "learn_kernels.h"
 
@@ -1370,6 +1372,46 @@ __global__ __launch_bounds__(kResetBS) void learn_reset_kernel(LearnArgs a, int 
     }
 }
 
+// ---- delta exchange of the batched step (multi-rank) ----
+// Entries touched this step: inserted since the mark, or with pending increments.
+template <int WIDTH>
+__global__ __launch_bounds__(256) void learn_delta_export_kernel(LearnTable T, unsigned long long* keys,
+                                                                 long long* acc, long long cap,
+                                                                 unsigned long long* count) {
+    const uint32_t n = *T.n, mark = *T.mark;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const size_t s = T.order[i];
+        long long q[WIDTH];
+        bool touched = i >= mark;
+#pragma unroll
+        for (int k = 0; k < WIDTH; k++) {
+            q[k] = T.acc[s * WIDTH + k];
+            touched = touched || q[k] != 0;
+        }
+        if (!touched) continue;
+        const unsigned long long r = atomicAdd(count, 1ull);
+        if ((long long)r >= cap) continue;
+        keys[r] = T.keys[s];
+#pragma unroll
+        for (int k = 0; k < WIDTH; k++) acc[r * WIDTH + k] = q[k];
+    }
+}
+
+// Another rank's records: insert missing keys (default values), add increments.
+template <int WIDTH>
+__global__ __launch_bounds__(256) void learn_delta_merge_kernel(LearnTable T, const unsigned long long* keys,
+                                                                const long long* acc, long long n, int* overflow) {
+    for (long long r = (long long)blockIdx.x * 256 + threadIdx.x; r < n; r += (long long)gridDim.x * 256) {
+        const int s = tab_get(T, keys[r], overflow);
+        if (s < 0) continue;
+#pragma unroll
+        for (int k = 0; k < WIDTH; k++) {
+            const long long q = acc[r * WIDTH + k];
+            if (q != 0) acc_add(T.acc + (size_t)s * WIDTH + k, q);
+        }
+    }
+}
+
 // Insert keys in the given order (one lane: the insertion order is the dict
 // order the reference's get_v_table / get_h_table return) and set their values.
 __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int width, const unsigned long long* keys,
@@ -1461,6 +1503,22 @@ hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     learn_reset_kernel<<<dim3((unsigned)a.E), dim3(kResetBS), smem, s>>>(a, all ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
+                                    long long cap, unsigned long long* count, hipStream_t s) {
+    if (width == 1) learn_delta_export_kernel<1><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
+    else learn_delta_export_kernel<5><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsigned long long* keys,
+                                   const long long* acc, long long n, int* overflow, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<long long>(4096, (n + 255) / 256);
+    if (width == 1) learn_delta_merge_kernel<1><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow);
+    else learn_delta_merge_kernel<5><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow);
     return hipGetLastError();
 }
 

@@ -33,7 +33,8 @@ EXPORTED = [
     "ffm_learner_set_mt_state", "ffm_learner_get_mt_state", "ffm_learner_get_counters",
     "ffm_learner_set_epsilon", "ffm_learner_set_v_default", "ffm_learner_table_size",
     "ffm_learner_export_table", "ffm_learner_import_table", "ffm_learner_get_step_index",
-    "ffm_learner_set_step_index",
+    "ffm_learner_set_step_index", "ffm_learner_step_local", "ffm_learner_step_apply", "ffm_learner_step_end",
+    "ffm_learner_delta_export", "ffm_learner_delta_merge",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY = 1, 2, 3
@@ -120,6 +121,11 @@ def load_library():
     L.ffm_learner_import_table.argtypes = [P, i32, P, P, i64, P]
     L.ffm_learner_get_step_index.argtypes = [P, C.POINTER(C.c_uint32)]
     L.ffm_learner_set_step_index.argtypes = [P, C.c_uint32]
+    L.ffm_learner_step_local.argtypes = [P, P]
+    L.ffm_learner_step_apply.argtypes = [P, i32, P]
+    L.ffm_learner_step_end.argtypes = [P, P]
+    L.ffm_learner_delta_export.argtypes = [P, i32, P, P, i64, C.POINTER(i64), P]
+    L.ffm_learner_delta_merge.argtypes = [P, i32, P, P, i64, P]
     for name in EXPORTED:
         if name != "ffm_last_error":
             getattr(L, name).restype = C.c_int
@@ -547,6 +553,42 @@ class Learner:
         k = np.ascontiguousarray(keys, dtype=np.uint64)
         v = np.ascontiguousarray(vals, dtype=np.float64).reshape(len(k), width)
         _check(self._L.ffm_learner_import_table(self._h, w, _ptr(k), _ptr(v), len(k), _stream_handle(stream)))
+
+    # -- the batched step in phases (multi-rank table exchange, ffm_amd/dist.py) -----------
+    @property
+    def actor(self) -> bool:
+        return self.variant == "actor_only" or (self.variant == "unified" and self.mode != "critic_only")
+
+    @property
+    def post_update(self) -> bool:
+        """ffm_unified actor_only: the actor's increments use the V of after the V apply."""
+        return self.variant == "unified" and self.mode == "actor_only"
+
+    def step_local(self, stream=None):
+        _check(self._L.ffm_learner_step_local(self._h, _stream_handle(stream)))
+
+    def step_apply(self, which: str, stream=None):
+        _check(self._L.ffm_learner_step_apply(self._h, TABLE_V if which == "V" else TABLE_H, _stream_handle(stream)))
+
+    def step_end(self, stream=None):
+        _check(self._L.ffm_learner_step_end(self._h, _stream_handle(stream)))
+
+    def delta_export(self, which: str, keys_ptr: int, acc_ptr: int, cap: int, stream=None) -> int:
+        """Write this step's touched entries of table `which` to device buffers (u64 keys,
+        i64 [width] increments) and return the record count.  A count above `cap`
+        means the buffers were too small: nothing usable was written, call again
+        with buffers of that size (the export does not change the table)."""
+        n = C.c_int64()
+        rc = self._L.ffm_learner_delta_export(self._h, TABLE_V if which == "V" else TABLE_H, keys_ptr, acc_ptr,
+                                              int(cap), C.byref(n), _stream_handle(stream))
+        if rc == E_INVALID and n.value > cap:
+            return int(n.value)
+        _check(rc)
+        return int(n.value)
+
+    def delta_merge(self, which: str, keys_ptr: int, acc_ptr: int, n: int, stream=None):
+        _check(self._L.ffm_learner_delta_merge(self._h, TABLE_V if which == "V" else TABLE_H, keys_ptr, acc_ptr,
+                                               int(n), _stream_handle(stream)))
 
     # -- telemetry -----------------------------------------------------------------------
     def counters(self, stream=None) -> dict:

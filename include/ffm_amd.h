@@ -212,6 +212,24 @@ int ffm_learner_export_table(ffm_learner* l, int32_t which, uint64_t* keys, doub
 /* Replace the table by these entries, inserted in the given order. */
 int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys, const double* vals,
                              int64_t n, void* stream);
+/* The batched (Philox) step in phases, for multi-rank runs whose ranks share
+ * the tables (ffm_amd/dist.py TableSync):
+ *   step_local -> exchange V (and H unless unified actor_only) -> step_apply(V)
+ *   -> [unified actor_only: exchange H] -> step_apply(H) (actor variants) -> step_end.
+ * ffm_learner_step == the same phases with no exchange.  A delta record is a
+ * key (u64) and its pending fixed-point increments (width i64: 1 for V, 5 for H)
+ * for every entry inserted or incremented during this step; a rank merges the
+ * other ranks' records (inserting missing keys) before applying, so every rank
+ * ends the step with the tables a single device holding all envs would have.
+ * Record buffers are DEVICE pointers; export fails with *n = the count needed
+ * when cap is too small. */
+int ffm_learner_step_local(ffm_learner* l, void* stream);
+int ffm_learner_step_apply(ffm_learner* l, int32_t which, void* stream);
+int ffm_learner_step_end(ffm_learner* l, void* stream);
+int ffm_learner_delta_export(ffm_learner* l, int32_t which, uint64_t* d_keys, int64_t* d_acc, int64_t cap,
+                             int64_t* n, void* stream);
+int ffm_learner_delta_merge(ffm_learner* l, int32_t which, const uint64_t* d_keys, const int64_t* d_acc,
+                            int64_t n, void* stream);
 int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t);
 int ffm_learner_set_step_index(ffm_learner* l, uint32_t t);
 

@@ -27,6 +27,7 @@ static const int NB[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};   /* U, D, L, R:
 struct ffo_tab {
     int32_t width;
     int64_t cap, n;
+    int64_t mark;          /* n at the start of the current batched step */
     uint64_t* keys;
     double* vals;
     int64_t* acc;          /* batched fixed-point increments */
@@ -93,6 +94,40 @@ static int64_t tab_get_sync(ffo_tab* t, uint64_t key, const double* init, int pa
         s = tab_get(t, key, init);
     }
     return s;
+}
+
+/* ---- delta exchange of the batched step (multi-rank) ---- */
+void ffo_tab_mark(ffo_tab* t) { t->mark = t->n; }
+
+/* Entries touched since the mark: inserted after it, or with pending increments.
+ * keys [n], acc [n][width]; returns n. */
+int64_t ffo_tab_delta_export(const ffo_tab* t, uint64_t* keys, int64_t* acc) {
+    int64_t m = 0;
+    for (int64_t i = 0; i < t->n; i++) {
+        const int64_t s = t->order[i];
+        int touched = i >= t->mark;
+        for (int k = 0; k < t->width; k++) touched |= t->acc[s * t->width + k] != 0;
+        if (!touched) continue;
+        keys[m] = t->keys[s];
+        memcpy(acc + m * t->width, t->acc + s * t->width, sizeof(int64_t) * (size_t)t->width);
+        m++;
+    }
+    return m;
+}
+
+/* Add another rank's records: insert missing keys with `init`, add increments. */
+int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, int64_t n, const double* init) {
+    for (int64_t r = 0; r < n; r++) {
+        const int64_t s = tab_get(t, keys[r], init);
+        if (s < 0) return -1;
+        for (int k = 0; k < t->width; k++) t->acc[s * t->width + k] += acc[r * t->width + k];
+    }
+    return 0;
+}
+
+void ffo_tab_apply(ffo_tab* t) {
+    for (int64_t s = 0; s < t->cap * t->width; s++)
+        if (t->acc[s]) { t->vals[s] = t->vals[s] + (double)t->acc[s] * (1.0 / FX_ONE); t->acc[s] = 0; }
 }
 
 int ffo_tab_import(ffo_tab* t, const uint64_t* keys, const double* vals, int64_t n) {
@@ -736,25 +771,46 @@ int ffo_learn_step_mt(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int32_t* 
     return rc;
 }
 
-int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E,
-                                int32_t A_cap, uint16_t* pos, int32_t* counts, float* dff,
-                                int32_t* episodes, int32_t* ep_steps, uint64_t seed, uint32_t t,
-                                int32_t auto_reset, int32_t N_reset, int32_t max_steps,
-                                int64_t env_base, uint64_t* agent_steps, int nthreads) {
+/* ---- the batched step in phases ------------------------------------------------ */
+struct ffo_lbatch {
+    const ffo_learn_cfg* c;
+    ffo_tab *V, *Ht;
+    int64_t E;
+    int32_t A_cap;
+    lrec* recs;
+    int32_t* nstart;
+};
+
+ffo_lbatch* ffo_lbatch_new(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E, int32_t A_cap) {
+    ffo_lbatch* b = (ffo_lbatch*)calloc(1, sizeof(ffo_lbatch));
+    b->c = c; b->V = V; b->Ht = Ht; b->E = E; b->A_cap = A_cap;
+    b->recs = (lrec*)calloc((size_t)(E * A_cap), sizeof(lrec));
+    b->nstart = (int32_t*)calloc((size_t)E, sizeof(int32_t));
+    return b;
+}
+
+void ffo_lbatch_free(ffo_lbatch* b) {
+    if (!b) return;
+    free(b->recs); free(b->nstart); free(b);
+}
+
+/* Every env's step against the tables as they are; increments left pending. */
+int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, uint64_t seed, uint32_t t,
+                     int64_t env_base, uint64_t* agent_steps, int nthreads) {
+    const ffo_learn_cfg* c = b->c;
     const int HW = c->H * c->W;
+    const int64_t E = b->E;
+    const int32_t A_cap = b->A_cap;
     const int actor = c->variant == FFO_VAR_ACTOR_ONLY ||
                       (c->variant == FFO_VAR_UNIFIED && c->mode != FFO_MODE_CRITIC);
-    const int post_update = c->variant == FFO_VAR_UNIFIED && c->mode == FFO_MODE_ACTOR;
     hstats hs;
     memset(&hs, 0, sizeof hs);
-    if (actor) h_stats(Ht, &hs);
+    if (actor) h_stats(b->Ht, &hs);
     float smin, smax;
     sff_minmax(c, &smin, &smax);
-    lrec* recs = (lrec*)calloc((size_t)(E * A_cap), sizeof(lrec));
-    int32_t* nstart = (int32_t*)malloc(sizeof(int32_t) * (size_t)E);
-    ffo_core_cfg cc;
-    memset(&cc, 0, sizeof cc);
-    cc.H = c->H; cc.W = c->W; cc.map = c->map; cc.nb = 4;
+    ffo_tab_mark(b->V);
+    ffo_tab_mark(b->Ht);
+    memset(b->recs, 0, sizeof(lrec) * (size_t)(E * A_cap));
     uint64_t total = 0;
     int err = 0;
     const int nt = nthreads > 0 ? nthreads : 1;
@@ -769,7 +825,7 @@ int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht,
         int32_t* p32 = (int32_t*)malloc(sizeof(int32_t) * (size_t)(A_cap + 1));
         lctx L;
         memset(&L, 0, sizeof L);
-        L.c = c; L.V = V; L.Ht = Ht; L.jacobi = 1; L.parallel = nt > 1;
+        L.c = c; L.V = b->V; L.Ht = b->Ht; L.jacobi = 1; L.parallel = nt > 1;
         L.hs = hs; L.smin = smin; L.smax = smax;
         L.rng.philox = 1; L.rng.seed = seed; L.rng.t = t;
 #ifdef _OPENMP
@@ -778,46 +834,71 @@ int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht,
         for (int64_t e = 0; e < E; e++) {
             uint16_t* pe = pos + e * (int64_t)A_cap;
             int32_t n = counts[e];
-            nstart[e] = n;
+            b->nstart[e] = n;
             total += (uint64_t)n;
             for (int i = 0; i < n; i++) p32[i] = pe[i];
             L.rng.genv = (uint64_t)(env_base + e);
-            if (env_step(&L, p32, &n, dff + e * (int64_t)HW, occ, sm, sm + HW, B, recs + e * (int64_t)A_cap))
+            if (env_step(&L, p32, &n, dff + e * (int64_t)HW, occ, sm, sm + HW, B, b->recs + e * (int64_t)A_cap))
                 err = 1;
             for (int i = 0; i < n; i++) pe[i] = (uint16_t)p32[i];
             counts[e] = n;
         }
         free(occ); free(sm); free(B); free(p32);
     }
-    /* apply the critic's increments once (slot order is irrelevant: integer sums) */
-    for (int64_t s = 0; s < V->cap; s++)
-        if (V->acc[s]) { V->vals[s] = V->vals[s] + (double)V->acc[s] * (1.0 / FX_ONE); V->acc[s] = 0; }
-    if (post_update) {
-        /* _get_td_errors with the updated V, then the actor (model/ffm_unified.py:559-598) */
-        for (int64_t e = 0; e < E; e++)
-            for (int i = 0; i < nstart[e]; i++) {
-                const lrec* q = recs + e * (int64_t)A_cap + i;
-                if (!q->valid) continue;
-                const double vn = q->snv >= 0 ? V->vals[q->snv] : 0.0;
-                const double td = (q->r + c->gamma * vn) - V->vals[q->sv];
-                Ht->acc[(int64_t)q->hslot * 5 + q->k] += fx(c->alpha_h * td);
-            }
-    }
-    if (actor)
-        for (int64_t s = 0; s < Ht->cap * 5; s++)
-            if (Ht->acc[s]) { Ht->vals[s] = Ht->vals[s] + (double)Ht->acc[s] * (1.0 / FX_ONE); Ht->acc[s] = 0; }
-    /* episode ends: emptied, or truncated at max_steps (run_*_training.py MAX_STEPS) */
-    for (int64_t e = 0; e < E; e++) {
+    if (agent_steps) *agent_steps = total;
+    return err ? -1 : 0;
+}
+
+/* which 0: apply V, then (ffm_unified actor_only) the actor's increments from the
+ * TD errors of the updated V (model/ffm_unified.py:559-598); which 1: apply H. */
+void ffo_lbatch_apply(ffo_lbatch* b, int which) {
+    const ffo_learn_cfg* c = b->c;
+    if (which == 1) { ffo_tab_apply(b->Ht); return; }
+    ffo_tab_apply(b->V);
+    if (!(c->variant == FFO_VAR_UNIFIED && c->mode == FFO_MODE_ACTOR)) return;
+    for (int64_t e = 0; e < b->E; e++)
+        for (int i = 0; i < b->nstart[e]; i++) {
+            const lrec* q = b->recs + e * (int64_t)b->A_cap + i;
+            if (!q->valid) continue;
+            const double vn = q->snv >= 0 ? b->V->vals[q->snv] : 0.0;
+            const double td = (q->r + c->gamma * vn) - b->V->vals[q->sv];
+            b->Ht->acc[(int64_t)q->hslot * 5 + q->k] += fx(c->alpha_h * td);
+        }
+}
+
+/* Episode ends: emptied, or truncated at max_steps (run_*_training.py MAX_STEPS). */
+void ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, int32_t* episodes,
+                    int32_t* ep_steps, uint64_t seed, uint32_t t, int32_t auto_reset, int32_t N_reset,
+                    int32_t max_steps, int64_t env_base) {
+    const ffo_learn_cfg* c = b->c;
+    const int HW = c->H * c->W;
+    ffo_core_cfg cc;
+    memset(&cc, 0, sizeof cc);
+    cc.H = c->H; cc.W = c->W; cc.map = c->map; cc.nb = 4;
+    for (int64_t e = 0; e < b->E; e++) {
         ep_steps[e]++;
         if (auto_reset && (counts[e] == 0 || (max_steps > 0 && ep_steps[e] >= max_steps))) {
-            ffo_reset_philox(&cc, N_reset, seed, t, env_base + e, pos + e * (int64_t)A_cap);
+            ffo_reset_philox(&cc, N_reset, seed, t, env_base + e, pos + e * (int64_t)b->A_cap);
             counts[e] = N_reset;
             memset(dff + e * (int64_t)HW, 0, sizeof(float) * (size_t)HW);
             ep_steps[e] = 0;
             if (episodes) episodes[e]++;
         }
     }
-    free(recs); free(nstart);
-    if (agent_steps) *agent_steps = total;
-    return err ? -1 : 0;
+}
+
+int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E,
+                                int32_t A_cap, uint16_t* pos, int32_t* counts, float* dff,
+                                int32_t* episodes, int32_t* ep_steps, uint64_t seed, uint32_t t,
+                                int32_t auto_reset, int32_t N_reset, int32_t max_steps,
+                                int64_t env_base, uint64_t* agent_steps, int nthreads) {
+    const int actor = c->variant == FFO_VAR_ACTOR_ONLY ||
+                      (c->variant == FFO_VAR_UNIFIED && c->mode != FFO_MODE_CRITIC);
+    ffo_lbatch* b = ffo_lbatch_new(c, V, Ht, E, A_cap);
+    const int rc = ffo_lbatch_local(b, pos, counts, dff, seed, t, env_base, agent_steps, nthreads);
+    ffo_lbatch_apply(b, 0);
+    if (actor) ffo_lbatch_apply(b, 1);
+    ffo_lbatch_end(b, pos, counts, dff, episodes, ep_steps, seed, t, auto_reset, N_reset, max_steps, env_base);
+    ffo_lbatch_free(b);
+    return rc;
 }

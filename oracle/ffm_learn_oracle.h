@@ -70,6 +70,25 @@ int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht,
                                 int32_t auto_reset, int32_t N_reset, int32_t max_steps,
                                 int64_t env_base, uint64_t* agent_steps, int nthreads);
 
+/* The batched step in phases, for multi-rank runs:
+ * local (every env against the current tables, increments pending) ->
+ * exchange (delta export / merge per table) -> apply V (+ the post-update
+ * actor increments of ffm_unified actor_only) -> exchange H -> apply H -> end
+ * (episode ends).  ffo_learn_step_philox_batch = local, apply 0, apply 1, end. */
+typedef struct ffo_lbatch ffo_lbatch;
+ffo_lbatch* ffo_lbatch_new(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E, int32_t A_cap);
+void ffo_lbatch_free(ffo_lbatch* b);
+int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, uint64_t seed, uint32_t t,
+                     int64_t env_base, uint64_t* agent_steps, int nthreads);
+void ffo_lbatch_apply(ffo_lbatch* b, int which);
+void ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, int32_t* episodes,
+                    int32_t* ep_steps, uint64_t seed, uint32_t t, int32_t auto_reset, int32_t N_reset,
+                    int32_t max_steps, int64_t env_base);
+void ffo_tab_mark(ffo_tab* t);
+int64_t ffo_tab_delta_export(const ffo_tab* t, uint64_t* keys, int64_t* acc);
+int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, int64_t n, const double* init);
+void ffo_tab_apply(ffo_tab* t);
+
 /* Deterministic float64 exp (fdlibm's algorithm, +,*,/ only): the f64
  * softmax of the actor modes on CPU and GPU alike. */
 double ffo_det_exp(double x);

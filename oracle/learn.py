@@ -68,6 +68,18 @@ def _lib():
             C.POINTER(LearnCfg), P, P, C.c_int64, C.c_int32, P, P, P, P, P, C.c_uint64, C.c_uint32,
             C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.POINTER(C.c_uint64), C.c_int]
         L.ffo_learn_step_philox_batch.restype = C.c_int
+        L.ffo_lbatch_new.argtypes = [C.POINTER(LearnCfg), P, P, C.c_int64, C.c_int32]
+        L.ffo_lbatch_new.restype = P
+        L.ffo_lbatch_free.argtypes = [P]
+        L.ffo_lbatch_local.argtypes = [P, P, P, P, C.c_uint64, C.c_uint32, C.c_int64, C.POINTER(C.c_uint64), C.c_int]
+        L.ffo_lbatch_local.restype = C.c_int
+        L.ffo_lbatch_apply.argtypes = [P, C.c_int]
+        L.ffo_lbatch_end.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_int64]
+        L.ffo_tab_delta_export.argtypes = [P, P, P]
+        L.ffo_tab_delta_export.restype = C.c_int64
+        L.ffo_tab_delta_merge.argtypes = [P, P, P, C.c_int64, P]
+        L.ffo_tab_delta_merge.restype = C.c_int
         L.ffo_det_exp.argtypes = [C.c_double]
         L.ffo_det_exp.restype = C.c_double
         L.ffo_encode_rank.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
@@ -161,6 +173,75 @@ class Learn:
         if rc:
             raise RuntimeError("oracle table full")
         return int(tot.value)
+
+
+class Shard:
+    """The batched step of envs [env_base, env_base + E) in phases, with the
+    Learner's phase interface (ffm_amd.dist.TableSync): the CPU side of the
+    multi-rank tests.  Record buffers are host pointers."""
+
+    def __init__(self, learn: Learn, E: int, A: int, N: int, seed: int, env_base: int, max_steps: int,
+                 nthreads: int = 1):
+        from . import oracle as O
+        self.L, self.E, self.A, self.N = learn, E, A, N
+        self.seed, self.env_base, self.max_steps, self.nthreads = seed, env_base, max_steps, nthreads
+        self.variant, self.mode = learn.variant, learn.mode
+        core = O.Core(learn.map, learn.sff32 if learn.sff32 is not None else learn.sff64, {"neighborhood": "neumann"})
+        self.pos = np.full((E, A), 0xFFFF, np.uint16)
+        for e in range(E):
+            self.pos[e, :N] = core.reset_philox(N, seed, 0, env_base + e)
+        self.counts = np.full(E, N, np.int32)
+        self.dff = np.zeros((E,) + learn.map.shape, np.float32)
+        self.episodes = np.zeros(E, np.int32)
+        self.ep_steps = np.zeros(E, np.int32)
+        self.t = 1
+        self.agent_steps = 0
+        self.b = _lib().ffo_lbatch_new(C.byref(learn.cfg), learn.V.h, learn.Ht.h, E, A)
+
+    def __del__(self):
+        if getattr(self, "b", None):
+            _lib().ffo_lbatch_free(self.b)
+            self.b = None
+
+    @property
+    def actor(self):
+        return self.variant == "actor_only" or (self.variant == "unified" and self.mode != "critic_only")
+
+    @property
+    def post_update(self):
+        return self.variant == "unified" and self.mode == "actor_only"
+
+    def _tab(self, which):
+        return self.L.V if which == "V" else self.L.Ht
+
+    def step_local(self):
+        tot = C.c_uint64(0)
+        if _lib().ffo_lbatch_local(self.b, O._ptr(self.pos), O._ptr(self.counts), O._ptr(self.dff), self.seed,
+                                   self.t, self.env_base, C.byref(tot), self.nthreads):
+            raise RuntimeError("oracle table full")
+        self.agent_steps += int(tot.value)
+
+    def step_apply(self, which):
+        _lib().ffo_lbatch_apply(self.b, 0 if which == "V" else 1)
+
+    def step_end(self):
+        _lib().ffo_lbatch_end(self.b, O._ptr(self.pos), O._ptr(self.counts), O._ptr(self.dff),
+                              O._ptr(self.episodes), O._ptr(self.ep_steps), self.seed, self.t, 1, self.N,
+                              self.max_steps, self.env_base)
+        self.t += 1
+
+    def delta_export(self, which, keys_ptr, acc_ptr, cap):
+        T = self._tab(which)
+        n = len(T)          # upper bound on the records
+        if n > cap:
+            return n
+        return int(_lib().ffo_tab_delta_export(T.h, keys_ptr, acc_ptr))
+
+    def delta_merge(self, which, keys_ptr, acc_ptr, n):
+        T = self._tab(which)
+        init = np.full(T.width, self.L.cfg.v_default if which == "V" else 0.0, np.float64)
+        if _lib().ffo_tab_delta_merge(T.h, keys_ptr, acc_ptr, int(n), O._ptr(init)):
+            raise RuntimeError("oracle table full")
 
 
 def det_exp(x: float) -> float:

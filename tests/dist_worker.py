@@ -78,3 +78,78 @@ def worker(rank, world, port, n_global, backend, out_path):
                      agent_steps=red["agent_steps"], steps=red["steps"])
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# Learning variants: shards share the V / H tables through TableSync
+# ---------------------------------------------------------------------------
+LEARN_STEPS, LEARN_N, LEARN_MAX = 50, 16, 30
+
+
+def learn_params(variant):
+    return {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+
+
+def learn_summary(shards_or_state):
+    pos, cnt, dff, eps, est, tabs = shards_or_state
+    mask = np.arange(pos.shape[1])[None, :] < cnt[:, None]
+    return dict(pos=np.where(mask, pos, 0xFFFF).astype(np.int32), cnt=cnt, dff=dff.reshape(len(cnt), -1).view(np.int32),
+                eps=eps, est=est, **tabs)
+
+
+def sorted_tables(learn):
+    out = {}
+    for which, T in (("V", learn.V), ("H", learn.Ht)):
+        k, v = T.export()
+        o = np.argsort(k)
+        out[f"{which}_keys"] = k[o]
+        out[f"{which}_vals"] = np.asarray(v)[o].view(np.uint64)
+    return out
+
+
+def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1):
+    """Single shard (or `coupled_shards` shards coupled in-process) of the batched
+    learning step on the CPU restatement."""
+    from oracle import learn as LO
+    from ffm_amd.dist import shard_range, step_coupled
+    m, s = room()
+    learns, shards = [], []
+    for r in range(coupled_shards):
+        b, c = shard_range(n, r, coupled_shards)
+        L = LO.Learn(m, s, variant, mode, learn_params(variant), log2_cap=20)
+        learns.append(L)
+        shards.append(LO.Shard(L, c, LEARN_N, LEARN_N, SEED, env_base + b, LEARN_MAX))
+    step_coupled(shards, LEARN_STEPS, device="cpu")
+    cat = lambda f: np.concatenate([f(x) for x in shards])
+    return (cat(lambda x: x.pos), cat(lambda x: x.counts), cat(lambda x: x.dff), cat(lambda x: x.episodes),
+            cat(lambda x: x.ep_steps), sorted_tables(learns[0])), [sorted_tables(L) for L in learns]
+
+
+def learn_worker(rank, world, port, n_global, variant, mode, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import learn as LO
+        from ffm_amd.dist import TableSync, shard_range
+        m, s = room()
+        base, n = shard_range(n_global, rank, world)
+        L = LO.Learn(m, s, variant, mode, learn_params(variant), log2_cap=20)
+        shard = LO.Shard(L, n, LEARN_N, LEARN_N, SEED, base, LEARN_MAX)
+        sync = TableSync(shard, device="cpu", capacity=64)      # small: exercises the regrow path
+        sync.step(LEARN_STEPS)
+        parts = {}
+        for name, a in (("pos", shard.pos), ("cnt", shard.counts), ("dff", shard.dff), ("eps", shard.episodes),
+                        ("est", shard.ep_steps)):
+            g = [None] * world
+            dist.all_gather_object(g, a)
+            parts[name] = np.concatenate(g)
+        tabs = [None] * world
+        dist.all_gather_object(tabs, sorted_tables(L))
+        if rank == 0:
+            summ = learn_summary((parts["pos"], parts["cnt"], parts["dff"], parts["eps"], parts["est"], tabs[0]))
+            for r in range(1, world):      # every rank ends with the same tables
+                for k, v in tabs[r].items():
+                    summ[f"r{r}_{k}"] = v
+            np.savez(out_path, **summ)
+    finally:
+        dist.destroy_process_group()

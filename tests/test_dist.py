@@ -72,3 +72,40 @@ def test_gloo_world2_sharded_engine_equals_oracle(tmp_path):
     assert np.array_equal(got["pos"], pos)
     assert np.array_equal(got["dff"], dff)
     assert int(got["agent_steps"]) == c["agent_steps"]
+
+
+LEARN_VARIANTS = [("ac", None), ("unified", "critic_only"), ("unified", "actor_only"), ("unified", "both"),
+                  ("actor_only", None)]
+
+
+@pytest.mark.parametrize("variant,mode", LEARN_VARIANTS)
+def test_coupled_learning_shards_equal_single_run(variant, mode):
+    """ffm_amd.dist.step_coupled: 3 shards exchanging table deltas == one batch of
+    all envs, bit for bit (states and V / H tables); every shard ends with the
+    same tables."""
+    n = 41
+    single, _ = W.run_learn_oracle(variant, mode, 0, n, coupled_shards=1)
+    coupled, per = W.run_learn_oracle(variant, mode, 0, n, coupled_shards=3)
+    a, b = W.learn_summary(single), W.learn_summary(coupled)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    for t in per[1:]:
+        for k in t:
+            assert np.array_equal(t[k], per[0][k]), k
+    assert a["eps"].sum() > 0 and len(a["V_keys"]) > 50
+
+
+@pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None), ("ac", None)])
+def test_gloo_world2_table_sync_equals_single_run(variant, mode, tmp_path):
+    """TableSync over a real world-2 gloo group (all_gather of variable-length
+    delta records) == a single-process batch of all envs."""
+    n = 37
+    out = str(tmp_path / "learn.npz")
+    mp.spawn(W.learn_worker, args=(2, _port(), n, variant, mode, out), nprocs=2, join=True)
+    got = dict(np.load(out))
+    single, _ = W.run_learn_oracle(variant, mode, 0, n)
+    want = W.learn_summary(single)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), k
+        if k.startswith(("V_", "H_")):
+            assert np.array_equal(got[f"r1_{k}"], want[k]), f"rank 1 {k}"

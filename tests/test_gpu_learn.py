@@ -284,3 +284,47 @@ def test_learner_unified_dense_table_rejects_foreign_keys():
     with pytest.raises(ValueError):
         L.import_table("H", [K.pack((1,) * 13, 0, 0)], np.zeros((1, 5)))
     L.close()
+
+
+@pytest.mark.parametrize("variant,mode", VARIANTS)
+def test_learner_coupled_shards_equal_one_learner(variant, mode):
+    """Multi-GPU contract on one device: three Learner shards (env_base offsets) stepped
+    through ffm_amd.dist.step_coupled (delta export -> merge of the others' records ->
+    apply) end every step with the tables of ONE learner holding all envs, bit for bit,
+    and the same env states."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.dist import shard_range, step_coupled
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    n, N, T = 3001, 32, 60
+    kw = dict(mode=mode, params=p, rng="philox", seed=21, auto_reset=True, max_steps=40)
+    one = _learner(m, s, variant, n_envs=n, n_agents=N, **kw)
+    one.reset()
+    one.step(T)
+    shards = []
+    for r in range(3):
+        b, c = shard_range(n, r, 3)
+        L = _learner(m, s, variant, n_envs=c, n_agents=N, env_base=b, **kw)
+        L.reset()
+        shards.append(L)
+    step_coupled(shards, T, device="cuda", capacity=1024)
+    op, oc, od = one.get_state()
+    sp = [L.get_state() for L in shards]
+    assert np.array_equal(oc, np.concatenate([x[1] for x in sp]))
+    assert np.array_equal(od.view(np.uint32), np.concatenate([x[2] for x in sp]).view(np.uint32))
+    pos = np.concatenate([x[0] for x in sp])
+    for e in range(0, n, 7):
+        assert np.array_equal(op[e, :oc[e]], pos[e, :oc[e]])
+    assert np.array_equal(one.episodes()[0], np.concatenate([L.episodes()[0] for L in shards]))
+    tabs = ["V"] + (["H"] if one.actor else [])
+    for which in tabs:
+        k0, v0 = one.export_table(which)
+        o0 = np.argsort(k0)
+        for L in shards:
+            k, v = L.export_table(which)
+            o = np.argsort(k)
+            assert np.array_equal(k[o], k0[o0]), which
+            assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), which
+    for L in shards + [one]:
+        L.close()
