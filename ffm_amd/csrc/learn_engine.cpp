@@ -165,6 +165,7 @@ static hipError_t clear_table(ffm_learner* l, DevTable& T, double dflt, hipStrea
     if ((e = hipMemsetAsync(T.t.vals, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.n, 0, 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(T.t.mark, 0, 4, s)) != hipSuccess) return e;
     if (T.width == 1 && dflt != 0.0) {
         ffm::LearnArgs a = make_args(l);
         a.v_default = dflt;
@@ -350,9 +351,9 @@ int ffm_learner_reset(ffm_learner* l, void* stream) {
 static int phase_local(ffm_learner* l, hipStream_t s) {
     // H statistics of the step-start table: produced by the previous step's H
     // apply, recomputed only after the table was replaced (create / import)
+    // (each table's mark -- its size at the step start -- is left by the previous
+    // step's apply, or by clear / import)
     if (l->actor && !l->hstat_valid) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
-    HIP_TRY(hipMemcpyAsync(l->V.t.mark, l->V.t.n, 4, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipMemcpyAsync(l->H.t.mark, l->H.t.n, 4, hipMemcpyDeviceToDevice, s));
     HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
     l->phase = 1;
     return FFM_OK;

@@ -80,7 +80,10 @@ __device__ __forceinline__ uint32_t dense_slot(unsigned long long key, uint32_t 
 __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflow) {
     uint32_t h = T.dense_by ? dense_slot(key, T.dense_by) : (uint32_t)mix64(key) & T.mask;
     for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
-        const unsigned long long k = __hip_atomic_load(&T.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // A plain load may see a slot empty that another CU has just filled; the CAS
+        // below then reports the key actually there.  Keys are never removed during
+        // a step, so a non-empty value read is never stale.
+        const unsigned long long k = T.keys[h];
         if (k == key) return (int)h;
         if (k == kEmptyKey) {
             // A hashed table past 7/8 load refuses new keys (probe chains would grow
@@ -913,10 +916,14 @@ __device__ __forceinline__ int env_scan_flag(bool f, int* ws, int& total) {
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// LDS of one env: occupancy grid, next-state bits, requests, scan words.  (Staging
+// the map, SFF and DFF in LDS as well measured slower at config 4, 324 vs 295 us:
+// they are L1/L2 hits, and the staging delays every short-lived workgroup.)
 struct BatchCarve {
-    size_t grid, bits, req, ws, total;
+    size_t grid, bits, req, ws, total;     // per env
+    size_t shared;                          // per block: EPB env regions
 };
-__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D) {
+__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB) {
     BatchCarve c;
     size_t o = 0;
     c.grid = o; o += align16((size_t)HW * 2);
@@ -924,6 +931,7 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D) {
     c.req = o; o += align16((size_t)A * D * 2);
     c.ws = o; o += 64;
     c.total = o;
+    c.shared = (size_t)EPB * o;
     return c;
 }
 
@@ -932,7 +940,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LPE = BS / EPB;
     const int H = a.H, W = a.W, HW = a.HW, A = a.A;
-    const BatchCarve cv = batch_carve(HW, A, D);
+    const BatchCarve cv = batch_carve(HW, A, D, EPB);
     const int sub = threadIdx.x / LPE, tid = threadIdx.x % LPE;
     unsigned char* base = smem + (size_t)sub * cv.total;
     uint16_t* grid = reinterpret_cast<uint16_t*>(base + cv.grid);
@@ -945,7 +953,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     const int n = live ? a.cnt[e] : 0;
     const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
     const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
-    const float* dff = a.dff_in + (live ? e : 0) * (long long)HW;
+    float* dff = a.dff_in + (live ? e : 0) * (long long)HW;
 
     for (int c = tid; c < HW; c += LPE) grid[c] = kNone16;
     for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
@@ -1102,7 +1110,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         const int i = tid + j * LPE;
         if (i >= n) continue;
         if (wins[j]) {
-            float* c = a.dff_in + e * (long long)HW + p[j];
+            float* c = dff + p[j];
             float v = *c;
             for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
             *c = v;
@@ -1261,6 +1269,8 @@ __global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a) {
 template <int WIDTH, bool STATS>
 __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* hpart) {
     const uint32_t n = *T.n;
+    // the next step's delta export reports entries inserted after this point
+    if (blockIdx.x == 0 && threadIdx.x == 0) *T.mark = n;
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
@@ -1412,6 +1422,50 @@ __global__ __launch_bounds__(256) void learn_delta_merge_kernel(LearnTable T, co
     }
 }
 
+// Philox placement for maps with F <= 256 free cells: one wave per 64 envs scans
+// their done flags and re-places those envs one after another (every lane
+// ranks F/64 keys against all F in LDS), instead of one workgroup per env.
+constexpr int kResetSmallF = 256;
+
+__global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int all) {
+    __shared__ unsigned long long keys[kResetSmallF];
+    const int lane = threadIdx.x;
+    const long long e0 = (long long)blockIdx.x * 64;
+    const long long me = e0 + lane;
+    const bool want = me < a.E && (all || a.done[me]);
+    unsigned long long m = __ballot(want);
+    const int F = a.F, N = a.N, HW = a.HW;
+    while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const long long e = e0 + b;
+        const uint32_t genv = (uint32_t)(a.env_base + e);
+        for (int j = lane; j < F; j += 64) {
+            const uint32_t k = philox(make_uint4(a.t, genv, (uint32_t)j, kPurReset << 28), a.key0, a.key1).x;
+            keys[j] = ((unsigned long long)k << 32) | (unsigned)j;
+        }
+        __syncthreads();
+        for (int j = lane; j < F; j += 64) {
+            const unsigned long long kj = keys[j];
+            int rank = 0;
+            for (int i = 0; i < F; i++) rank += keys[i] < kj ? 1 : 0;
+            if (rank < N) a.pos[e * a.A + rank] = a.free_cells[j];
+        }
+        float* d = a.dff_in + e * (long long)HW;
+        for (int c = lane; c < HW; c += 64) d[c] = 0.0f;
+        if (lane == 0) {
+            a.cnt[e] = N;
+            a.ep_steps[e] = 0;
+            a.done[e] = 0;
+            if (!all) {
+                a.episodes[e] += 1;
+                a.counters[4 * e + 2] += 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // Insert keys in the given order (one lane: the insertion order is the dict
 // order the reference's get_v_table / get_h_table return) and set their values.
 __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int width, const unsigned long long* keys,
@@ -1419,14 +1473,15 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
     if (threadIdx.x != 0) return;
     for (long long i = 0; i < n; i++) {
         const int s = tab_get(T, keys[i], overflow);
-        if (s < 0) return;
+        if (s < 0) break;
         for (int k = 0; k < width; k++) T.vals[(size_t)s * width + k] = vals[i * width + k];
     }
+    *T.mark = *T.n;
 }
 
 template <int BS, int EPB, int APT, int D>
 hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
-    const size_t smem = batch_carve(a.HW, a.A, D).total * EPB;
+    const size_t smem = batch_carve(a.HW, a.A, D, EPB).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D>),
@@ -1441,7 +1496,7 @@ hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
 template <int D>
 hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
     const int A = a.A;
-    if (A <= 32 && 2 * batch_carve(a.HW, A, D).total <= 64 * 1024) return launch_batch_t<64, 2, 1, D>(a, s);
+    if (A <= 32 && batch_carve(a.HW, A, D, 2).shared <= 64 * 1024) return launch_batch_t<64, 2, 1, D>(a, s);
     if (A <= 64) return launch_batch_t<64, 1, 1, D>(a, s);
     if (A <= 256) return launch_batch_t<256, 1, 1, D>(a, s);
     if (A <= 1024) return launch_batch_t<1024, 1, 1, D>(a, s);
@@ -1457,7 +1512,7 @@ size_t learn_exact_scratch_bytes(int HW, int A) { return exact_carve(nullptr, HW
 
 int learn_batch_block_size(int A) { return A <= 64 ? 64 : A <= 256 ? 256 : 1024; }
 
-size_t learn_batch_smem_bytes(int HW, int A, int D) { return batch_carve(HW, A, D).total; }
+size_t learn_batch_smem_bytes(int HW, int A, int D) { return batch_carve(HW, A, D, 1).shared; }
 
 bool learn_batch_supported(int HW, int A, int D) {
     return A <= 16384 && learn_batch_smem_bytes(HW, A, D) <= 160 * 1024;
@@ -1494,6 +1549,10 @@ hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
+    if (a.F <= kResetSmallF && a.N <= a.F) {
+        learn_reset_small_kernel<<<dim3((unsigned)((a.E + 63) / 64)), dim3(64), 0, s>>>(a, all ? 1 : 0);
+        return hipGetLastError();
+    }
     int P = 1;
     while (P < (a.F < kResetCap ? a.F : kResetCap)) P <<= 1;
     const size_t smem = (size_t)P * 8;
