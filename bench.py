@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=0, help="0 = size the sample to ~15 s")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--log2-table", type=int, default=0, help="learner V/H hash capacity (0 = engine default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_config2.json"))
     a = ap.parse_args()
     size, agents, envs, steps, warmup = {2: (12, 32, 65536, 500, 50), 3: (64, 512, 8192, 200, 20),
@@ -225,7 +226,8 @@ def bench_learner(args, world, rank, torch, dist):
     s = l1_sff(m)
     L = Learner(m, s, cfg["variant"], n_envs=E, n_agents=A, mode=cfg["mode"], params=cfg["params"],
                 rng="philox", seed=args.seed, auto_reset=True, max_steps=cfg["max_steps"], env_base=rank * E,
-                device=torch.cuda.current_device())
+                device=torch.cuda.current_device(), log2_v_capacity=args.log2_table,
+                log2_h_capacity=args.log2_table)
     stream = torch.cuda.current_stream()
     L.reset(stream)
     if world > 1:

@@ -46,6 +46,7 @@ struct ffm_learner {
     ffm_engine_desc d{};
     ffm_learn_desc L{};
     bool mt = false, f64 = false, actor = false, post_update = false;
+    bool trained = false;              // ffm_trained_core: H read only, no learning
     int HW = 0, F = 0, D = 1;
     float smin = 0, smax = 0;
     uint32_t t = 0;
@@ -181,8 +182,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     *out = nullptr;
     const ffm_engine_desc& d = *desc;
     if (d.abi_version != FFM_ABI_VERSION) return fail(FFM_E_INVALID, "abi_version mismatch");
-    if (d.variant != FFM_VARIANT_AC && d.variant != FFM_VARIANT_UNIFIED && d.variant != FFM_VARIANT_ACTOR_ONLY)
-        return fail(FFM_E_INVALID, "learner variant must be AC, UNIFIED or ACTOR_ONLY");
+    if (d.variant != FFM_VARIANT_AC && d.variant != FFM_VARIANT_UNIFIED && d.variant != FFM_VARIANT_ACTOR_ONLY &&
+        d.variant != FFM_VARIANT_TRAINED)
+        return fail(FFM_E_INVALID, "learner variant must be AC, UNIFIED, ACTOR_ONLY or TRAINED");
     if (d.variant == FFM_VARIANT_UNIFIED && (learn->mode < 0 || learn->mode > 2))
         return fail(FFM_E_INVALID, "learning_mode must be one of ['critic_only', 'actor_only', 'both']");
     // Cells are u16 indices and 0xFFFF marks "none": up to 256 x 256 cells, the
@@ -232,6 +234,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     l->D = d.variant == FFM_VARIANT_ACTOR_ONLY ? 4 : 1;
     l->actor = d.variant == FFM_VARIANT_ACTOR_ONLY || (d.variant == FFM_VARIANT_UNIFIED && learn->mode != FFM_LEARN_CRITIC_ONLY);
     l->post_update = d.variant == FFM_VARIANT_UNIFIED && learn->mode == FFM_LEARN_ACTOR_ONLY;
+    l->trained = d.variant == FFM_VARIANT_TRAINED;
     if (!l->mt && !ffm::learn_batch_supported(HW, d.agent_capacity, l->D)) {
         release(l);
         return fail(FFM_E_UNSUPPORTED, "env does not fit the batched learner's LDS budget");
@@ -284,10 +287,11 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         ALLOC(l->d_scratch, ffm::learn_exact_scratch_bytes(HW, (int)A));
     }
 #undef ALLOC
-    // ffm_unified: dense tables over 256 rank codes x Bx x By blocks (at most 2^28 slots).
+    // ffm_unified / ffm_trained_core: dense tables over 256 rank codes x Bx x By blocks
+    // (at most 2^28 slots).
     uint32_t dense_by = 0;
     size_t dense_n = 0;
-    if (d.variant == FFM_VARIANT_UNIFIED) {
+    if (d.variant == FFM_VARIANT_UNIFIED || d.variant == FFM_VARIANT_TRAINED) {
         const size_t bs = (size_t)learn->block_size;
         const size_t bx = (size_t)(H - 1) / bs + 1, by = (size_t)(W - 1) / bs + 1;
         if (256 * bx * by <= ((size_t)1 << 28)) {
@@ -297,7 +301,8 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     }
     l->dense_bx = dense_by ? (uint32_t)((H - 1) / learn->block_size + 1) : 0;
     if ((he = alloc_table(l->V, l->L.log2_v_capacity, 1, dense_by, dense_n)) != hipSuccess ||
-        (he = alloc_table(l->H, l->actor ? l->L.log2_h_capacity : 8, 5, l->actor ? dense_by : 0, dense_n)) != hipSuccess)
+        (he = alloc_table(l->H, l->actor || l->trained ? l->L.log2_h_capacity : 8, 5,
+                          l->actor || l->trained ? dense_by : 0, dense_n)) != hipSuccess)
         return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(l->d_sff, d.sff, (size_t)HW * (l->f64 ? 8 : 4), hipMemcpyHostToDevice);
@@ -353,7 +358,10 @@ static int phase_local(ffm_learner* l, hipStream_t s) {
     // apply, recomputed only after the table was replaced (create / import)
     // (each table's mark -- its size at the step start -- is left by the previous
     // step's apply, or by clear / import)
-    if (l->actor && !l->hstat_valid) HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
+    if ((l->actor || l->trained) && !l->hstat_valid) {
+        HIP_TRY(ffm::launch_learn_hstat(make_args(l), s));
+        l->hstat_valid = true;
+    }
     HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
     l->phase = 1;
     return FFM_OK;
@@ -361,7 +369,7 @@ static int phase_local(ffm_learner* l, hipStream_t s) {
 
 static int phase_apply(ffm_learner* l, int32_t which, hipStream_t s) {
     if (which == FFM_TABLE_V) {
-        HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
+        if (!l->trained) HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
         if (l->post_update) HIP_TRY(ffm::launch_learn_post(make_args(l), s));
         l->phase = 2;
         return FFM_OK;
@@ -581,7 +589,7 @@ int ffm_learner_set_v_default(ffm_learner* l, double v_default, void* stream) {
 
 static DevTable* pick(ffm_learner* l, int32_t which) {
     if (which == FFM_TABLE_V) return &l->V;
-    if (which == FFM_TABLE_H && l->actor) return &l->H;
+    if (which == FFM_TABLE_H && (l->actor || l->trained)) return &l->H;
     return nullptr;
 }
 

@@ -8,7 +8,7 @@
 
 namespace ffm {
 
-enum : int { kVarAC = 1, kVarUnified = 2, kVarActorOnly = 3 };
+enum : int { kVarAC = 1, kVarUnified = 2, kVarActorOnly = 3, kVarTrained = 4 };
 enum : int { kModeCritic = 0, kModeActor = 1, kModeBoth = 2 };
 
 // Per-agent record kept between the step kernel and the post-update actor

@@ -103,6 +103,18 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
     return -1;
 }
 
+// Slot of `key`, or -1 when absent (read-only tables: ffm_trained_core).
+__device__ int tab_find(const LearnTable& T, unsigned long long key) {
+    uint32_t h = T.dense_by ? dense_slot(key, T.dense_by) : (uint32_t)mix64(key) & T.mask;
+    for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
+        const unsigned long long k = T.keys[h];
+        if (k == key) return (int)h;
+        if (k == kEmptyKey) return -1;
+        h = (h + 1) & T.mask;
+    }
+    return -1;
+}
+
 // ---- state maps and encoders ------------------------------------------------
 struct SmArray {                 // exact kernel: explicit state map
     const uint8_t* sm;
@@ -188,7 +200,7 @@ __device__ unsigned long long enc13(const SM& sm, int H, int W, int x, int y, in
 
 template <class SM>
 __device__ unsigned long long encode(const LearnArgs& a, const SM& sm, int x, int y) {
-    if (a.variant == kVarUnified) return enc_rank(sm, a.H, a.W, x, y, a.bs);
+    if (a.variant == kVarUnified || a.variant == kVarTrained) return enc_rank(sm, a.H, a.W, x, y, a.bs);
     if (a.variant == kVarAC) return enc13(sm, a.H, a.W, x, y, a.bs, 2);
     return enc13(sm, a.H, a.W, x, y, 5, 0);                    // block 5 hard-coded, :143
 }
@@ -471,217 +483,6 @@ __device__ void h_stats_seq(const LearnArgs& a, HStat& hs) {
     }
 }
 
-struct ExactScratch {
-    int *occ, *rq_tgt, *rq_agent, *list, *nxt, *coll, *act, *avalid, *wexit;
-    uint8_t *sm, *smn, *done;
-    float* B;
-    unsigned long long* skey;
-    double* td;
-};
-
-__host__ __device__ inline size_t exact_carve(unsigned char* base, int HW, int A, ExactScratch* s) {
-    size_t o = 0;
-    auto take = [&](size_t bytes) {
-        unsigned char* p = base ? base + o : nullptr;
-        o += (bytes + 15) & ~(size_t)15;
-        return p;
-    };
-    const size_t R = (size_t)A * 4 + 1;
-    ExactScratch t;
-    t.occ = (int*)take((size_t)HW * 4);
-    t.rq_tgt = (int*)take(R * 4);
-    t.rq_agent = (int*)take(R * 4);
-    t.list = (int*)take(R * 4);
-    t.nxt = (int*)take((size_t)A * 4 + 4);
-    t.coll = (int*)take((size_t)A * 4 + 4);
-    t.act = (int*)take((size_t)A * 4 + 4);
-    t.avalid = (int*)take((size_t)A * 4 + 4);
-    t.wexit = (int*)take((size_t)A * 4 + 4);
-    t.sm = (uint8_t*)take((size_t)HW);
-    t.smn = (uint8_t*)take((size_t)HW);
-    t.done = (uint8_t*)take(R);
-    t.B = (float*)take((size_t)HW * 4);
-    t.skey = (unsigned long long*)take((size_t)A * 8 + 8);
-    t.td = (double*)take((size_t)A * 8 + 8);
-    if (s) *s = t;
-    return o;
-}
-
-// ===========================================================================
-// Reference-exact step (one lane, envs in order, MT streams).  Restates
-// model/ffm_ac_core.py:111-236, model/ffm_unified.py:271-606 and
-// model/ffm_actor_only.py:149-409 statement by statement.
-// ===========================================================================
-__global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
-    if (threadIdx.x != 0) return;
-    ExactScratch S;
-    exact_carve(a.scratch, a.HW, a.A, &S);
-    const int W = a.W, HW = a.HW, A = a.A;
-    const int D = a.D;
-    const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
-    const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
-    for (int i = 0; i < HW; i++) S.occ[i] = -1;
-    for (long long e = 0; e < a.E; e++) {
-        uint16_t* pe = a.pos + e * A;
-        float* dff = a.dff_in + e * (long long)HW;
-        DrawMT rng{a.mt_np + e * 625, a.mt_py + e * 625};
-        const int n = a.cnt[e];
-        HStat hs{};
-        if (actor) h_stats_seq(a, hs);
-        for (int c = 0; c < HW; c++) S.sm[c] = a.map[c];
-        for (int i = 0; i < n; i++) { S.sm[pe[i]] = 1; S.occ[pe[i]] = i; }
-        auto occ = [&](int c) { return S.occ[c] >= 0; };
-        int nrq = 0;
-        // ---- decide -------------------------------------------------------
-        for (int i = 0; i < n; i++) {
-            const int x = pe[i] / W, y = pe[i] % W;
-            S.skey[i] = encode(a, SmArray{S.sm}, x, y);
-            S.nxt[i] = pe[i];
-            S.coll[i] = -1; S.act[i] = -1; S.avalid[i] = 0; S.wexit[i] = 0;
-            if (a.variant == kVarAC) {
-                const int T = ac_decide(a, x, y, occ, dff, S.wexit[i], rng);
-                if (T >= 0) { S.rq_tgt[nrq] = T; S.rq_agent[nrq++] = i; }
-                continue;
-            }
-            int coord[5], valid[5], inb[5];
-            moves5(a, x, y, occ, coord, valid, inb);
-            if (a.variant == kVarUnified) {
-                int ex = -1;
-                for (int k = 0; k < 4; k++)
-                    if (inb[k] && a.map[coord[k]] == 3) { ex = k; break; }
-                int k;
-                if (ex >= 0) {
-                    S.wexit[i] = 1;
-                    k = ex;
-                } else if (!actor) {
-                    k = critic_choose(a, coord, valid, dff, rng);
-                } else {
-                    const uint32_t before = *a.Ht.n;
-                    const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
-                    if (hsl < 0) return;
-                    if (*a.Ht.n > before) {                   // a zero row joins min/max (:414-423)
-                        hs.has = 1;
-                        hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
-                        hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
-                    }
-                    k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, false, rng);
-                }
-                S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
-                S.act[i] = k; S.avalid[i] = valid[k];
-            } else {
-                // ffm_actor_only: exit test and decision inside the neighbour loop (:214-355)
-                int ex = -1;
-                for (int j = 0; j < 4; j++) {
-                    if (ex < 0 && inb[j] && a.map[coord[j]] == 3) ex = j;
-                    int k;
-                    if (ex >= 0) {
-                        S.wexit[i] = 1;
-                        k = ex;
-                    } else {
-                        const uint32_t before = *a.Ht.n;
-                        const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
-                        if (hsl < 0) return;
-                        if (*a.Ht.n > before) {
-                            hs.has = 1;
-                            hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
-                            hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
-                        }
-                        k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, true, rng);
-                    }
-                    S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
-                    S.act[i] = k; S.avalid[i] = valid[k];
-                }
-            }
-        }
-        // ---- resolve: dict order, always a winner (random.choice) ---------
-        for (int q = 0; q < nrq; q++) S.done[q] = 0;
-        for (int q = 0; q < nrq; q++) {
-            if (S.done[q]) continue;
-            const int T = S.rq_tgt[q];
-            int m = 0;
-            for (int q2 = q; q2 < nrq; q2++)
-                if (S.rq_tgt[q2] == T) { S.list[m++] = S.rq_agent[q2]; S.done[q2] = 1; }
-            int w;
-            if (m == 1) {
-                w = S.list[0];
-                S.coll[w] = 0;
-            } else {
-                w = S.list[mt_randbelow(rng.py, (uint32_t)m)];
-                for (int z = 0; z < m; z++) S.coll[S.list[z]] = m - 1;
-            }
-            S.nxt[w] = T;
-            dff[pe[w]] += 1.0f;
-        }
-        // ---- learning --------------------------------------------------------
-        for (int c = 0; c < HW; c++) S.smn[c] = a.map[c];
-        for (int i = 0; i < n; i++)
-            if (a.map[S.nxt[i]] != 3) S.smn[S.nxt[i]] = 1;
-        for (int i = 0; i < n; i++) {
-            double r = a.step_penalty;
-            if (S.wexit[i]) r = r + a.exit_reward;
-            if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
-            double vn = 0.0;
-            if (!S.wexit[i]) {
-                const int sn = tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow);
-                if (sn < 0) return;
-                vn = a.V.vals[sn];
-            }
-            const int sv = tab_get(a.V, S.skey[i], a.overflow);
-            if (sv < 0) return;
-            const double v = a.V.vals[sv];
-            const double td = (r + a.gamma * vn) - v;
-            S.td[i] = td;
-            a.V.vals[sv] = v + a.alpha_v * td;
-        }
-        if (post_update) {        // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
-            for (int i = 0; i < n; i++) {
-                double r = a.step_penalty;
-                if (S.wexit[i]) r = r + a.exit_reward;
-                if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
-                double vn = 0.0;
-                if (!S.wexit[i])
-                    vn = a.V.vals[tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow)];
-                const double v = a.V.vals[tab_get(a.V, S.skey[i], a.overflow)];
-                S.td[i] = (r + a.gamma * vn) - v;
-            }
-        }
-        if (actor) {
-            for (int i = 0; i < n; i++) {
-                if (S.act[i] < 0) continue;
-                const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);    // :769-773
-                if (hsl < 0) return;
-                if (!S.avalid[i]) continue;
-                double* hv = a.Ht.vals + (size_t)hsl * 5 + S.act[i];
-                *hv = *hv + a.alpha_h * S.td[i];
-            }
-        }
-        // ---- exit removal, DFF -------------------------------------------------
-        for (int i = 0; i < n; i++) S.occ[pe[i]] = -1;
-        int nn = 0;
-        for (int i = 0; i < n; i++)
-            if (a.map[S.nxt[i]] != 3) pe[nn++] = (uint16_t)S.nxt[i];
-        a.cnt[e] = nn;
-        update_dff_seq(a, dff, S.B);
-        unsigned long long* slot = a.counters + 4 * e;
-        slot[0] += (unsigned long long)n;
-        slot[1] += (unsigned long long)(n - nn);
-        slot[3] += 1;
-        (void)D;
-    }
-}
-
-// Diagnostic builds only (tools/learn_ablate.sh): FFM_LABLATE bits drop parts of the
-// batched step to time them.  1: table increments, 2: learning phase,
-// 4: policy (agents stay; no H lookup), 8: DFF stencil.
-#ifndef FFM_LABLATE
-#define FFM_LABLATE 0
-#endif
-
-// ===========================================================================
-// Batched step: EPB envs per workgroup, LPE = BS / EPB lanes per env, APT
-// agents per lane.  Small rooms (A <= 32) pack two envs onto one wavefront.
-// ===========================================================================
-
 // A decision's policy, computed once per agent: the normalised cdf of
 // np.random.choice (cdf / cdf[-1], model/ffm_unified.py:497) over the five
 // moves (U, D, L, R, stay; invalid moves carry zero mass) and the valid-move
@@ -885,6 +686,288 @@ __device__ __forceinline__ void ac_policy(const LearnArgs& a, const int* coord, 
     finish_cdf(P, p);
 }
 
+// ffm_trained_core policy (model/ffm_trained_core.py:219-300): the trained H row
+// (float32; zeros when the state is missing), the whole-table min/max
+// normalisation in float32 (Python floats are weak scalars next to the f32
+// array), score -k_A*h + k_D*dff in float32, NumPy's float32 exp, masked sum and
+// divide, uniform fallbacks.  Same arithmetic as the oracle's trained_choose.
+__device__ __forceinline__ void trained_policy(const LearnArgs& a, int hslot, const int* coord, const int* valid,
+                                               const float* dff, const HStat& hs, Policy& P) {
+    float h[5], score[5], e[5];
+    double p[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) h[k] = hslot >= 0 ? (float)a.Ht.vals[(size_t)hslot * 5 + k] : 0.0f;
+    if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
+        const float hmax = (float)hs.mx, den = (float)(hs.mx - hs.mn);
+        const float srange = (float)((double)a.smax - (double)a.smin), smin = a.smin;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const float q = (hmax - h[k]) / den;
+            const float d = q * srange;
+            h[k] = d + smin;
+        }
+    }
+    const float nkA = (float)a.nkA;
+    bool bad = false;
+    int vm = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const float x = nkA * h[k];
+        const float y = a.kD32 * dff[coord[k]];
+        score[k] = x + y;
+        bad = bad || !__builtin_isfinite(score[k]);
+        vm |= valid[k] << k;
+    }
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if (bad) score[k] = valid[k] ? 1.0f : 0.0f;
+        mx = score[k] > mx ? score[k] : mx;
+    }
+    float sum = -0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const float x = np_expf(score[k] - mx);
+        e[k] = valid[k] ? x : 0.0f;
+        sum += e[k];
+    }
+    const bool ok = __builtin_isfinite(sum) && sum > 0;
+    const float u = (float)(1.0 / (double)__builtin_popcount(vm));
+#pragma unroll
+    for (int k = 0; k < 5; k++) p[k] = ok ? (double)(e[k] / sum) : (valid[k] ? (double)u : 0.0);
+    P.vmask = vm;
+    P.none = 0;
+    finish_cdf(P, p);
+}
+
+struct ExactScratch {
+    int *occ, *rq_tgt, *rq_agent, *list, *nxt, *coll, *act, *avalid, *wexit;
+    uint8_t *sm, *smn, *done;
+    float* B;
+    unsigned long long* skey;
+    double* td;
+};
+
+__host__ __device__ inline size_t exact_carve(unsigned char* base, int HW, int A, ExactScratch* s) {
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        unsigned char* p = base ? base + o : nullptr;
+        o += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    const size_t R = (size_t)A * 4 + 1;
+    ExactScratch t;
+    t.occ = (int*)take((size_t)HW * 4);
+    t.rq_tgt = (int*)take(R * 4);
+    t.rq_agent = (int*)take(R * 4);
+    t.list = (int*)take(R * 4);
+    t.nxt = (int*)take((size_t)A * 4 + 4);
+    t.coll = (int*)take((size_t)A * 4 + 4);
+    t.act = (int*)take((size_t)A * 4 + 4);
+    t.avalid = (int*)take((size_t)A * 4 + 4);
+    t.wexit = (int*)take((size_t)A * 4 + 4);
+    t.sm = (uint8_t*)take((size_t)HW);
+    t.smn = (uint8_t*)take((size_t)HW);
+    t.done = (uint8_t*)take(R);
+    t.B = (float*)take((size_t)HW * 4);
+    t.skey = (unsigned long long*)take((size_t)A * 8 + 8);
+    t.td = (double*)take((size_t)A * 8 + 8);
+    if (s) *s = t;
+    return o;
+}
+
+// ===========================================================================
+// Reference-exact step (one lane, envs in order, MT streams).  Restates
+// model/ffm_ac_core.py:111-236, model/ffm_unified.py:271-606 and
+// model/ffm_actor_only.py:149-409 statement by statement.
+// ===========================================================================
+__global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
+    if (threadIdx.x != 0) return;
+    ExactScratch S;
+    exact_carve(a.scratch, a.HW, a.A, &S);
+    const int W = a.W, HW = a.HW, A = a.A;
+    const int D = a.D;
+    const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
+    const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
+    const bool trained = a.variant == kVarTrained;
+    for (int i = 0; i < HW; i++) S.occ[i] = -1;
+    for (long long e = 0; e < a.E; e++) {
+        uint16_t* pe = a.pos + e * A;
+        float* dff = a.dff_in + e * (long long)HW;
+        DrawMT rng{a.mt_np + e * 625, a.mt_py + e * 625};
+        const int n = a.cnt[e];
+        HStat hs{};
+        if (actor || trained) h_stats_seq(a, hs);
+        for (int c = 0; c < HW; c++) S.sm[c] = a.map[c];
+        for (int i = 0; i < n; i++) { S.sm[pe[i]] = 1; S.occ[pe[i]] = i; }
+        auto occ = [&](int c) { return S.occ[c] >= 0; };
+        int nrq = 0;
+        // ---- decide -------------------------------------------------------
+        for (int i = 0; i < n; i++) {
+            const int x = pe[i] / W, y = pe[i] % W;
+            S.skey[i] = encode(a, SmArray{S.sm}, x, y);
+            S.nxt[i] = pe[i];
+            S.coll[i] = -1; S.act[i] = -1; S.avalid[i] = 0; S.wexit[i] = 0;
+            if (a.variant == kVarAC) {
+                const int T = ac_decide(a, x, y, occ, dff, S.wexit[i], rng);
+                if (T >= 0) { S.rq_tgt[nrq] = T; S.rq_agent[nrq++] = i; }
+                continue;
+            }
+            int coord[5], valid[5], inb[5];
+            moves5(a, x, y, occ, coord, valid, inb);
+            if (trained) {                                    // model/ffm_trained_core.py:169-258
+                int k = -1;
+                for (int j = 0; j < 4; j++)
+                    if (inb[j] && a.map[coord[j]] == 3) { k = j; break; }
+                if (k < 0) {
+                    Policy P;
+                    trained_policy(a, tab_find(a.Ht, S.skey[i]), coord, valid, dff, hs, P);
+                    const double u = rng.u();
+                    k = 4;
+                    for (int j = 3; j >= 0; j--) k = P.cn[j] > u ? j : k;
+                }
+                S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
+                continue;
+            }
+            if (a.variant == kVarUnified) {
+                int ex = -1;
+                for (int k = 0; k < 4; k++)
+                    if (inb[k] && a.map[coord[k]] == 3) { ex = k; break; }
+                int k;
+                if (ex >= 0) {
+                    S.wexit[i] = 1;
+                    k = ex;
+                } else if (!actor) {
+                    k = critic_choose(a, coord, valid, dff, rng);
+                } else {
+                    const uint32_t before = *a.Ht.n;
+                    const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
+                    if (hsl < 0) return;
+                    if (*a.Ht.n > before) {                   // a zero row joins min/max (:414-423)
+                        hs.has = 1;
+                        hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
+                        hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
+                    }
+                    k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, false, rng);
+                }
+                S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
+                S.act[i] = k; S.avalid[i] = valid[k];
+            } else {
+                // ffm_actor_only: exit test and decision inside the neighbour loop (:214-355)
+                int ex = -1;
+                for (int j = 0; j < 4; j++) {
+                    if (ex < 0 && inb[j] && a.map[coord[j]] == 3) ex = j;
+                    int k;
+                    if (ex >= 0) {
+                        S.wexit[i] = 1;
+                        k = ex;
+                    } else {
+                        const uint32_t before = *a.Ht.n;
+                        const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
+                        if (hsl < 0) return;
+                        if (*a.Ht.n > before) {
+                            hs.has = 1;
+                            hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
+                            hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
+                        }
+                        k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, true, rng);
+                    }
+                    S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
+                    S.act[i] = k; S.avalid[i] = valid[k];
+                }
+            }
+        }
+        // ---- resolve: dict order, always a winner (random.choice) ---------
+        for (int q = 0; q < nrq; q++) S.done[q] = 0;
+        for (int q = 0; q < nrq; q++) {
+            if (S.done[q]) continue;
+            const int T = S.rq_tgt[q];
+            int m = 0;
+            for (int q2 = q; q2 < nrq; q2++)
+                if (S.rq_tgt[q2] == T) { S.list[m++] = S.rq_agent[q2]; S.done[q2] = 1; }
+            int w;
+            if (m == 1) {
+                w = S.list[0];
+                S.coll[w] = 0;
+            } else {
+                w = S.list[mt_randbelow(rng.py, (uint32_t)m)];
+                for (int z = 0; z < m; z++) S.coll[S.list[z]] = m - 1;
+            }
+            S.nxt[w] = T;
+            dff[pe[w]] += 1.0f;
+        }
+        // ---- learning (none for the trained actor) ----------------------------
+        if (trained) goto exits;
+        for (int c = 0; c < HW; c++) S.smn[c] = a.map[c];
+        for (int i = 0; i < n; i++)
+            if (a.map[S.nxt[i]] != 3) S.smn[S.nxt[i]] = 1;
+        for (int i = 0; i < n; i++) {
+            double r = a.step_penalty;
+            if (S.wexit[i]) r = r + a.exit_reward;
+            if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
+            double vn = 0.0;
+            if (!S.wexit[i]) {
+                const int sn = tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow);
+                if (sn < 0) return;
+                vn = a.V.vals[sn];
+            }
+            const int sv = tab_get(a.V, S.skey[i], a.overflow);
+            if (sv < 0) return;
+            const double v = a.V.vals[sv];
+            const double td = (r + a.gamma * vn) - v;
+            S.td[i] = td;
+            a.V.vals[sv] = v + a.alpha_v * td;
+        }
+        if (post_update) {        // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
+            for (int i = 0; i < n; i++) {
+                double r = a.step_penalty;
+                if (S.wexit[i]) r = r + a.exit_reward;
+                if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
+                double vn = 0.0;
+                if (!S.wexit[i])
+                    vn = a.V.vals[tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow)];
+                const double v = a.V.vals[tab_get(a.V, S.skey[i], a.overflow)];
+                S.td[i] = (r + a.gamma * vn) - v;
+            }
+        }
+        if (actor) {
+            for (int i = 0; i < n; i++) {
+                if (S.act[i] < 0) continue;
+                const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);    // :769-773
+                if (hsl < 0) return;
+                if (!S.avalid[i]) continue;
+                double* hv = a.Ht.vals + (size_t)hsl * 5 + S.act[i];
+                *hv = *hv + a.alpha_h * S.td[i];
+            }
+        }
+        // ---- exit removal, DFF -------------------------------------------------
+    exits:
+        for (int i = 0; i < n; i++) S.occ[pe[i]] = -1;
+        int nn = 0;
+        for (int i = 0; i < n; i++)
+            if (a.map[S.nxt[i]] != 3) pe[nn++] = (uint16_t)S.nxt[i];
+        a.cnt[e] = nn;
+        update_dff_seq(a, dff, S.B);
+        unsigned long long* slot = a.counters + 4 * e;
+        slot[0] += (unsigned long long)n;
+        slot[1] += (unsigned long long)(n - nn);
+        slot[3] += 1;
+        (void)D;
+    }
+}
+
+// Diagnostic builds only (tools/learn_ablate.sh): FFM_LABLATE bits drop parts of the
+// batched step to time them.  1: table increments, 2: learning phase,
+// 4: policy (agents stay; no H lookup), 8: DFF stencil.
+#ifndef FFM_LABLATE
+#define FFM_LABLATE 0
+#endif
+
+// ===========================================================================
+// Batched step: EPB envs per workgroup, LPE = BS / EPB lanes per env, APT
+// agents per lane.  Small rooms (A <= 32) pack two envs onto one wavefront.
+// ===========================================================================
+
 // Segmented exclusive scan of a flag over each env's LPE lanes.
 template <int BS, int LPE>
 __device__ __forceinline__ int env_scan_flag(bool f, int* ws, int& total) {
@@ -966,8 +1049,9 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         p[j] = i < n ? a.pos[e * A + i] : 0;
         if (i < n) grid[p[j]] = (uint16_t)i;
     }
+    const bool trained = a.variant == kVarTrained;
     HStat hs{};
-    if (actor) {
+    if (actor || trained) {
         hs.has = (int)a.hstat[0];
         hs.nonfinite = (int)a.hstat[1];
         hs.mn = a.hstat[2];
@@ -1021,7 +1105,9 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                 wexit[j] = 1;
                 k = ex;
             } else {
-                if (!actor) {
+                if (trained) {
+                    trained_policy(a, tab_find(a.Ht, skey[j]), coord, valid, dff, hs, P);
+                } else if (!actor) {
                     critic_policy(a, coord, valid, dff, P);
                 } else {
                     hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
@@ -1124,7 +1210,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;
-        if (i >= n || (FFM_LABLATE & 2)) continue;
+        if (i >= n || trained || (FFM_LABLATE & 2)) continue;
         double r = a.step_penalty;
         if (wexit[j]) r = r + a.exit_reward;
         if (coll[j] >= 0) r = r + (double)coll[j] * a.collision_penalty;

@@ -37,7 +37,7 @@ EXPORTED = [
     "ffm_learner_delta_export", "ffm_learner_delta_merge",
 ]
 
-VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY = 1, 2, 3
+VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
 LEARN_MODES = {"critic_only": 0, "actor_only": 1, "both": 2}
 TABLE_V, TABLE_H = 0, 1
 
@@ -358,16 +358,20 @@ LEARN_DEFAULTS = {
     "actor_only": {"k_D": 1, "k_A": 10, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann",
                    "alpha_v": 0.1, "gamma": 0.95, "exit_reward": 100.0, "step_penalty": 0.0,
                    "collision_penalty": -1.0, "alpha_h": 0.1, "epsilon": 0.0},
+    # model/ffm_trained_core.py:29-36 (inference: no learning parameters)
+    "trained": {"k_D": 1, "k_A": 10, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann", "block_size": 5},
 }
-_LEARN_VARIANTS = {"ac": VARIANT_AC, "unified": VARIANT_UNIFIED, "actor_only": VARIANT_ACTOR_ONLY}
+_LEARN_VARIANTS = {"ac": VARIANT_AC, "unified": VARIANT_UNIFIED, "actor_only": VARIANT_ACTOR_ONLY,
+                   "trained": VARIANT_TRAINED}
 
 
 class Learner:
     """E environments of one learning model class plus its shared V / H tables.
 
     variant: "ac" (model/ffm_ac_core.py), "unified" (model/ffm_unified.py, with
-    ``mode`` critic_only / actor_only / both) or "actor_only"
-    (model/ffm_actor_only.py).  rng="mt" reproduces the reference bit for bit
+    ``mode`` critic_only / actor_only / both), "actor_only"
+    (model/ffm_actor_only.py) or "trained" (model/ffm_trained_core.py: import
+    the trained H with ``import_table("H", ...)``; nothing is learned).  rng="mt" reproduces the reference bit for bit
     (per-env MT19937 streams, agents and table updates in the reference's
     order); rng="philox" is the batched production step.
     Table keys are packed u64 (ffm_amd/learn_keys.py).
@@ -415,9 +419,10 @@ class Learner:
         ld = LearnDesc()
         ld.mode = LEARN_MODES.get(self.mode, 1) if variant == "unified" else (1 if variant == "actor_only" else 0)
         ld.k_A = float(p.get("k_A", 0.0))
-        ld.alpha_v, ld.alpha_h, ld.gamma = float(p["alpha_v"]), float(p.get("alpha_h", 0.0)), float(p["gamma"])
-        ld.exit_reward, ld.step_penalty = float(p["exit_reward"]), float(p["step_penalty"])
-        ld.collision_penalty = float(p["collision_penalty"])
+        ld.alpha_v, ld.alpha_h = float(p.get("alpha_v", 0.0)), float(p.get("alpha_h", 0.0))
+        ld.gamma = float(p.get("gamma", 0.0))
+        ld.exit_reward, ld.step_penalty = float(p.get("exit_reward", 0.0)), float(p.get("step_penalty", 0.0))
+        ld.collision_penalty = float(p.get("collision_penalty", 0.0))
         ld.epsilon = float(min(max(float(p.get("epsilon", 0.0)), 0.0), 1.0))
         ld.v_default = 0.0
         ld.block_size = int(p.get("block_size", 5))

@@ -53,7 +53,9 @@ enum {
     FFM_VARIANT_CORE = 0,      /* model/ffm_core.py FloorFieldModel              (ffm_engine_*)  */
     FFM_VARIANT_AC = 1,        /* model/ffm_ac_core.py FloorFieldModel           (ffm_learner_*) */
     FFM_VARIANT_UNIFIED = 2,   /* model/ffm_unified.py FloorFieldModelUnified    (ffm_learner_*) */
-    FFM_VARIANT_ACTOR_ONLY = 3 /* model/ffm_actor_only.py FloorFieldModelActorOnly (ffm_learner_*) */
+    FFM_VARIANT_ACTOR_ONLY = 3, /* model/ffm_actor_only.py FloorFieldModelActorOnly (ffm_learner_*) */
+    FFM_VARIANT_TRAINED = 4    /* model/ffm_trained_core.py FloorFieldModel: inference with a trained
+                                  H (ffm_learner_*; import the table, nothing is learned) */
 };
 
 /* Where the random draws come from. */
@@ -183,6 +185,8 @@ typedef struct {
 
 typedef struct ffm_learner ffm_learner;
 
+/* FFM_VARIANT_TRAINED: ffm_learner_import_table(FFM_TABLE_H, ...) loads the trained actor
+ * (model/ffm_trained_core.py:51-68); steps read it and never change it. */
 int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn, ffm_learner** out);
 int ffm_learner_destroy(ffm_learner* l);
 /* Philox: place n_agents in every env (keyed by the step counter, which advances)

@@ -83,6 +83,16 @@ static int64_t tab_get(ffo_tab* t, uint64_t key, const double* init) {
     return h;
 }
 
+/* slot of `key` or -1 (no insertion) */
+static int64_t tab_find(const ffo_tab* t, uint64_t key) {
+    int64_t h = (int64_t)(mix64(key) & (uint64_t)(t->cap - 1));
+    for (;;) {
+        if (t->keys[h] == key) return h;
+        if (t->keys[h] == EMPTY_KEY) return -1;
+        h = (h + 1) & (t->cap - 1);
+    }
+}
+
 static int64_t tab_get_sync(ffo_tab* t, uint64_t key, const double* init, int parallel) {
     int64_t s;
     if (parallel) {
@@ -229,6 +239,7 @@ uint64_t ffo_encode_cells13(const uint8_t* sm, int H, int W, int x, int y, int b
 }
 
 static uint64_t encode(const ffo_learn_cfg* c, const uint8_t* sm, int x, int y) {
+    if (c->variant == FFO_VAR_TRAINED) return ffo_encode_rank(sm, c->H, c->W, x, y, c->block_size);
     if (c->variant == FFO_VAR_UNIFIED) return ffo_encode_rank(sm, c->H, c->W, x, y, c->block_size);
     if (c->variant == FFO_VAR_AC) return ffo_encode_cells13(sm, c->H, c->W, x, y, c->block_size, 2);
     return ffo_encode_cells13(sm, c->H, c->W, x, y, 5, 0);         /* block_size = 5 hard-coded, :143 */
@@ -470,6 +481,50 @@ static int critic_choose(lctx* L, const int32_t* coord, const int* valid, const 
     return choice_cdf(p, 5, dec_u53(&L->rng));
 }
 
+/* ffm_trained_core policy (model/ffm_trained_core.py:219-300): H row (float32;
+ * zeros when the state is missing, :231-239), min/max normalisation of the whole
+ * table in float32 (NEP 50: Python floats are weak next to the f32 array,
+ * :242-267), score -k_A*h + k_D*dff in float32, NumPy's float32 exp, the masked
+ * sum and divide, uniform fallbacks (:270-296), then np.random.choice. */
+static int trained_choose(lctx* L, int64_t hslot, const int32_t* coord, const int* valid, const float* dff) {
+    const ffo_learn_cfg* c = L->c;
+    float h[5], score[5], e[5];
+    double p[5];
+    for (int k = 0; k < 5; k++) h[k] = hslot >= 0 ? (float)L->Ht->vals[hslot * 5 + k] : 0.0f;
+    if (L->hs.has && !L->hs.nonfinite && L->hs.mx - L->hs.mn > 1e-6) {
+        const float hmax = (float)L->hs.mx, den = (float)(L->hs.mx - L->hs.mn);
+        const float srange = (float)((double)L->smax - (double)L->smin), smin = L->smin;
+        for (int k = 0; k < 5; k++) {
+            const float a = hmax - h[k];
+            const float b = a / den;
+            const float d = b * srange;
+            h[k] = d + smin;
+        }
+    }
+    const float nkA = (float)(-c->k_A), kD = (float)c->k_D;
+    int bad = 0, nvalid = 0;
+    for (int k = 0; k < 5; k++) {
+        const float a = nkA * h[k];
+        const float b = kD * dff[coord[k]];
+        score[k] = a + b;
+        if (!isfinite(score[k])) bad = 1;
+        nvalid += valid[k];
+    }
+    if (bad)
+        for (int k = 0; k < 5; k++) score[k] = valid[k] ? 1.0f : 0.0f;
+    float mx = score[0];
+    for (int k = 1; k < 5; k++) mx = score[k] > mx ? score[k] : mx;
+    for (int k = 0; k < 5; k++) e[k] = valid[k] ? ffo_np_expf(score[k] - mx) : 0.0f;
+    const float sum = ffo_np_sumf(e, 5);
+    if (isfinite(sum) && sum > 0) {
+        for (int k = 0; k < 5; k++) p[k] = (double)(e[k] / sum);
+    } else {
+        const float u = (float)(1.0 / (double)nvalid);
+        for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)u : 0.0;
+    }
+    return choice_cdf(p, 5, dec_u53(&L->rng));
+}
+
 /* ffm_ac_core decide = ffm_core decide (model/ffm_ac_core.py:126-199):
  * free neighbours + stay, exit forcing, SFF/DFF softmax.  -1: no request. */
 static int32_t ac_decide(lctx* L, int x, int y, const int32_t* occ, const float* dff, int* will_exit) {
@@ -593,6 +648,17 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
             valid[k] = inb[k] && (m == 0 || m == 3) && (k == 4 || occ[coord[k]] < 0);
         }
         valid[4] = 1;
+        if (c->variant == FFO_VAR_TRAINED) {            /* model/ffm_trained_core.py:169-258 */
+            dec_begin(&L->rng, (uint32_t)i);
+            int ex = -1;
+            for (int k = 0; k < 4; k++)
+                if (inb[k] && c->map[coord[k]] == 3) { ex = k; break; }
+            int k = ex;
+            if (ex < 0) k = trained_choose(L, tab_find(L->Ht, skey[i]), coord, valid, dff);
+            else wexit[i] = 1;
+            rq_tgt[nrq] = coord[k]; rq_agent[nrq++] = i;
+            continue;
+        }
         if (c->variant == FFO_VAR_UNIFIED) {
             dec_begin(&L->rng, (uint32_t)i);
             int ex = -1;
@@ -663,7 +729,8 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
         free(list);
     }
 
-    /* ---- learning ---- */
+    /* ---- learning (none for the trained actor) ---- */
+    if (c->variant == FFO_VAR_TRAINED) goto exits;
     memcpy(smn, c->map, (size_t)HW);
     for (int i = 0; i < n; i++)
         if (c->map[nxt[i]] != 3) smn[nxt[i]] = 1;                    /* :543-546 */
@@ -727,6 +794,7 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
     }
 
     /* ---- exit removal, DFF ---- */
+exits:
     for (int i = 0; i < n; i++) occ[pos[i]] = -1;
     {
         int nn = 0;
@@ -805,7 +873,7 @@ int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, 
                       (c->variant == FFO_VAR_UNIFIED && c->mode != FFO_MODE_CRITIC);
     hstats hs;
     memset(&hs, 0, sizeof hs);
-    if (actor) h_stats(b->Ht, &hs);
+    if (actor || c->variant == FFO_VAR_TRAINED) h_stats(b->Ht, &hs);
     float smin, smax;
     sff_minmax(c, &smin, &smax);
     ffo_tab_mark(b->V);

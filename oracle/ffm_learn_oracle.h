@@ -11,6 +11,9 @@
  *    tables read and written in agent order exactly as the reference's dicts
  *    (Gauss-Seidel).  Pinned by tests/golden/learn_*.npz, recorded from the
  *    reference itself (tests/golden/gen_golden_learn.py).
+ *  * FFO_VAR_TRAINED restates model/ffm_trained_core.py: the rank-keyed H table
+ *    of a trained actor, read only (missing states score as zeros), float32
+ *    policy arithmetic, conflicts always have a winner, no learning.
  *  * Philox ("batched"): every env of a batch steps against
  *    the tables as they were at the start of the step; the TD and actor
  *    increments of all envs are summed in 2^-32 fixed point (order-free, so
@@ -30,7 +33,7 @@
 extern "C" {
 #endif
 
-enum { FFO_VAR_AC = 1, FFO_VAR_UNIFIED = 2, FFO_VAR_ACTOR_ONLY = 3 };
+enum { FFO_VAR_AC = 1, FFO_VAR_UNIFIED = 2, FFO_VAR_ACTOR_ONLY = 3, FFO_VAR_TRAINED = 4 };
 enum { FFO_MODE_CRITIC = 0, FFO_MODE_ACTOR = 1, FFO_MODE_BOTH = 2 };
 
 typedef struct {

@@ -15,7 +15,7 @@ import numpy as np
 
 from . import oracle as O
 
-VARIANTS = {"ac": 1, "unified": 2, "actor_only": 3}
+VARIANTS = {"ac": 1, "unified": 2, "actor_only": 3, "trained": 4}
 MODES = {"critic_only": 0, "actor_only": 1, "both": 2}
 
 # Class defaults of the reference (merged under the caller's params like the reference does).
@@ -32,6 +32,8 @@ DEFAULTS = {
     "actor_only": {"k_D": 1, "k_A": 10, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann",
                    "alpha_v": 0.1, "gamma": 0.95, "exit_reward": 100.0, "step_penalty": 0.0,
                    "collision_penalty": -1.0, "alpha_h": 0.1, "epsilon": 0.0},
+    # model/ffm_trained_core.py:29-36 (inference only: no learning parameters)
+    "trained": {"k_D": 1, "k_A": 10, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann", "block_size": 5},
 }
 
 
@@ -138,8 +140,8 @@ class Learn:
             self.sff64.ctypes.data if self.sff64 is not None else None,
             VARIANTS[variant], MODES[self.mode] if variant == "unified" else (0 if variant == "ac" else 1),
             float(p.get("k_S", 0.0)), float(p["k_D"]), float(p.get("k_A", 0.0)), float(p["diffuse"]),
-            float(p["decay"]), float(p["alpha_v"]), float(p.get("alpha_h", 0.0)), float(p["gamma"]),
-            float(p["exit_reward"]), float(p["step_penalty"]), float(p["collision_penalty"]),
+            float(p["decay"]), float(p.get("alpha_v", 0.0)), float(p.get("alpha_h", 0.0)), float(p.get("gamma", 0.0)),
+            float(p.get("exit_reward", 0.0)), float(p.get("step_penalty", 0.0)), float(p.get("collision_penalty", 0.0)),
             float(p.get("epsilon", 0.0)), 0.0, int(p.get("block_size", 5)))
 
     def set_epsilon(self, e: float):

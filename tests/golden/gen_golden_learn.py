@@ -128,6 +128,59 @@ def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_ste
           f"-> {os.path.getsize(path)} B")
 
 
+def run_trained_case(name, cls, map_array, sff, params, N, seeds, n_ep, max_steps, h_table):
+    """model/ffm_trained_core.py driven like run_trained_ffm.py:213-295: per episode
+    model.N, model.positions = model.initialize_agents(), model.dff = zeros, run."""
+    H, W = map_array.shape
+    init, nsteps, counts, cells, hashes, np_tail, py_tail = [], [], [], [], [], [], []
+    with tempfile.TemporaryDirectory() as td:
+        sff_path = os.path.join(td, "sff.npy")
+        np.save(sff_path, sff)
+        h_path = os.path.join(td, "h.pkl")
+        with open(h_path, "wb") as f:      # bytes keys: the loader calls pickle.loads on them (:55-68)
+            pickle.dump({pickle.dumps(k): list(v) for k, v in h_table.items()}, f)
+        for seed in seeds:
+            np.random.seed(seed)
+            random.seed(seed)
+            with contextlib.redirect_stdout(io.StringIO()):
+                model = cls(map_array, sff_path, N, h_path, params=dict(params))
+            for ep in range(n_ep):
+                if ep > 0:
+                    model.positions = model.initialize_agents()
+                    model.dff = np.zeros_like(model.map_array, dtype=np.float32)
+                p0 = model.positions
+                init.append((p0[:, 0] * W + p0[:, 1]).astype(np.int16))
+                steps = 0
+                while model.positions.shape[0] > 0 and steps < max_steps:
+                    model.step()
+                    steps += 1
+                    p = model.positions
+                    counts.append(p.shape[0])
+                    cells.extend((p[:, 0] * W + p[:, 1]).astype(np.int16).tolist())
+                    hashes.append(dff_hash(model.dff))
+                nsteps.append(steps)
+            bg = np.random.mtrand._rand._bit_generator
+            np_tail.append(np.asarray(bg.random_raw(4), dtype=np.uint32))
+            py_tail.append(np.asarray([random.getrandbits(32) for _ in range(4)], dtype=np.uint32))
+    out = dict(
+        map=map_array.astype(np.uint8), sff=sff, params=json.dumps(params), variant="trained", mode="",
+        N=np.int32(N), seeds=np.asarray(seeds, np.int64), n_ep=np.int32(n_ep), max_steps=np.int32(max_steps),
+        reload_v=np.int32(0), eps=np.zeros(len(nsteps)),
+        init=np.concatenate(init).astype(np.int16), init_n=np.asarray([len(i) for i in init], np.int32),
+        nsteps=np.asarray(nsteps, np.int32), counts=np.asarray(counts, np.int16),
+        cells=np.asarray(cells, np.int16), dff_hash=np.asarray(hashes, np.uint64),
+        v_keys=np.zeros(0, np.uint64), v_vals=np.zeros(0, np.float64), v_n=np.zeros(len(seeds), np.int64),
+        h_keys=np.zeros(0, np.uint64), h_vals=np.zeros((0, 5), np.float64), h_n=np.zeros(len(seeds), np.int64),
+        np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
+        pre_h_keys=np.asarray([K.from_rank_tuple(k) for k in h_table], np.uint64),
+        pre_h_vals=np.asarray([list(map(float, v)) for v in h_table.values()], np.float64).reshape(-1, 5),
+    )
+    path = os.path.join(HERE, f"learn_{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: seeds={len(seeds)} episodes={len(nsteps)} steps={sum(nsteps)} |H|={len(h_table)} "
+          f"-> {os.path.getsize(path)} B")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -138,6 +191,7 @@ def main():
     from model.ffm_ac_core import FloorFieldModel as AC
     from model.ffm_unified import FloorFieldModelUnified as UNI
     from model.ffm_actor_only import FloorFieldModelActorOnly as AO
+    from model.ffm_trained_core import FloorFieldModel as TR
 
     global run_case
     _run = run_case
@@ -199,6 +253,28 @@ def main():
              mode="actor_only", eps_sched=eps, pretrained=pre_u)
     run_case("actoronly_pretrained_12x12_N16", "actor_only", AO, m12, s12, ao_p, 16, [16], 3, 300,
              eps_sched=eps, pretrained=pre_a)
+
+    # ffm_trained_core with an H trained by the reference's unified actor
+    # (run_trained_ffm.py loads such a table, :141-203)
+    if not only or "trained_12x12_N24" in only or "trained_12x12_N40_bs5" in only:
+        np.random.seed(17)
+        random.seed(17)
+        with tempfile.TemporaryDirectory() as td, contextlib.redirect_stdout(io.StringIO()):
+            sp = os.path.join(td, "s.npy")
+            np.save(sp, s12)
+            tables = {}
+            for bs in (1, 5):
+                ua = UNI(m12, sp, 24, learning_mode="both", params=dict(uni_p, block_size=bs))
+                for ep in range(6):
+                    ua.set_epsilon(0.2)
+                    ua.reset()
+                    ua.run(max_steps=200)
+                tables[bs] = ua.get_h_table()
+        tr_p = {"k_D": 1, "k_A": 10, "neighborhood": "neumann", "block_size": 1}
+        if not only or "trained_12x12_N24" in only:
+            run_trained_case("trained_12x12_N24", TR, m12, s12, tr_p, 24, [18, 19], 3, 300, tables[1])
+        if not only or "trained_12x12_N40_bs5" in only:
+            run_trained_case("trained_12x12_N40_bs5", TR, m12, s12, {}, 40, [20], 3, 300, tables[5])
 
 
 if __name__ == "__main__":

@@ -169,6 +169,16 @@ def test_learning_dropin_signatures_match_reference():
             assert callable(getattr(c, m)), (c, m)
 
 
+def test_trained_dropin_signature_matches_reference():
+    """model/ffm_trained_core.py:20 FloorFieldModel(map_array, sff_path, N, h_table_path, params=None)."""
+    from ffm_amd.model.ffm_trained_core import FloorFieldModel as TR
+    assert list(inspect.signature(TR.__init__).parameters) == ["self", "map_array", "sff_path", "N", "h_table_path",
+                                                              "params"]
+    assert list(inspect.signature(TR.run).parameters) == ["self", "save_prefix", "save_interval", "max_steps"]
+    for m in ("initialize_agents", "get_neighbors", "step", "update_dff"):
+        assert callable(getattr(TR, m))
+
+
 def test_unified_dropin_rejects_bad_mode_before_device(tmp_path):
     """ValueError of model/ffm_unified.py:59-63, raised before any device work."""
     from ffm_amd.data import make_room, l1_sff

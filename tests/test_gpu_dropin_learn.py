@@ -46,6 +46,7 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
     from ffm_amd.model.ffm_ac_core import FloorFieldModel as AC
     from ffm_amd.model.ffm_actor_only import FloorFieldModelActorOnly as AO
     from ffm_amd.model.ffm_unified import FloorFieldModelUnified as UNI
+    from ffm_amd.model.ffm_trained_core import FloorFieldModel as TR
     z = np.load(os.path.join(GOLDEN_DIR, f"learn_{name}.npz"), allow_pickle=False)
     z = {k: z[k] for k in z.files}
     params = json.loads(str(z["params"]))
@@ -55,6 +56,11 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
     sff_path = str(tmp_path / "sff.npy")
     np.save(sff_path, z["sff"])
     kw = {}
+    if "pre_h_keys" in z:            # a trained actor, pickled as run_trained_ffm.py loads it
+        kw["h_table_path"] = str(tmp_path / "h.pkl")
+        with open(kw["h_table_path"], "wb") as f:
+            pickle.dump({pickle.dumps(K.to_rank_tuple(k)): [float(x) for x in v]
+                         for k, v in zip(z["pre_h_keys"], z["pre_h_vals"])}, f)
     if "pre_keys" in z:
         kw["pretrained_v_path"] = str(tmp_path / "v.pkl")
         if variant == "unified":
@@ -71,10 +77,15 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
             model = UNI(z["map"], sff_path, N, learning_mode=mode, params=dict(params), **kw)
         elif variant == "ac":
             model = AC(z["map"], sff_path, N, params=dict(params))
+        elif variant == "trained":
+            model = TR(z["map"], sff_path, N, kw["h_table_path"], params=dict(params))
         else:
             model = AO(z["map"], sff_path, N, params=dict(params), **kw)
         for ep in range(n_ep):
-            if ep > 0:
+            if ep > 0 and variant == "trained":      # run_trained_ffm.py:227-237
+                model.positions = model.initialize_agents()
+                model.dff = np.zeros_like(model.map_array, dtype=np.float32)
+            elif ep > 0:
                 if int(z["reload_v"]):
                     model.set_v_table(model.get_v_table())
                 model.reset()
@@ -98,6 +109,12 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
                 step_i += 1
             assert steps == int(z["nsteps"][ep_i])
             ep_i += 1
+        if variant == "trained":
+            assert list(np.random.mtrand._rand._bit_generator.random_raw(4)) == list(z["np_tail"][si])
+            assert [random.getrandbits(32) for _ in range(4)] == list(z["py_tail"][si])
+            assert len(model.H) == len(z["pre_h_keys"])
+            model.close()
+            continue
         V = model.get_v_table()
         nv = int(z["v_n"][si])
         assert len(V) == nv

@@ -62,7 +62,7 @@ def test_learner_replays_reference_goldens(name):
     for si, seed in enumerate(z["seeds"]):
         L = _learner(z["map"], z["sff"], variant, n_envs=1, n_agents=0, agent_capacity=max(N, 1), mode=mode,
                      params=params, rng="mt", auto_reset=False)
-        inert_k, inert_v = pretrained(z, variant, lambda k, v: L.import_table("V", k, v))
+        inert_k, inert_v = pretrained(z, variant, lambda k, v, w="V": L.import_table(w, k, v))
         np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
         for ep in range(n_ep):
             if ep > 0 and int(z["reload_v"]):
@@ -120,6 +120,16 @@ def test_learner_replays_reference_goldens(name):
 # ---------------------------------------------------------------------------
 # Philox (batched) mode: GPU == CPU restatement
 # ---------------------------------------------------------------------------
+def _random_rank_table(H, W, bs, seed=0, frac=0.6):
+    """A trained-actor-like H over the rank keys of an H x W map (ffm_trained_core input)."""
+    from ffm_amd import learn_keys as K
+    rs = np.random.RandomState(seed)
+    keys = [K.pack(((c >> 0) & 3, (c >> 2) & 3, (c >> 4) & 3, (c >> 6) & 3), bx, by)
+            for bx in range((H - 1) // bs + 1) for by in range((W - 1) // bs + 1) for c in range(256)
+            if rs.uniform() < frac]
+    return np.array(keys, np.uint64), rs.standard_normal((len(keys), 5)) * 3.0
+
+
 def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
                     nthreads=16, sff_dtype=np.float32):
     from ffm_amd.data import make_room, l1_sff
@@ -131,6 +141,10 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     L = _learner(m, s, variant, n_envs=E, n_agents=N, agent_capacity=A, mode=mode, params=params,
                  rng="philox", seed=seed, auto_reset=True, max_steps=max_steps, env_base=env_base)
     cpu = LO.Learn(m, s, variant, mode, params, log2_cap=22)
+    if variant == "trained":
+        hk, hv = _random_rank_table(H, W, int(params.get("block_size", 5)), seed=seed)
+        L.import_table("H", hk, hv)
+        cpu.Ht.load(hk, hv)
     core = O.Core(m, s, {"neighborhood": "neumann"})
     pos = np.full((E, A), 0xFFFF, np.uint16)
     for e in range(E):
@@ -157,7 +171,7 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
         assert np.array_equal(gp[e, :counts[e]], pos[e, :counts[e]]), f"env {e} positions"
     assert np.array_equal(gd.view(np.uint32), dff.view(np.uint32)), "DFF bits"
     for which, tab in (("V", cpu.V), ("H", cpu.Ht)):
-        if which == "H" and variant != "actor_only" and mode in (None, "critic_only"):
+        if which == "H" and variant not in ("actor_only", "trained") and mode in (None, "critic_only"):
             continue
         ck, cv = tab.export()
         gk, gv = L.export_table(which)
@@ -172,6 +186,14 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     assert c["steps"] == T
     L.close()
     return counts, eps
+
+
+def test_learner_philox_trained_matches_cpu():
+    """ffm_trained_core batched: a read-only trained H, float32 policy, always-a-winner
+    conflicts; 12x12 block 1 and an odd room with block 3."""
+    _philox_compare("trained", None, {"block_size": 1}, 12, 12, 32, 2048, 120)
+    _philox_compare("trained", None, {"block_size": 3, "k_A": 4}, 11, 17, 20, 333, 90, A=24, seed=9,
+                    env_base=1 << 20)
 
 
 @pytest.mark.parametrize("variant,mode", VARIANTS)

@@ -31,6 +31,9 @@ def pretrained(z, variant, load):
     never match, so it stays inert and only leads get_v_table()'s order.
     Returns that inert prefix (keys, values)."""
     none = (np.zeros(0, np.uint64), np.zeros(0, np.float64))
+    if "pre_h_keys" in z:                # ffm_trained_core: the trained H (model/ffm_trained_core.py:51-68)
+        load(z["pre_h_keys"], z["pre_h_vals"], "H")
+        return none
     if "pre_keys" not in z:
         return none
     if variant == "unified":
@@ -50,7 +53,7 @@ def replay(z, make_step):
     v_off = h_off = 0
     for si, seed in enumerate(z["seeds"]):
         L = LO.Learn(z["map"], z["sff"], variant, mode, params)
-        inert_k, inert_v = pretrained(z, variant, lambda k, v: L.V.load(k, v))
+        inert_k, inert_v = pretrained(z, variant, lambda k, v, w="V": (L.V if w == "V" else L.Ht).load(k, v))
         np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
         for ep in range(n_ep):
             if ep > 0 and int(z["reload_v"]):
