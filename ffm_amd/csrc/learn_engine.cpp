@@ -73,6 +73,10 @@ struct ffm_learner {
     bool hstat_valid = false;          // d_hstat holds the H statistics of the current table
     int phase = 0;                     // batched step in phases: 0 idle, 1 local done, 2 V applied
     unsigned long long* d_count = nullptr;   // delta export record counter
+    int32_t* d_eplog = nullptr;              // [eplog_cap][4] ended episodes
+    unsigned long long* d_eplog_n = nullptr;
+    long long eplog_cap = 0;
+    int F_all = 0;                           // free cells of the map (placement capacity)
     DevTable V, H;
 };
 
@@ -89,7 +93,8 @@ static void release(ffm_learner* l) {
     if (!l) return;
     void* bufs[] = {l->d_map, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
-                    l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count};
+                    l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
+                    l->d_eplog, l->d_eplog_n};
     for (void* p : bufs) (void)hipFree(p);
     free_table(l->V);
     free_table(l->H);
@@ -148,6 +153,9 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.auto_reset = d.auto_reset && !l->mt; a.max_steps = l->L.max_steps;
     a.mt_np = l->d_mt_np; a.mt_py = l->d_mt_py; a.scratch = l->d_scratch;
     a.free_cells = l->d_free_cells;
+    a.eps_start = l->L.eps_start; a.eps_end = l->L.eps_end;
+    a.eps_offset = l->L.eps_offset; a.eps_span = l->L.eps_span;
+    a.eplog = l->d_eplog; a.eplog_n = l->d_eplog_n; a.eplog_cap = l->eplog_cap;
     return a;
 }
 
@@ -231,6 +239,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     l->f64 = d.sff_dtype == FFM_SFF_F64;
     l->HW = HW;
     l->F = (int)fl.size();
+    l->F_all = l->F;
     l->D = d.variant == FFM_VARIANT_ACTOR_ONLY ? 4 : 1;
     l->actor = d.variant == FFM_VARIANT_ACTOR_ONLY || (d.variant == FFM_VARIANT_UNIFIED && learn->mode != FFM_LEARN_CRITIC_ONLY);
     l->post_update = d.variant == FFM_VARIANT_UNIFIED && learn->mode == FFM_LEARN_ACTOR_ONLY;
@@ -281,6 +290,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (l->post_update && !l->mt) ALLOC(l->d_recs, E * A * sizeof(ffm::LearnRec));
     ALLOC(l->d_overflow, 4);
     ALLOC(l->d_count, 8);
+    l->eplog_cap = std::max<long long>(4 * (long long)E, 4096);
+    ALLOC(l->d_eplog, (size_t)l->eplog_cap * 16);
+    ALLOC(l->d_eplog_n, 8);
     if (l->mt) {
         ALLOC(l->d_mt_np, E * 625 * 4);
         ALLOC(l->d_mt_py, E * 625 * 4);
@@ -318,6 +330,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (he == hipSuccess) he = hipMemset(l->d_ctr, 0, E * 32);
     if (he == hipSuccess) he = hipMemset(l->d_hstat, 0, 32);
     if (he == hipSuccess) he = hipMemset(l->d_overflow, 0, 4);
+    if (he == hipSuccess) he = hipMemset(l->d_eplog_n, 0, 8);
     if (he == hipSuccess && l->mt) he = hipMemset(l->d_mt_np, 0, E * 625 * 4);
     if (he == hipSuccess && l->mt) he = hipMemset(l->d_mt_py, 0, E * 625 * 4);
     if (he == hipSuccess) he = clear_table(l, l->V, l->L.v_default, nullptr);
@@ -664,6 +677,65 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
         if (he != hipSuccess) return fail(FFM_E_HIP, std::string("import: ") + hipGetErrorString(he));
     }
     return check_overflow(l, s);
+}
+
+int ffm_learner_set_placement(ffm_learner* l, const uint16_t* cells, int32_t count, int32_t n_agents) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (count < 0 || count > l->F_all || (count > 0 && !cells)) return fail(FFM_E_INVALID, "placement cell count");
+    const int navail = count > 0 ? count : l->F_all;
+    if (n_agents < 0 || n_agents > navail || n_agents > l->d.agent_capacity)
+        return fail(FFM_E_INVALID, "n_agents must be <= the candidate cells and agent_capacity");
+    std::vector<uint16_t> fl;
+    std::vector<uint8_t> map(l->HW);
+    HIP_TRY(hipMemcpy(map.data(), l->d_map, l->HW, hipMemcpyDeviceToHost));
+    if (count > 0) {
+        std::vector<uint8_t> seen(l->HW, 0);
+        for (int i = 0; i < count; i++) {
+            if (cells[i] >= l->HW || map[cells[i]] != 0) return fail(FFM_E_INVALID, "placement cell is not free");
+            if (seen[cells[i]]) return fail(FFM_E_INVALID, "placement cells repeat");
+            seen[cells[i]] = 1;
+            fl.push_back(cells[i]);
+        }
+    } else {
+        for (int i = 0; i < l->HW; i++)
+            if (map[i] == 0) fl.push_back((uint16_t)i);
+    }
+    if (!l->mt && (int)fl.size() > 16384 && n_agents > 12288)
+        return fail(FFM_E_UNSUPPORTED, "on-device placement supports n_agents <= 12288 above 16384 candidates");
+    HIP_TRY(hipDeviceSynchronize());
+    if (!fl.empty()) HIP_TRY(hipMemcpy(l->d_free_cells, fl.data(), fl.size() * 2, hipMemcpyHostToDevice));
+    l->F = (int)fl.size();
+    l->d.n_agents = n_agents;
+    return FFM_OK;
+}
+
+int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double eps_end, double eps_offset,
+                                     double eps_span) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    l->L.eps_start = eps_start; l->L.eps_end = eps_end;
+    l->L.eps_offset = eps_offset; l->L.eps_span = eps_span;
+    return FFM_OK;
+}
+
+int ffm_learner_drain_episodes(ffm_learner* l, int32_t* records, int64_t cap, int64_t* n, int64_t* dropped,
+                               void* stream) {
+    if (!l || !n) return fail(FFM_E_INVALID, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, l->d_eplog_n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const long long have = std::min<long long>((long long)c, l->eplog_cap);
+    if (have > cap) {
+        *n = have;
+        return fail(FFM_E_INVALID, "drain_episodes: buffer too small (*n holds the count)");
+    }
+    if (have > 0 && records)
+        HIP_TRY(hipMemcpyAsync(records, l->d_eplog, (size_t)have * 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemsetAsync(l->d_eplog_n, 0, 8, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n = have;
+    if (dropped) *dropped = (int64_t)c - have;
+    return FFM_OK;
 }
 
 int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t) {

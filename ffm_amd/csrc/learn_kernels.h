@@ -69,7 +69,12 @@ struct LearnArgs {
     uint32_t* mt_np;            // [E][625] (exact mode)
     uint32_t* mt_py;
     unsigned char* scratch;     // exact mode scratch
-    const uint16_t* free_cells;    // [F] x*W+y of the free cells, row-major (np.argwhere(map == 0))
+    const uint16_t* free_cells;    // [F] placement candidates: x*W+y of the free cells, row-major
+                                   // (np.argwhere(map == 0)), or a radius-limited subset of them
+    double eps_start, eps_end, eps_offset, eps_span;   // batched epsilon schedule (eps_span > 0)
+    int* eplog;                 // [eplog_cap][4] ended episodes: global env, index, steps, emptied
+    unsigned long long* eplog_n;
+    long long eplog_cap;
 };
 
 constexpr int kHstatBlocks = 512;

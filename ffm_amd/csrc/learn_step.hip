@@ -968,6 +968,25 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 // agents per lane.  Small rooms (A <= 32) pack two envs onto one wavefront.
 // ===========================================================================
 
+// This env's epsilon: the learner's, or the batched schedule's after k ended
+// episodes (run_actor_only_training.py:190-196, run_unified_actor_training.py:253-259).
+__device__ __forceinline__ double env_epsilon(const LearnArgs& a, int k) {
+    if (!(a.eps_span > 0)) return a.epsilon;
+    const double e = a.eps_start + (a.eps_end - a.eps_start) * (((double)k + a.eps_offset) / a.eps_span);
+    return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
+}
+
+// One record per ended episode (ffm_learner_drain_episodes).
+__device__ __forceinline__ void log_episode(const LearnArgs& a, long long e) {
+    const unsigned long long r = atomicAdd(a.eplog_n, 1ull);
+    if ((long long)r >= a.eplog_cap) return;
+    int* q = a.eplog + 4 * r;
+    q[0] = (int)(a.env_base + e);
+    q[1] = a.episodes[e];
+    q[2] = a.ep_steps[e];
+    q[3] = a.cnt[e] == 0;
+}
+
 // Segmented exclusive scan of a flag over each env's LPE lanes.
 template <int BS, int LPE>
 __device__ __forceinline__ int env_scan_flag(bool f, int* ws, int& total) {
@@ -1050,6 +1069,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         if (i < n) grid[p[j]] = (uint16_t)i;
     }
     const bool trained = a.variant == kVarTrained;
+    const double eps = live && actor ? env_epsilon(a, a.episodes[e]) : 0.0;
     HStat hs{};
     if (actor || trained) {
         hs.has = (int)a.hstat[0];
@@ -1115,7 +1135,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                     actor_policy(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, false, P);
                 }
                 DrawPh rng(a, genv, (uint32_t)i);
-                k = policy_draw(P, actor ? a.epsilon : 0.0, rng);
+                k = policy_draw(P, eps, rng);
             }
             req[i] = (uint16_t)coord[k];
             act[j] = k; avalid[j] = valid[k];
@@ -1134,7 +1154,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                     k = ex;
                 } else {
                     DrawPh rng(a, genv, (uint32_t)(i * 4 + d));
-                    k = policy_draw(P, a.epsilon, rng);
+                    k = policy_draw(P, eps, rng);
                 }
                 req[i * 4 + d] = (uint16_t)coord[k];
             }
@@ -1458,6 +1478,7 @@ __global__ __launch_bounds__(kResetBS) void learn_reset_kernel(LearnArgs a, int 
     float* d = a.dff_in + e * (long long)a.HW;
     for (int c = tid; c < a.HW; c += kResetBS) d[c] = 0.0f;
     if (tid == 0) {
+        if (!all) log_episode(a, e);
         a.cnt[e] = NN;
         a.ep_steps[e] = 0;
         a.done[e] = 0;
@@ -1540,6 +1561,7 @@ __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int 
         float* d = a.dff_in + e * (long long)HW;
         for (int c = lane; c < HW; c += 64) d[c] = 0.0f;
         if (lane == 0) {
+            if (!all) log_episode(a, e);
             a.cnt[e] = N;
             a.ep_steps[e] = 0;
             a.done[e] = 0;

@@ -34,7 +34,8 @@ EXPORTED = [
     "ffm_learner_set_epsilon", "ffm_learner_set_v_default", "ffm_learner_table_size",
     "ffm_learner_export_table", "ffm_learner_import_table", "ffm_learner_get_step_index",
     "ffm_learner_set_step_index", "ffm_learner_step_local", "ffm_learner_step_apply", "ffm_learner_step_end",
-    "ffm_learner_delta_export", "ffm_learner_delta_merge",
+    "ffm_learner_delta_export", "ffm_learner_delta_merge", "ffm_learner_set_placement",
+    "ffm_learner_set_epsilon_schedule", "ffm_learner_drain_episodes",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -63,6 +64,7 @@ class LearnDesc(C.Structure):
         ("epsilon", C.c_double), ("v_default", C.c_double),
         ("block_size", C.c_int32), ("max_steps", C.c_int32),
         ("log2_v_capacity", C.c_int32), ("log2_h_capacity", C.c_int32),
+        ("eps_start", C.c_double), ("eps_end", C.c_double), ("eps_offset", C.c_double), ("eps_span", C.c_double),
     ]
 
 
@@ -126,6 +128,9 @@ def load_library():
     L.ffm_learner_step_end.argtypes = [P, P]
     L.ffm_learner_delta_export.argtypes = [P, i32, P, P, i64, C.POINTER(i64), P]
     L.ffm_learner_delta_merge.argtypes = [P, i32, P, P, i64, P]
+    L.ffm_learner_set_placement.argtypes = [P, P, i32, i32]
+    L.ffm_learner_set_epsilon_schedule.argtypes = [P, C.c_double, C.c_double, C.c_double, C.c_double]
+    L.ffm_learner_drain_episodes.argtypes = [P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     for name in EXPORTED:
         if name != "ffm_last_error":
             getattr(L, name).restype = C.c_int
@@ -458,6 +463,41 @@ class Learner:
 
     def set_epsilon(self, eps: float):
         _check(self._L.ffm_learner_set_epsilon(self._h, float(eps)))
+
+    def set_placement(self, cells=None, n_agents: int | None = None):
+        """Placement candidates of later resets (cell indices x*W+y; None = every free
+        cell) and the agents placed, min(N, len(cells)) like model/ffm_unified.py:150-171."""
+        c = np.zeros(0, np.uint16) if cells is None else np.ascontiguousarray(cells, dtype=np.uint16)
+        n = int(n_agents if n_agents is not None else self.n_agents)
+        _check(self._L.ffm_learner_set_placement(self._h, _ptr(c) if len(c) else None, len(c), n))
+        self.n_agents = n
+
+    def set_radius_placement(self, exit_pos, radius: int, N: int):
+        """The radius curriculum of run_unified_*_training.py: free cells within L1
+        distance `radius` of `exit_pos` (row-major), min(N, their count) agents."""
+        free = np.argwhere(self.map == 0)
+        m = np.abs(free[:, 0] - exit_pos[0]) + np.abs(free[:, 1] - exit_pos[1]) <= radius
+        cells = (free[m, 0] * self.W + free[m, 1]).astype(np.uint16)
+        self.set_placement(cells if len(cells) else None, min(int(N), len(cells)))
+        return len(cells)
+
+    def set_epsilon_schedule(self, start: float, end: float, offset: float, span: float):
+        """Per-env epsilon clip(start + (end - start) * (k + offset) / span) after k ended episodes."""
+        _check(self._L.ffm_learner_set_epsilon_schedule(self._h, float(start), float(end), float(offset),
+                                                          float(span)))
+
+    def drain_episodes(self, stream=None) -> np.ndarray:
+        """Ended episodes since the last drain: int32 [n, 4] rows {global env, episode index,
+        steps, emptied}, sorted by (env, episode)."""
+        cap = max(4 * self.n_envs, 4096)
+        buf = np.empty((cap, 4), np.int32)
+        n, dropped = C.c_int64(), C.c_int64()
+        _check(self._L.ffm_learner_drain_episodes(self._h, _ptr(buf), cap, C.byref(n), C.byref(dropped),
+                                                  _stream_handle(stream)))
+        if dropped.value:
+            raise RuntimeError(f"episode log overflowed: {dropped.value} records lost (drain more often)")
+        out = buf[: n.value]
+        return out[np.lexsort((out[:, 1], out[:, 0]))]
 
     def set_v_default(self, v: float, stream=None):
         _check(self._L.ffm_learner_set_v_default(self._h, float(v), _stream_handle(stream)))

@@ -181,6 +181,11 @@ typedef struct {
     int32_t max_steps;        /* Philox mode: an episode also ends after this many steps (0 = never) */
     int32_t log2_v_capacity;  /* hash-table slots (0 = 21) */
     int32_t log2_h_capacity;
+    /* Philox mode, eps_span > 0: each env explores with
+     * clip(eps_start + (eps_end - eps_start) * (k + eps_offset) / eps_span, 0, 1) after k ended
+     * episodes (run_actor_only_training.py:190-196: offset 0, span total episodes - 1;
+     * run_unified_actor_training.py:253-259: offset 1, span episodes per configuration). */
+    double eps_start, eps_end, eps_offset, eps_span;
 } ffm_learn_desc;
 
 typedef struct ffm_learner ffm_learner;
@@ -234,6 +239,18 @@ int ffm_learner_delta_export(ffm_learner* l, int32_t which, uint64_t* d_keys, in
                              int64_t* n, void* stream);
 int ffm_learner_delta_merge(ffm_learner* l, int32_t which, const uint64_t* d_keys, const int64_t* d_acc,
                             int64_t n, void* stream);
+/* Philox placement candidates of later resets: `count` distinct free cells (x*W+y) and the
+ * agents to place, <= count (the radius curriculum, model/ffm_unified.py:150-171:
+ * actual_N = min(N, cells within the radius)).  count = 0 restores every free cell. */
+int ffm_learner_set_placement(ffm_learner* l, const uint16_t* cells, int32_t count, int32_t n_agents);
+int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double eps_end, double eps_offset,
+                                     double eps_span);
+/* Ended episodes since the last drain, in no particular order: records of 4 int32
+ * {global env, episode index, steps, 1 = emptied / 0 = truncated at max_steps}
+ * (the per-episode rows of run_*_training.py's steps_per_episode.csv).  *dropped counts
+ * records lost because the log was full (capacity max(4 E, 4096)). */
+int ffm_learner_drain_episodes(ffm_learner* l, int32_t* records, int64_t cap, int64_t* n, int64_t* dropped,
+                               void* stream);
 int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t);
 int ffm_learner_set_step_index(ffm_learner* l, uint32_t t);
 

@@ -345,6 +345,7 @@ typedef struct {
     hstats hs;
     float smin, smax;      /* min/max of the inf->0 SFF (model/ffm_unified.py:74-76, 425-426) */
     lrng rng;
+    double eps;            /* this env's epsilon (the global one, or the batched schedule's) */
 } lctx;
 
 typedef struct {
@@ -427,7 +428,7 @@ static int actor_choose(lctx* L, int64_t hslot, const int32_t* coord, const int*
     } else {
         for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
     }
-    if (c->epsilon > 0 && dec_coin(&L->rng) < c->epsilon) {          /* :478-495 */
+    if (L->eps > 0 && dec_coin(&L->rng) < L->eps) {                  /* :478-495 */
         if (nvalid > 0) return vidx[dec_randint(&L->rng, (uint32_t)nvalid)];
         return 4;
     }
@@ -827,6 +828,7 @@ int ffo_learn_step_mt(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int32_t* 
     lctx L;
     memset(&L, 0, sizeof L);
     L.c = c; L.V = V; L.Ht = Ht; L.jacobi = 0; L.parallel = 0;
+    L.eps = c->epsilon;
     if (Ht) h_stats(Ht, &L.hs);
     sff_minmax(c, &L.smin, &L.smax);
     L.rng.philox = 0; L.rng.np = np_rng; L.rng.py = py_rng;
@@ -847,7 +849,22 @@ struct ffo_lbatch {
     int32_t A_cap;
     lrec* recs;
     int32_t* nstart;
+    uint16_t* place;       /* placement candidates (NULL: every free cell) */
+    int32_t nplace;
 };
+
+void ffo_lbatch_set_placement(ffo_lbatch* b, const uint16_t* cells, int32_t count) {
+    free(b->place);
+    b->place = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(count > 0 ? count : 1));
+    memcpy(b->place, cells, sizeof(uint16_t) * (size_t)count);
+    b->nplace = count;
+}
+
+static double eps_of(const ffo_learn_cfg* c, int32_t k) {
+    if (!(c->eps_span > 0)) return c->epsilon;
+    double e = c->eps_start + (c->eps_end - c->eps_start) * (((double)k + c->eps_offset) / c->eps_span);
+    return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
+}
 
 ffo_lbatch* ffo_lbatch_new(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E, int32_t A_cap) {
     ffo_lbatch* b = (ffo_lbatch*)calloc(1, sizeof(ffo_lbatch));
@@ -859,12 +876,12 @@ ffo_lbatch* ffo_lbatch_new(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int6
 
 void ffo_lbatch_free(ffo_lbatch* b) {
     if (!b) return;
-    free(b->recs); free(b->nstart); free(b);
+    free(b->recs); free(b->nstart); free(b->place); free(b);
 }
 
 /* Every env's step against the tables as they are; increments left pending. */
-int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, uint64_t seed, uint32_t t,
-                     int64_t env_base, uint64_t* agent_steps, int nthreads) {
+int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, const int32_t* episodes,
+                     uint64_t seed, uint32_t t, int64_t env_base, uint64_t* agent_steps, int nthreads) {
     const ffo_learn_cfg* c = b->c;
     const int HW = c->H * c->W;
     const int64_t E = b->E;
@@ -906,6 +923,7 @@ int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, 
             total += (uint64_t)n;
             for (int i = 0; i < n; i++) p32[i] = pe[i];
             L.rng.genv = (uint64_t)(env_base + e);
+            L.eps = eps_of(c, episodes ? episodes[e] : 0);
             if (env_step(&L, p32, &n, dff + e * (int64_t)HW, occ, sm, sm + HW, B, b->recs + e * (int64_t)A_cap))
                 err = 1;
             for (int i = 0; i < n; i++) pe[i] = (uint16_t)p32[i];
@@ -935,9 +953,10 @@ void ffo_lbatch_apply(ffo_lbatch* b, int which) {
 }
 
 /* Episode ends: emptied, or truncated at max_steps (run_*_training.py MAX_STEPS). */
-void ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, int32_t* episodes,
-                    int32_t* ep_steps, uint64_t seed, uint32_t t, int32_t auto_reset, int32_t N_reset,
-                    int32_t max_steps, int64_t env_base) {
+int64_t ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, int32_t* episodes,
+                       int32_t* ep_steps, uint64_t seed, uint32_t t, int32_t auto_reset, int32_t N_reset,
+                       int32_t max_steps, int64_t env_base, int32_t* log) {
+    int64_t nlog = 0;
     const ffo_learn_cfg* c = b->c;
     const int HW = c->H * c->W;
     ffo_core_cfg cc;
@@ -946,13 +965,24 @@ void ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, i
     for (int64_t e = 0; e < b->E; e++) {
         ep_steps[e]++;
         if (auto_reset && (counts[e] == 0 || (max_steps > 0 && ep_steps[e] >= max_steps))) {
-            ffo_reset_philox(&cc, N_reset, seed, t, env_base + e, pos + e * (int64_t)b->A_cap);
+            if (log) {
+                int32_t* r = log + 4 * nlog;
+                r[0] = (int32_t)(env_base + e);
+                r[1] = episodes ? episodes[e] : 0;
+                r[2] = ep_steps[e];
+                r[3] = counts[e] == 0;
+            }
+            nlog++;
+            if (b->place) ffo_reset_philox_list(b->place, b->nplace, N_reset, seed, t, env_base + e,
+                                                pos + e * (int64_t)b->A_cap);
+            else ffo_reset_philox(&cc, N_reset, seed, t, env_base + e, pos + e * (int64_t)b->A_cap);
             counts[e] = N_reset;
             memset(dff + e * (int64_t)HW, 0, sizeof(float) * (size_t)HW);
             ep_steps[e] = 0;
             if (episodes) episodes[e]++;
         }
     }
+    return nlog;
 }
 
 int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E,
@@ -963,10 +993,11 @@ int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht,
     const int actor = c->variant == FFO_VAR_ACTOR_ONLY ||
                       (c->variant == FFO_VAR_UNIFIED && c->mode != FFO_MODE_CRITIC);
     ffo_lbatch* b = ffo_lbatch_new(c, V, Ht, E, A_cap);
-    const int rc = ffo_lbatch_local(b, pos, counts, dff, seed, t, env_base, agent_steps, nthreads);
+    const int rc = ffo_lbatch_local(b, pos, counts, dff, episodes, seed, t, env_base, agent_steps, nthreads);
     ffo_lbatch_apply(b, 0);
     if (actor) ffo_lbatch_apply(b, 1);
-    ffo_lbatch_end(b, pos, counts, dff, episodes, ep_steps, seed, t, auto_reset, N_reset, max_steps, env_base);
+    ffo_lbatch_end(b, pos, counts, dff, episodes, ep_steps, seed, t, auto_reset, N_reset, max_steps, env_base,
+                   NULL);
     ffo_lbatch_free(b);
     return rc;
 }

@@ -47,6 +47,11 @@ typedef struct {
     double epsilon;
     double v_default;         /* value of a V entry created by a read (0.0; -1.0 after set_v_table, ac) */
     int32_t block_size;
+    /* batched epsilon schedule (eps_span > 0): an env whose k episodes have ended
+     * explores with clip(eps_start + (eps_end - eps_start) * (k + eps_offset) / eps_span)
+     * (run_actor_only_training.py:190-196: offset 0, span total-1;
+     * run_unified_actor_training.py:253-259: offset 1, span episodes per config) */
+    double eps_start, eps_end, eps_offset, eps_span;
 } ffo_learn_cfg;
 
 typedef struct ffo_tab ffo_tab;
@@ -81,12 +86,17 @@ int ffo_learn_step_philox_batch(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht,
 typedef struct ffo_lbatch ffo_lbatch;
 ffo_lbatch* ffo_lbatch_new(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E, int32_t A_cap);
 void ffo_lbatch_free(ffo_lbatch* b);
-int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, uint64_t seed, uint32_t t,
-                     int64_t env_base, uint64_t* agent_steps, int nthreads);
+int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, const int32_t* episodes,
+                     uint64_t seed, uint32_t t, int64_t env_base, uint64_t* agent_steps, int nthreads);
+/* Placement candidates of the episode ends (default: every free cell). */
+void ffo_lbatch_set_placement(ffo_lbatch* b, const uint16_t* cells, int32_t count);
 void ffo_lbatch_apply(ffo_lbatch* b, int which);
-void ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, int32_t* episodes,
-                    int32_t* ep_steps, uint64_t seed, uint32_t t, int32_t auto_reset, int32_t N_reset,
-                    int32_t max_steps, int64_t env_base);
+/* Episode ends; log (may be NULL) receives one record per ended episode:
+ * {global env, index of the episode, its steps, 1 if emptied / 0 if truncated};
+ * returns the record count. */
+int64_t ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, int32_t* episodes,
+                       int32_t* ep_steps, uint64_t seed, uint32_t t, int32_t auto_reset, int32_t N_reset,
+                       int32_t max_steps, int64_t env_base, int32_t* log);
 void ffo_tab_mark(ffo_tab* t);
 int64_t ffo_tab_delta_export(const ffo_tab* t, uint64_t* keys, int64_t* acc);
 int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, int64_t n, const double* init);

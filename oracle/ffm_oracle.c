@@ -512,6 +512,13 @@ static void reset_with_list(const uint16_t* fl, int F, int32_t N, uint64_t seed,
     for (int s = 0; s < N; s++) pos_out[s] = fl[scratch[s] & 0xFFFFu];
 }
 
+void ffo_reset_philox_list(const uint16_t* fl, int32_t F, int32_t N, uint64_t seed, uint32_t t, int64_t genv,
+                           uint16_t* pos_out) {
+    uint64_t* scratch = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(F > 0 ? F : 1));
+    reset_with_list(fl, F, N, seed, t, genv, scratch, pos_out);
+    free(scratch);
+}
+
 void ffo_reset_philox(const ffo_core_cfg* c, int32_t N, uint64_t seed, uint32_t t,
                       int64_t genv, uint16_t* pos_out) {
     const int HW = c->H * c->W;

@@ -45,6 +45,7 @@ class LearnCfg(C.Structure):
         ("decay", C.c_double), ("alpha_v", C.c_double), ("alpha_h", C.c_double), ("gamma", C.c_double),
         ("exit_reward", C.c_double), ("step_penalty", C.c_double), ("collision_penalty", C.c_double),
         ("epsilon", C.c_double), ("v_default", C.c_double), ("block_size", C.c_int32),
+        ("eps_start", C.c_double), ("eps_end", C.c_double), ("eps_offset", C.c_double), ("eps_span", C.c_double),
     ]
 
 
@@ -73,11 +74,14 @@ def _lib():
         L.ffo_lbatch_new.argtypes = [C.POINTER(LearnCfg), P, P, C.c_int64, C.c_int32]
         L.ffo_lbatch_new.restype = P
         L.ffo_lbatch_free.argtypes = [P]
-        L.ffo_lbatch_local.argtypes = [P, P, P, P, C.c_uint64, C.c_uint32, C.c_int64, C.POINTER(C.c_uint64), C.c_int]
+        L.ffo_lbatch_local.argtypes = [P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int64, C.POINTER(C.c_uint64),
+                                       C.c_int]
+        L.ffo_lbatch_set_placement.argtypes = [P, P, C.c_int32]
         L.ffo_lbatch_local.restype = C.c_int
         L.ffo_lbatch_apply.argtypes = [P, C.c_int]
         L.ffo_lbatch_end.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
-                                     C.c_int64]
+                                     C.c_int64, P]
+        L.ffo_lbatch_end.restype = C.c_int64
         L.ffo_tab_delta_export.argtypes = [P, P, P]
         L.ffo_tab_delta_export.restype = C.c_int64
         L.ffo_tab_delta_merge.argtypes = [P, P, P, C.c_int64, P]
@@ -150,6 +154,10 @@ class Learn:
     def set_v_default(self, v: float):
         self.cfg.v_default = float(v)
 
+    def set_epsilon_schedule(self, start: float, end: float, offset: float, span: float):
+        self.cfg.eps_start, self.cfg.eps_end = float(start), float(end)
+        self.cfg.eps_offset, self.cfg.eps_span = float(offset), float(span)
+
     def step_mt(self, pos, dff, np_rng, py_rng):
         p = np.ascontiguousarray(pos, dtype=np.int32).copy()
         n = np.array([p.shape[0]], dtype=np.int32)
@@ -198,6 +206,7 @@ class Shard:
         self.ep_steps = np.zeros(E, np.int32)
         self.t = 1
         self.agent_steps = 0
+        self.log = []
         self.b = _lib().ffo_lbatch_new(C.byref(learn.cfg), learn.V.h, learn.Ht.h, E, A)
 
     def __del__(self):
@@ -218,18 +227,26 @@ class Shard:
 
     def step_local(self):
         tot = C.c_uint64(0)
-        if _lib().ffo_lbatch_local(self.b, O._ptr(self.pos), O._ptr(self.counts), O._ptr(self.dff), self.seed,
-                                   self.t, self.env_base, C.byref(tot), self.nthreads):
+        if _lib().ffo_lbatch_local(self.b, O._ptr(self.pos), O._ptr(self.counts), O._ptr(self.dff),
+                                   O._ptr(self.episodes), self.seed, self.t, self.env_base, C.byref(tot),
+                                   self.nthreads):
             raise RuntimeError("oracle table full")
         self.agent_steps += int(tot.value)
 
     def step_apply(self, which):
         _lib().ffo_lbatch_apply(self.b, 0 if which == "V" else 1)
 
+    def set_placement(self, cells, n_agents: int):
+        c = np.ascontiguousarray(cells, np.uint16)
+        _lib().ffo_lbatch_set_placement(self.b, O._ptr(c), len(c))
+        self.N = int(n_agents)
+
     def step_end(self):
-        _lib().ffo_lbatch_end(self.b, O._ptr(self.pos), O._ptr(self.counts), O._ptr(self.dff),
-                              O._ptr(self.episodes), O._ptr(self.ep_steps), self.seed, self.t, 1, self.N,
-                              self.max_steps, self.env_base)
+        log = np.zeros((self.E, 4), np.int32)
+        n = _lib().ffo_lbatch_end(self.b, O._ptr(self.pos), O._ptr(self.counts), O._ptr(self.dff),
+                                  O._ptr(self.episodes), O._ptr(self.ep_steps), self.seed, self.t, 1, self.N,
+                                  self.max_steps, self.env_base, O._ptr(log))
+        self.log.extend(map(tuple, log[:n].tolist()))
         self.t += 1
 
     def delta_export(self, which, keys_ptr, acc_ptr, cap):

@@ -103,6 +103,7 @@ def lib():
             C.c_int32, C.c_int32, C.c_int64, C.POINTER(C.c_uint64), C.c_int]
         L.ffo_reset_philox.argtypes = [C.POINTER(CoreCfg), C.c_int32, C.c_uint64, C.c_uint32,
                                        C.c_int64, P]
+        L.ffo_reset_philox_list.argtypes = [P, C.c_int32, C.c_int32, C.c_uint64, C.c_uint32, C.c_int64, P]
         _lib = L
     return _lib
 
@@ -190,6 +191,14 @@ class Core:
         out = np.zeros(max(N, 1), dtype=np.uint16)
         lib().ffo_reset_philox(C.byref(self.cfg), N, seed, t, genv, _ptr(out))
         return out[:N]
+
+
+def reset_philox_list(cells, N, seed, t, genv) -> np.ndarray:
+    """Philox placement over an explicit candidate list (radius curriculum)."""
+    c = np.ascontiguousarray(cells, dtype=np.uint16)
+    out = np.zeros(max(N, 1), dtype=np.uint16)
+    lib().ffo_reset_philox_list(_ptr(c), len(c), N, seed, t, genv, _ptr(out))
+    return out[:N]
 
 
 def np_expf(x: np.ndarray, nthreads: int = 8) -> np.ndarray:

@@ -350,3 +350,60 @@ def test_learner_coupled_shards_equal_one_learner(variant, mode):
             assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), which
     for L in shards + [one]:
         L.close()
+
+
+@pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None), ("unified", "critic_only")])
+def test_learner_curriculum_schedule_and_episode_log(variant, mode):
+    """The batched training drivers' knobs against the CPU restatement: radius-limited
+    placement (model/ffm_unified.py:150-171: min(N, cells within the radius)), the
+    per-env epsilon schedule (run_unified_actor_training.py:253-259), and the episode
+    log (one record per ended episode: env, index, steps, emptied)."""
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import learn as LO
+    from oracle import oracle as O
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"block_size": 1, "step_penalty": -1.0, "gamma": 0.99, "alpha_v": 0.01}
+    E, N, T, seed, maxs = 600, 30, 160, 7, 40
+    L = _learner(m, s, variant, n_envs=E, n_agents=N, mode=mode, params=p, seed=seed, max_steps=maxs)
+    ncell = L.set_radius_placement((0, 6), 4, N)
+    n = min(N, ncell)
+    L.set_epsilon_schedule(0.2, 0.01, 1, 10)
+    L.reset()
+    cpu = LO.Learn(m, s, variant, mode, p, log2_cap=22)
+    cpu.set_epsilon_schedule(0.2, 0.01, 1, 10)
+    sh = LO.Shard(cpu, E, N, n, seed, 0, maxs, nthreads=16)
+    free = np.argwhere(m == 0)
+    r = np.abs(free[:, 0]) + np.abs(free[:, 1] - 6) <= 4
+    cells = (free[r, 0] * 12 + free[r, 1]).astype(np.uint16)
+    assert len(cells) == ncell
+    sh.set_placement(cells, n)
+    sh.pos[:] = 0xFFFF
+    for e in range(E):
+        sh.pos[e, :n] = O.reset_philox_list(cells, n, seed, 0, e)
+    sh.counts[:] = n
+    for _ in range(T):
+        sh.step_local()
+        sh.step_apply("V")
+        if sh.actor:
+            sh.step_apply("H")
+        sh.step_end()
+    L.step(T)
+    gp, gc, gd = L.get_state()
+    assert np.array_equal(gc, sh.counts)
+    assert np.array_equal(gd.view(np.uint32), sh.dff.view(np.uint32))
+    for e in range(E):
+        assert np.array_equal(gp[e, :gc[e]], sh.pos[e, :gc[e]])
+    eps_, _ = L.episodes()
+    assert np.array_equal(eps_, sh.episodes)
+    log = L.drain_episodes()
+    want = np.array(sorted(sh.log), np.int32).reshape(-1, 4)
+    assert np.array_equal(log, want)
+    assert len(log) > E and set(np.unique(log[:, 3])) <= {0, 1}
+    assert (log[log[:, 3] == 0, 2] == maxs).all()       # truncated episodes ran max_steps
+    assert L.drain_episodes().shape == (0, 4)             # drained
+    k0, v0 = L.export_table("V")
+    k1, v1 = cpu.V.export()
+    assert np.array_equal(np.sort(k0), np.sort(k1))
+    assert np.array_equal(v0[np.argsort(k0)].view(np.uint64), v1[np.argsort(k1)].view(np.uint64))
+    L.close()
