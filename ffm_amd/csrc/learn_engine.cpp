@@ -290,7 +290,8 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (l->post_update && !l->mt) ALLOC(l->d_recs, E * A * sizeof(ffm::LearnRec));
     ALLOC(l->d_overflow, 4);
     ALLOC(l->d_count, 8);
-    l->eplog_cap = std::max<long long>(4 * (long long)E, 4096);
+    // an env ends at most one episode per step: 16 steps between drains always fit
+    l->eplog_cap = std::max<long long>(16 * (long long)E, 4096);
     ALLOC(l->d_eplog, (size_t)l->eplog_cap * 16);
     ALLOC(l->d_eplog_n, 8);
     if (l->mt) {
@@ -356,6 +357,7 @@ int ffm_learner_reset(ffm_learner* l, void* stream) {
     HIP_TRY(hipMemsetAsync(l->d_dff[l->cur], 0, E * l->HW * 4, s));
     HIP_TRY(hipMemsetAsync(l->d_cnt, 0, E * 4, s));
     HIP_TRY(hipMemsetAsync(l->d_ep_steps, 0, E * 4, s));
+    HIP_TRY(hipMemsetAsync(l->d_eps, 0, E * 4, s));        // episodes count from this reset
     HIP_TRY(hipMemsetAsync(l->d_pos, 0xFF, E * l->d.agent_capacity * 2, s));
     if (l->mt) return FFM_OK;
     HIP_TRY(ffm::launch_learn_reset(make_args(l), true, s));

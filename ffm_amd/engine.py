@@ -489,7 +489,7 @@ class Learner:
     def drain_episodes(self, stream=None) -> np.ndarray:
         """Ended episodes since the last drain: int32 [n, 4] rows {global env, episode index,
         steps, emptied}, sorted by (env, episode)."""
-        cap = max(4 * self.n_envs, 4096)
+        cap = max(16 * self.n_envs, 4096)
         buf = np.empty((cap, 4), np.int32)
         n, dropped = C.c_int64(), C.c_int64()
         _check(self._L.ffm_learner_drain_episodes(self._h, _ptr(buf), cap, C.byref(n), C.byref(dropped),

@@ -194,8 +194,8 @@ typedef struct ffm_learner ffm_learner;
  * (model/ffm_trained_core.py:51-68); steps read it and never change it. */
 int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn, ffm_learner** out);
 int ffm_learner_destroy(ffm_learner* l);
-/* Philox: place n_agents in every env (keyed by the step counter, which advances)
- * and zero the DFF.  MT: zero the DFF and counts only (the caller uploads
+/* Philox: place n_agents in every env (keyed by the step counter, which advances),
+ * zero the DFF and the per-env episode counters.  MT: zero the DFF and counts only (the caller uploads
  * positions drawn from its own generators, like ffm_engine_reset). */
 int ffm_learner_reset(ffm_learner* l, void* stream);
 int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream);
@@ -248,7 +248,8 @@ int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double ep
 /* Ended episodes since the last drain, in no particular order: records of 4 int32
  * {global env, episode index, steps, 1 = emptied / 0 = truncated at max_steps}
  * (the per-episode rows of run_*_training.py's steps_per_episode.csv).  *dropped counts
- * records lost because the log was full (capacity max(4 E, 4096)). */
+ * records lost because the log was full (capacity max(16 E, 4096): an env ends at most one
+ * episode per step, so draining every 16 steps never loses one). */
 int ffm_learner_drain_episodes(ffm_learner* l, int32_t* records, int64_t cap, int64_t* n, int64_t* dropped,
                                void* stream);
 int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t);

@@ -407,3 +407,41 @@ def test_learner_curriculum_schedule_and_episode_log(variant, mode):
     assert np.array_equal(np.sort(k0), np.sort(k1))
     assert np.array_equal(v0[np.argsort(k0)].view(np.uint64), v1[np.argsort(k1)].view(np.uint64))
     L.close()
+
+
+# model/ffm_unified.py critic_only on the 12x12 room with run_unified_critic_training.py's
+# MODEL_PARAMS: mean steps per episode per (radius, N), 1000 reference episodes each
+# (output/logs/unified_critic_training/run_20260117_101523/summary.txt:38-82 of the reference).
+REF_CRITIC_MEAN_STEPS = {(5, 10): 19.71, (15, 1): 7.95, (15, 10): 21.46, (15, 20): 40.46, (15, 50): 99.56}
+
+
+def test_batched_critic_curriculum_matches_reference_logged_means(tmp_path):
+    """Distributional pin of the batched semantics against the reference's own run
+    log: critic_only's policy does not read V, so the episode-length distribution per
+    (radius, N) is fixed by the dynamics alone.  ffm_amd.train.run_curriculum runs
+    the same curriculum batched; each mean must lie within 4 standard errors of the
+    logged one (the reference's standard error estimated from our spread, n = 1000)."""
+    import csv
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Learner
+    from ffm_amd.train import run_curriculum
+    m = make_room(12, 12)
+    p = {"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99, "exit_reward": 100.0,
+         "step_penalty": -1.0, "collision_penalty": -1.0, "neighborhood": "neumann", "block_size": 1}
+    L = Learner(m, l1_sff(m), "unified", n_envs=2048, n_agents=50, mode="critic_only", params=p, seed=3,
+                max_steps=300)
+    res = run_curriculum(L, (0, 6), [5, 15], [1, 10, 20, 50], 4096, out_dir=str(tmp_path), verbose=False)
+    got = {(c["radius"], c["N"]): c for c in res["configs"]}
+    assert (5, 20) in got and (5, 50) not in got           # N above the cells in radius 5 is skipped
+    for key, ref in REF_CRITIC_MEAN_STEPS.items():
+        c = got[key]
+        se = np.sqrt(c["std_steps"] ** 2 / c["episodes"] + c["std_steps"] ** 2 / 1000)
+        assert abs(c["mean_steps"] - ref) <= max(4 * se, 0.05), (key, c["mean_steps"], ref, se)
+        assert c["emptied"] == c["episodes"]                # no truncation at 300 steps
+    with open(tmp_path / "steps_per_episode.csv") as f:
+        rows = list(csv.reader(f))
+    assert rows[0] == ["episode_num", "config_idx", "radius", "N", "steps", "v_table_size", "h_table_size",
+                       "epsilon"]
+    assert len(rows) == 1 + 4096 * len(res["configs"])      # 2 episodes of every one of the 2048 envs
+    assert (tmp_path / "summary.txt").exists() and (tmp_path / "V_table.pkl").exists()
+    L.close()
