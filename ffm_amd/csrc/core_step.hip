@@ -514,15 +514,28 @@ void core_wave_kernel(CoreStepArgs a) {
 // ===========================================================================
 // Block kernel: K envs per workgroup of BS threads.
 // ===========================================================================
+// The map and SFF are read from global memory (L2-resident, shared by every
+// block) and the placement keys are capped: LDS per block drops from ~82 KB to
+// ~40 KB at config 3 (64x64, 512 agents), 3 blocks per CU instead of 1.
 struct BlockCarve {
-    size_t map, sff, grid, dff, pos, req, nxt, misc, u, flag, keys, total;
+    size_t grid, dff, pos, req, nxt, misc, u, flag, keys, total;
 };
+
+// Placement candidates kept in LDS: the threshold of reset_threshold() passes
+// ~2N + 16 keys (N <= A); room for 8 standard deviations more.  More (or fewer
+// than N) take the exact recomputing path (probability < 1e-15).
+__host__ __device__ inline int block_keys_cap(int A, int F) {
+    const int m = 2 * A + 16;
+    int r = 1;
+    while (r * r < m) r++;
+    const int cap = m + 8 * r + 64;
+    return cap < F ? cap : F;
+}
 
 __host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, bool f64, bool mt, bool reset) {
     BlockCarve c;
     size_t o = 0;
-    c.map = o;  o += align16((size_t)PHW);
-    c.sff = o;  o += align16((size_t)PHW * (f64 ? 8 : 4));
+    (void)f64;
     c.grid = o; o += align16((size_t)K * PHW * 2);
     c.dff = o;  o += align16((size_t)K * PHW * 4);
     c.pos = o;  o += align16((size_t)K * A * 2);
@@ -531,7 +544,7 @@ __host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, 
     c.misc = o; o += align16((size_t)(8 * K + 64) * 4);
     c.u = o;    o += mt ? align16((size_t)K * A * 8) : 0;
     c.flag = o; o += mt ? align16((size_t)K * A * 2) : 0;
-    c.keys = o; o += reset ? align16((size_t)F * 8) : 0;
+    c.keys = o; o += reset ? align16((size_t)block_keys_cap(A, F) * 8) : 0;
     c.total = o;
     return c;
 }
@@ -570,9 +583,10 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     const int K = (int)((a.E - e0) < a.K ? (a.E - e0) : a.K);
     const bool do_reset = !MT && a.auto_reset;
     const BlockCarve cv = block_carve(PHW, A, a.K, a.F, F64, MT, do_reset);
-    uint8_t* pmap = smem + cv.map;
-    float* psff32 = reinterpret_cast<float*>(smem + cv.sff);
-    double* psff64 = reinterpret_cast<double*>(smem + cv.sff);
+    const uint8_t* pmap = a.pmap;
+    const float* psff32 = reinterpret_cast<const float*>(a.psff);
+    const double* psff64 = reinterpret_cast<const double*>(a.psff);
+    const int KC = block_keys_cap(A, a.F);
     GT* grid = reinterpret_cast<GT*>(smem + cv.grid);
     float* tile = reinterpret_cast<float*>(smem + cv.dff);
     uint16_t* spos = reinterpret_cast<uint16_t*>(smem + cv.pos);
@@ -589,11 +603,6 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     const int nP = K * PHW;
 
     // ---- load -------------------------------------------------------------------
-    for (int i = tid; i < PHW; i += BS) {
-        pmap[i] = a.pmap[i];
-        if (F64) psff64[i] = reinterpret_cast<const double*>(a.psff)[i];
-        else psff32[i] = reinterpret_cast<const float*>(a.psff)[i];
-    }
     for (int i = tid; i < nP; i += BS) {
         const int k = i / PHW, pc = i - k * PHW;
         const int x = pc / PW - 1, y = pc - (pc / PW) * PW - 1;
@@ -778,19 +787,36 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
                     }
                     int tot;
                     const int ex = block_excl_scan<BS>(cand, swsum, tot);
-                    if (cand) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
+                    if (cand && C + ex < KC) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
                     C += tot;
                 }
-                if (C >= a.N || T == 0xFFFFFFFFu) break;
+                if ((C >= a.N && C <= KC) || T == 0xFFFFFFFFu) break;
+                if (C > KC) break;       // too many to keep: the recomputing path below
                 T = 0xFFFFFFFFu;
             }
             __syncthreads();
-            for (int i = tid; i < C; i += BS) {
-                const unsigned long long ki = keys[i];
-                int rank = 0;
+            if (C <= KC) {
+                for (int i = tid; i < C; i += BS) {
+                    const unsigned long long ki = keys[i];
+                    int rank = 0;
 #pragma unroll 4
-                for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-                if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[(int)(ki & 0xFFFFu)], PW);
+                    for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
+                    if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[(int)(ki & 0xFFFFu)], PW);
+                }
+            } else {
+                // Exact but slow (keys recomputed per comparison): the candidates exceed KC.
+                for (int j = tid; j < a.F; j += BS) {
+                    const uint32_t kj = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
+                    if (kj > T) continue;
+                    const unsigned long long ki = ((unsigned long long)kj << 32) | (unsigned)j;
+                    int rank = 0;
+                    for (int q = 0; q < a.F && rank < a.N; q++) {
+                        const unsigned long long kq =
+                            ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)q) << 32) | (unsigned)q;
+                        rank += kq < ki ? 1 : 0;
+                    }
+                    if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[j], PW);
+                }
             }
             __syncthreads();
         }

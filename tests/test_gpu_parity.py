@@ -296,3 +296,11 @@ def test_invalid_inputs_raise():
     with pytest.raises(ValueError):
         eng.set_state(0, positions=np.zeros((1, 4), np.uint16), counts=np.array([2], np.int32))  # wall cell
     eng.close()
+
+
+def test_philox_block_kernel_capped_placement_keys():
+    """Block kernel with more free cells than the LDS key capacity (40x40 room, 16 agents:
+    F = 1444 > 2A + 16 + 8 sqrt(2A + 16) + 64): auto-resets draw their placement from the
+    thresholded candidates kept in LDS, identical to the oracle's full sort."""
+    cnt, eps = _philox_compare(40, 40, 16, 300, 200, {"neighborhood": "neumann"}, seed=13, envs_per_block=1)
+    assert eps.sum() > 0
