@@ -553,6 +553,47 @@ size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool m
     return block_carve((H + 2) * (W + 2), A, K, F, f64, mt, reset).total;
 }
 
+// (env, row, column) of a flat index i = (k * rows + r) * cols + c, advanced by a
+// fixed stride without integer division (a runtime divide is ~30 VALU, and the
+// cell loops of the block kernel would otherwise run two per cell).
+struct Idx3 {
+    int k, r, c;
+    int dr, dc, rows, cols;
+    __device__ Idx3(int i, int stride, int rows_, int cols_) : rows(rows_), cols(cols_) {
+        const int per = rows * cols;
+        k = i / per;
+        const int rem = i - k * per;
+        r = rem / cols;
+        c = rem - r * cols;
+        dr = stride / cols;
+        dc = stride - dr * cols;
+    }
+    __device__ __forceinline__ void advance() {
+        c += dc;
+        r += dr;
+        if (c >= cols) { c -= cols; r++; }
+        while (r >= rows) { r -= rows; k++; }
+    }
+};
+
+// (env, agent) of flat agent slot it = k * A + i, advanced by the block size
+// without integer division.
+struct AgentIdx {
+    int it, k, i, dk, di, A;
+    __device__ AgentIdx(int it0, int stride, int A_) : it(it0), A(A_) {
+        k = it0 / A;
+        i = it0 - k * A;
+        dk = stride / A;
+        di = stride - dk * A;
+    }
+    __device__ __forceinline__ void advance() {
+        it += dk * A + di;
+        i += di;
+        k += dk;
+        if (i >= A) { i -= A; k++; }
+    }
+};
+
 // Block-wide exclusive prefix of a 0/1 flag over thread order (+ total).
 template <int BS>
 __device__ __forceinline__ int block_excl_scan(bool flag, int* swsum, int& total) {
@@ -601,22 +642,26 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
 
     const int nA = K * A;
     const int nP = K * PHW;
+    const AgentIdx ag0(tid, BS, A);   // this thread's first (env, agent) slot
 
     // ---- load -------------------------------------------------------------------
-    for (int i = tid; i < nP; i += BS) {
-        const int k = i / PHW, pc = i - k * PHW;
-        const int x = pc / PW - 1, y = pc - (pc / PW) * PW - 1;
-        const bool in = x >= 0 && x < H && y >= 0 && y < W;
-        tile[i] = in ? a.dff[(e0 + k) * HW + x * W + y] : 0.0f;
-        grid[i] = a.pmap[pc];
+    {
+        Idx3 ix(tid, BS, H + 2, PW);
+        for (int i = tid; i < nP; i += BS, ix.advance()) {
+            const int x = ix.r - 1, y = ix.c - 1, pc = ix.r * PW + ix.c;
+            const bool in = x >= 0 && x < H && y >= 0 && y < W;
+            tile[i] = in ? a.dff[(e0 + ix.k) * HW + x * W + y] : 0.0f;
+            grid[i] = a.pmap[pc];
+        }
     }
     if (tid < K) {
         scnt[tid] = a.cnt[e0 + tid];
         sreset[tid] = 0;
     }
     __syncthreads();
-    for (int it = tid; it < nA; it += BS) {
-        const int k = it / A, i = it - k * A;
+    for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
+        const int it = ag.it;
+        const int k = ag.k, i = ag.i;
         int pp = 0xFFFF;
         if (i < scnt[k]) {
             const int c = a.pos[(e0 + k) * A + i];
@@ -628,8 +673,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     __syncthreads();
 
     // ---- occupancy marks --------------------------------------------------------------
-    for (int it = tid; it < nA; it += BS) {
-        const int k = it / A, i = it - k * A;
+    for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
+        const int it = ag.it;
+        const int k = ag.k, i = ag.i;
         if (i < scnt[k]) grid[k * PHW + spos[it]] = (GT)(GridCodes<GT>::kAgent | (uint32_t)i);
         snxt[it] = spos[it];
         sreq[it] = kNoReq;
@@ -637,8 +683,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     __syncthreads();
 
     // ---- decide (model/ffm_core.py:40-88) -----------------------------------------------
-    for (int it = tid; it < nA; it += BS) {
-        const int k = it / A, i = it - k * A;
+    for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
+        const int it = ag.it;
+        const int k = ag.k, i = ag.i;
         if (i >= scnt[k]) continue;
         const int pp = spos[it];
         uint32_t r;
@@ -662,8 +709,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
                 if (sreq[tid * A + i] == kPending) su[tid * A + i] = mt_u53(mt_np);
         }
         __syncthreads();
-        for (int it = tid; it < nA; it += BS) {
-            const int k = it / A, i = it - k * A;
+        for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
+        const int it = ag.it;
+            const int k = ag.k, i = ag.i;
             if (i >= scnt[k] || sreq[it] != kPending) continue;
             sreq[it] = (uint16_t)slot_cell<NB>(decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
                                                      a.kS32, a.kD32, a.kS64, DrawFixed{su[it]}), spos[it], PW);
@@ -672,8 +720,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
 
         // Owners of contested targets, then their draws in owner (= dict) order.
         uint16_t* sflag = reinterpret_cast<uint16_t*>(smem + cv.flag);
-        for (int it = tid; it < nA; it += BS) {
-            const int k = it / A, i = it - k * A;
+        for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
+        const int it = ag.it;
+            const int k = ag.k, i = ag.i;
             sflag[it] = 0;
             if (i >= scnt[k]) continue;
             const int r = sreq[it];
@@ -701,8 +750,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     }
 
     // ---- resolve (model/ffm_core.py:90-98) ---------------------------------------------------
-    for (int it = tid; it < nA; it += BS) {
-        const int k = it / A, i = it - k * A;
+    for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
+        const int it = ag.it;
+        const int k = ag.k, i = ag.i;
         if (i >= scnt[k]) continue;
         const int r = sreq[it];
         if (r == kNoReq) continue;
@@ -747,9 +797,10 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) -------------------------
     {
         int carry = 0;
-        for (int base = 0; base < nA; base += BS) {
+        AgentIdx ex = ag0;
+        for (int base = 0; base < nA; base += BS, ex.advance()) {
             const int it = base + tid;
-            const int k = it / A, i = it - k * A;
+            const int k = ex.k, i = ex.i;
             const bool live = it < nA && i < scnt[k];
             const bool keep = live && pmap[snxt[it]] != 3;
             int tot;
@@ -844,9 +895,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     // ---- update_dff (model/ffm_core.py:106-117) --------------------------------------------------
     for (int i = tid; i < nP; i += BS) tile[i] = a.c0 * tile[i];                       // :109 (halo stays 0)
     __syncthreads();
-    for (int c = tid; c < K * HW; c += BS) {
-        const int k = c / HW, cell = c - k * HW;
-        const int x = cell / W, y = cell - (cell / W) * W;
+    Idx3 ix(tid, BS, H, W);
+    for (int c = tid; c < K * HW; c += BS, ix.advance()) {
+        const int k = ix.k, x = ix.r, y = ix.c;
         const float* p = tile + k * PHW + (x + 1) * PW + y + 1;
         float acc = *p;
 #pragma unroll
