@@ -156,6 +156,9 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.eps_start = l->L.eps_start; a.eps_end = l->L.eps_end;
     a.eps_offset = l->L.eps_offset; a.eps_span = l->L.eps_span;
     a.eplog = l->d_eplog; a.eplog_n = l->d_eplog_n; a.eplog_cap = l->eplog_cap;
+    auto magic = [](int div) { return div <= 1 ? 0u : (uint32_t)(((1ull << 32) + (unsigned)div - 1) / (unsigned)div); };
+    a.mW = magic(d.W);
+    a.mBS = magic(a.bs);
     return a;
 }
 

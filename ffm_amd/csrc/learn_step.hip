@@ -131,6 +131,13 @@ struct SmBits {                  // batch kernel, next positions (exit cells exc
     __device__ int operator()(int c) const { return ((bits[c >> 5] >> (c & 31)) & 1u) ? 1 : map[c]; }
 };
 
+// n / d for 0 <= n < 65536 through m = ceil(2^32 / d): (n * m) >> 32 (checked
+// exhaustively for every 2 <= d <= 65536; m = 0 encodes d = 1).  One v_mul_hi_u32
+// instead of a ~30-instruction integer divide.
+__device__ __forceinline__ int fdiv(int n, uint32_t m) {
+    return m ? (int)__umulhi((unsigned)n, m) : n;
+}
+
 __device__ __forceinline__ unsigned long long pack_key(unsigned long long cells, int bx, int by) {
     return cells | ((unsigned long long)bx << 26) | ((unsigned long long)by << 45);
 }
@@ -140,7 +147,7 @@ __constant__ int kNBy[4] = {0, 0, -1, 1};
 
 // model/ffm_unified.py:188-269
 template <class SM>
-__device__ unsigned long long enc_rank(const SM& sm, int H, int W, int x, int y, int bs) {
+__device__ unsigned long long enc_rank(const SM& sm, int H, int W, int x, int y, uint32_t mbs) {
     unsigned long long cells = 0;
 #pragma unroll
     for (int d = 0; d < 4; d++) {
@@ -173,12 +180,12 @@ __device__ unsigned long long enc_rank(const SM& sm, int H, int W, int x, int y,
         }
         cells |= (unsigned long long)rank << (2 * d);
     }
-    return pack_key(cells, x / bs, y / bs);
+    return pack_key(cells, fdiv(x, mbs), fdiv(y, mbs));
 }
 
 // model/ffm_ac_core.py:62-109 (oob 2) and model/ffm_actor_only.py:102-147 (oob 0)
 template <class SM>
-__device__ unsigned long long enc13(const SM& sm, int H, int W, int x, int y, int bs, int oob) {
+__device__ unsigned long long enc13(const SM& sm, int H, int W, int x, int y, uint32_t mbs, int oob) {
     unsigned long long cells = 0;
     int i = 0;
 #pragma unroll
@@ -195,14 +202,14 @@ __device__ unsigned long long enc13(const SM& sm, int H, int W, int x, int y, in
         const int v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? sm(nx * W + ny) : oob;
         cells |= (unsigned long long)(v & 3) << (2 * i);
     }
-    return pack_key(cells, x / bs, y / bs);
+    return pack_key(cells, fdiv(x, mbs), fdiv(y, mbs));
 }
 
 template <class SM>
 __device__ unsigned long long encode(const LearnArgs& a, const SM& sm, int x, int y) {
-    if (a.variant == kVarUnified || a.variant == kVarTrained) return enc_rank(sm, a.H, a.W, x, y, a.bs);
-    if (a.variant == kVarAC) return enc13(sm, a.H, a.W, x, y, a.bs, 2);
-    return enc13(sm, a.H, a.W, x, y, 5, 0);                    // block 5 hard-coded, :143
+    if (a.variant == kVarUnified || a.variant == kVarTrained) return enc_rank(sm, a.H, a.W, x, y, a.mBS);
+    if (a.variant == kVarAC) return enc13(sm, a.H, a.W, x, y, a.mBS, 2);
+    return enc13(sm, a.H, a.W, x, y, a.mBS, 0);                // block 5 hard-coded, :143 (a.bs = 5)
 }
 
 // ---- random draws -----------------------------------------------------------
@@ -1089,7 +1096,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         const int i = tid + j * LPE;
         act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
         if (i >= n) continue;
-        const int x = p[j] / W, y = p[j] - (p[j] / W) * W;
+        const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
         skey[j] = encode(a, smc, x, y);
         int coord[5], valid[5], inb[5];
         moves5(a, x, y, occ, coord, valid, inb);
@@ -1180,7 +1187,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             const int T = req[i * D + d];
             if (T == kNone16) continue;
             const int mine = i * D + d;
-            const int tx = T / W, ty = T - (T / W) * W;
+            const int tx = fdiv(T, a.mW), ty = T - tx * W;
             int m = 0, owner = 0x7FFFFFFF, rank = 0;
 #pragma unroll
             for (int c5 = 0; c5 < 5; c5++) {
@@ -1237,7 +1244,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         int sn = -1;
         double vn = 0.0;
         if (!wexit[j]) {
-            const int nx = nxt[j] / W, ny = nxt[j] - (nxt[j] / W) * W;
+            const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
             sn = tab_get(a.V, encode(a, smn, nx, ny), a.overflow);
             vn = sn >= 0 ? a.V.vals[sn] : 0.0;
         }
@@ -1275,7 +1282,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     if (live && !(FFM_LABLATE & 8)) {
         float* out = a.dff_out + e * (long long)HW;
         for (int c = tid; c < HW; c += LPE) {
-            const int x = c / W, y = c - (c / W) * W;
+            const int x = fdiv(c, a.mW), y = c - x * W;
             float acc = a.c0 * dff[c];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
