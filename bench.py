@@ -381,20 +381,15 @@ def cpu_baseline(args, m, s, params, torch):
     cnt = np.full(E, A, np.int32)
     dff = np.zeros((E, H, W), np.float32)
     eps = np.zeros(E, np.int32)
-    # calibrate: a few steps, then size the sample to ~15 s of CPU work
+    # a bounded sample: whole steps until ~15 s of CPU work (--cpu-steps fixes the count)
     t = 1
-    ta = time.perf_counter()
-    calib = 0
-    for _ in range(5):
-        calib += core.step_philox_batch(pos, cnt, dff, eps, args.seed, t, True, A, 0, threads)
-        t += 1
-    dt = time.perf_counter() - ta
-    steps = args.cpu_steps or max(10, int(15.0 / max(dt / 5, 1e-6)))
-    tb = time.perf_counter()
     total = 0
-    for _ in range(steps):
+    tb = time.perf_counter()
+    steps = 0
+    while (args.cpu_steps and steps < args.cpu_steps) or (not args.cpu_steps and time.perf_counter() - tb < 15.0):
         total += core.step_philox_batch(pos, cnt, dff, eps, args.seed, t, True, A, 0, threads)
         t += 1
+        steps += 1
     elapsed = time.perf_counter() - tb
     # single-thread rate on a smaller slice of the same state (~3 s)
     n1 = min(E, 512)
