@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--log2-table", type=int, default=0, help="learner V/H hash capacity (0 = engine default)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_config2.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (default: profiles/traffic_<H>x<W>_A<A>_E<E>.json)")
     a = ap.parse_args()
     size, agents, envs, steps, warmup = {2: (12, 32, 65536, 500, 50), 3: (64, 512, 8192, 200, 20),
                                          4: (12, 32, 65536, 300, 30), 5: (256, 8192, 512, 50, 5)}[a.config]
@@ -149,8 +150,9 @@ def main():
         mean_kernel_s = float(np.mean(kern_ms)) / 1e3
         achieved = E * bytes_per_env_step / mean_kernel_s / 1e9
         traffic = None
-        if os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as f:
+        tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{H}x{W}_A{A}_E{E}.json")
+        if os.path.exists(tpath):
+            with open(tpath) as f:
                 tj = json.load(f)
             if tj.get("config") == f"{H}x{W}_A{A}_E{E}":
                 traffic = tj.get("hbm_bytes_per_launch")

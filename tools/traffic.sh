@@ -1,6 +1,6 @@
 #!/bin/bash
 # HBM traffic of the step kernel: FETCH_SIZE and WRITE_SIZE in separate rocprofv3
-# passes (kernel trace only), then profiles/traffic_config2.json.
+# passes (kernel trace only), then <outdir>/traffic.json (copy to profiles/traffic_<H>x<W>_A<A>_E<E>.json).
 # Usage: bash tools/traffic.sh <outdir> [bench args]
 set -o pipefail
 OUT=${1:-gpurun_out/traffic}; shift || true

@@ -36,7 +36,9 @@ wk = sum(w) / len(w)
 def arg(name, default):
     return args[args.index(name) + 1] if name in args else default
 
-E = int(arg("--envs", 65536)); S = int(arg("--size", 12)); A = int(arg("--agents", 32))
+cfg = int(arg("--config", 2))
+dS, dA, dE = {2: (12, 32, 65536), 3: (64, 512, 8192)}[cfg]
+E = int(arg("--envs", dE)); S = int(arg("--size", dS)); A = int(arg("--agents", dA))
 alg = E * 2 * (2 * A + 4 * S * S + 4)
 res = {
     "config": f"{S}x{S}_A{A}_E{E}",
