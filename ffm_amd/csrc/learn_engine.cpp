@@ -52,6 +52,7 @@ struct ffm_learner {
     uint32_t t = 0;
     int cur = 0;                       // which DFF buffer is current
     uint8_t* d_map = nullptr;
+    uint32_t* d_map2 = nullptr;              // 2-bit packed map (learn_step.hip map_at)
     void* d_sff = nullptr;
     uint16_t* d_free_cells = nullptr;
     uint16_t* d_pos = nullptr;
@@ -87,11 +88,12 @@ static void free_table(DevTable& T) {
     (void)hipFree(T.t.order);
     (void)hipFree(T.t.n);
     (void)hipFree(T.t.mark);
+    (void)hipFree(T.t.present);
 }
 
 static void release(ffm_learner* l) {
     if (!l) return;
-    void* bufs[] = {l->d_map, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
+    void* bufs[] = {l->d_map, l->d_map2, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
                     l->d_eplog, l->d_eplog_n};
@@ -121,6 +123,7 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     if ((e = hipMalloc((void**)&T.t.order, T.cap * 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.n, 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.mark, 4)) != hipSuccess) return e;
+    if (dense_by && (e = hipMalloc((void**)&T.t.present, T.cap / 8)) != hipSuccess) return e;
     return hipMemset(T.t.mark, 0, 4);
 }
 
@@ -132,6 +135,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.variant = d.variant; a.mode = l->L.mode; a.bs = d.variant == FFM_VARIANT_ACTOR_ONLY ? 5 : l->L.block_size;
     a.D = l->D;
     a.map = l->d_map;
+    a.map2 = l->d_map2;
     a.sff32 = l->f64 ? nullptr : reinterpret_cast<const float*>(l->d_sff);
     a.sff64 = l->f64 ? reinterpret_cast<const double*>(l->d_sff) : nullptr;
     a.smin = l->smin; a.smax = l->smax;
@@ -174,6 +178,7 @@ static int check_overflow(ffm_learner* l, hipStream_t s) {
 static hipError_t clear_table(ffm_learner* l, DevTable& T, double dflt, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(T.t.keys, 0xFF, T.cap * 8, s)) != hipSuccess) return e;
+    if (T.t.present && (e = hipMemsetAsync(T.t.present, 0, T.cap / 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.vals, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.n, 0, 4, s)) != hipSuccess) return e;
@@ -277,6 +282,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         if (he != hipSuccess) return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(he))); \
     } while (0)
     ALLOC(l->d_map, (size_t)HW);
+    ALLOC(l->d_map2, ((size_t)HW + 15) / 16 * 4);
     ALLOC(l->d_sff, (size_t)HW * (l->f64 ? 8 : 4));
     ALLOC(l->d_free_cells, std::max<size_t>(1, fl.size()) * 2);
     ALLOC(l->d_pos, E * A * 2);
@@ -321,6 +327,11 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
                           l->actor || l->trained ? dense_by : 0, dense_n)) != hipSuccess)
         return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
+    if (he == hipSuccess) {
+        std::vector<uint32_t> m2(((size_t)HW + 15) / 16, 0u);
+        for (size_t c = 0; c < (size_t)HW; c++) m2[c >> 4] |= (uint32_t)(d.map[c] & 3) << ((c & 15) * 2);
+        he = hipMemcpy(l->d_map2, m2.data(), m2.size() * 4, hipMemcpyHostToDevice);
+    }
     if (he == hipSuccess) he = hipMemcpy(l->d_sff, d.sff, (size_t)HW * (l->f64 ? 8 : 4), hipMemcpyHostToDevice);
     if (he == hipSuccess && !fl.empty()) he = hipMemcpy(l->d_free_cells, fl.data(), fl.size() * 2, hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemset(l->d_pos, 0xFF, E * A * 2);

@@ -31,6 +31,7 @@ struct LearnTable {
     // Dense layout (ffm_unified's rank keys): slot = ranks | (bx * dense_by + by) << 8,
     // injective, so no probing and never full.  0 = hashed (13-cell keys).
     uint32_t dense_by;
+    uint32_t* present;          // dense: [cap / 32] occupancy bits (lookups hit L2, not the key array)
     uint32_t limit;             // hashed: insertions refused beyond this many keys (7/8 load)
 };
 
@@ -43,6 +44,7 @@ struct LearnArgs {
     int variant, mode, bs;      // bs: block size of the state keys
     int D;                      // decisions per agent: 4 for ffm_actor_only, else 1
     const uint8_t* map;         // [HW] raw map values (0 free, 1/2 blocked, 3 exit)
+    const uint32_t* map2;       // the same, 2 bits per cell (16 KB at 256x256: stays in L1)
     const float* sff32;         // [HW] raw SFF or nullptr
     const double* sff64;        // [HW] (when sff32 == nullptr)
     float smin, smax;           // min/max of the inf->0 SFF (model/ffm_unified.py:425-426)

@@ -77,8 +77,31 @@ __device__ __forceinline__ uint32_t dense_slot(unsigned long long key, uint32_t 
     return (uint32_t)(key & 0xFFu) | ((bx * by_count + by) << 8);
 }
 
+// Next index of T.order for each calling lane: one atomic per wave on the shared
+// counter (inserters of a whole step otherwise serialise on that one word).
+__device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {
+    const unsigned long long m = __ballot(1);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int lane = (int)__lane_id();
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflow) {
-    uint32_t h = T.dense_by ? dense_slot(key, T.dense_by) : (uint32_t)mix64(key) & T.mask;
+    if (T.dense_by) {
+        // The slot is the key: presence is one bit of a 2 MB-scale bitmap that stays
+        // in L2, so a lookup touches no key line (the key is stored for export only).
+        const uint32_t h = dense_slot(key, T.dense_by), bit = 1u << (h & 31);
+        uint32_t* w = T.present + (h >> 5);
+        if (*w & bit) return (int)h;                    // stale 0 only costs the atomic
+        if (atomicOr(w, bit) & bit) return (int)h;
+        T.keys[h] = key;
+        T.order[wave_claim(T.n)] = h;
+        return (int)h;
+    }
+    uint32_t h = (uint32_t)mix64(key) & T.mask;
     for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
         // A plain load may see a slot empty that another CU has just filled; the CAS
         // below then reports the key actually there.  Keys are never removed during
@@ -91,7 +114,7 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
             if (!T.dense_by && __hip_atomic_load(T.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= T.limit) break;
             const unsigned long long old = atomicCAS(&T.keys[h], kEmptyKey, key);
             if (old == kEmptyKey) {
-                const uint32_t idx = atomicAdd(T.n, 1u);
+                const uint32_t idx = wave_claim(T.n);
                 T.order[idx] = h;
                 return (int)h;
             }
@@ -105,7 +128,11 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
 
 // Slot of `key`, or -1 when absent (read-only tables: ffm_trained_core).
 __device__ int tab_find(const LearnTable& T, unsigned long long key) {
-    uint32_t h = T.dense_by ? dense_slot(key, T.dense_by) : (uint32_t)mix64(key) & T.mask;
+    if (T.dense_by) {
+        const uint32_t h = dense_slot(key, T.dense_by);
+        return (T.present[h >> 5] >> (h & 31)) & 1u ? (int)h : -1;
+    }
+    uint32_t h = (uint32_t)mix64(key) & T.mask;
     for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
         const unsigned long long k = T.keys[h];
         if (k == key) return (int)h;
@@ -120,15 +147,25 @@ struct SmArray {                 // exact kernel: explicit state map
     const uint8_t* sm;
     __device__ int operator()(int c) const { return sm[c]; }
 };
+__device__ __forceinline__ int map2_at(const uint32_t* m2, int c) {
+    return (int)((m2[c >> 4] >> ((c & 15) << 1)) & 3u);
+}
 struct SmGrid {                  // batch kernel, current positions: agent grid in LDS
-    const uint8_t* map;
+    const uint32_t* map2;
     const uint16_t* grid;
-    __device__ int operator()(int c) const { return grid[c] != kNone16 ? 1 : map[c]; }
+    __device__ int operator()(int c) const {
+        const int g = grid[c], m = map2_at(map2, c);
+        return g != kNone16 ? 1 : m;
+    }
 };
 struct SmBits {                  // batch kernel, next positions (exit cells excluded)
-    const uint8_t* map;
+    const uint32_t* map2;
     const uint32_t* bits;
-    __device__ int operator()(int c) const { return ((bits[c >> 5] >> (c & 31)) & 1u) ? 1 : map[c]; }
+    __device__ int operator()(int c) const {
+        const uint32_t b = bits[c >> 5];
+        const int m = map2_at(map2, c);
+        return ((b >> (c & 31)) & 1u) ? 1 : m;
+    }
 };
 
 // n / d for 0 <= n < 65536 through m = ceil(2^32 / d): (n * m) >> 32 (checked
@@ -145,39 +182,30 @@ __device__ __forceinline__ unsigned long long pack_key(unsigned long long cells,
 __constant__ int kNBx[4] = {-1, 1, 0, 0};   // U, D, L, R (model/ffm_unified.py:174-175)
 __constant__ int kNBy[4] = {0, 0, -1, 1};
 
-// model/ffm_unified.py:188-269
+// model/ffm_unified.py:188-269.  The rank of direction d from the neighbour n1,
+// the two cells beside n1 (diagonals of the agent) and the cell two ahead n2:
+// 0 blocked / person / off-map at n1, 1 a person on a diagonal, 2 blocked / person
+// / off-map at n2, else 3.  All twelve cells are read first (no load waits on
+// another), then ranked.
 template <class SM>
 __device__ unsigned long long enc_rank(const SM& sm, int H, int W, int x, int y, uint32_t mbs) {
+    auto at = [&](int cx, int cy) {          // -1 off the map
+        const bool in = cx >= 0 && cx < H && cy >= 0 && cy < W;
+        const int v = sm(in ? cx * W + cy : 0);
+        return in ? v : -1;
+    };
+    const int dUL = at(x - 1, y - 1), dUR = at(x - 1, y + 1), dDL = at(x + 1, y - 1), dDR = at(x + 1, y + 1);
+    const int n1[4] = {at(x - 1, y), at(x + 1, y), at(x, y - 1), at(x, y + 1)};
+    const int n2[4] = {at(x - 2, y), at(x + 2, y), at(x, y - 2), at(x, y + 2)};
+    const int da[4] = {dUL, dDL, dUL, dUR}, db[4] = {dUR, dDR, dDL, dDR};
     unsigned long long cells = 0;
 #pragma unroll
     for (int d = 0; d < 4; d++) {
-        const int dx = d == 0 ? -1 : d == 1 ? 1 : 0, dy = d == 2 ? -1 : d == 3 ? 1 : 0;
-        int rank = 3;
-        const int nx1 = x + dx, ny1 = y + dy;
-        if (nx1 >= 0 && nx1 < H && ny1 >= 0 && ny1 < W) {
-            const int v1 = sm(nx1 * W + ny1);
-            if (v1 == 2 || v1 == 1) {
-                rank = 0;
-            } else {
-                const int ax = dx != 0 ? nx1 : nx1 - 1, ay = dx != 0 ? ny1 - 1 : ny1;
-                const int bx = dx != 0 ? nx1 : nx1 + 1, by = dx != 0 ? ny1 + 1 : ny1;
-                bool diag = ax >= 0 && ax < H && ay >= 0 && ay < W && sm(ax * W + ay) == 1;
-                diag = diag || (bx >= 0 && bx < H && by >= 0 && by < W && sm(bx * W + by) == 1);
-                if (diag) {
-                    rank = 1;
-                } else {
-                    const int nx2 = x + 2 * dx, ny2 = y + 2 * dy;
-                    if (nx2 >= 0 && nx2 < H && ny2 >= 0 && ny2 < W) {
-                        const int v2 = sm(nx2 * W + ny2);
-                        if (v2 == 2 || v2 == 1) rank = 2;
-                    } else {
-                        rank = 2;
-                    }
-                }
-            }
-        } else {
-            rank = 0;
-        }
+        int rank;
+        if (n1[d] < 0 || n1[d] == 2 || n1[d] == 1) rank = 0;
+        else if (da[d] == 1 || db[d] == 1) rank = 1;
+        else if (n2[d] < 0 || n2[d] == 2 || n2[d] == 1) rank = 2;
+        else rank = 3;
         cells |= (unsigned long long)rank << (2 * d);
     }
     return pack_key(cells, fdiv(x, mbs), fdiv(y, mbs));
@@ -452,7 +480,7 @@ __device__ __forceinline__ void moves5(const LearnArgs& a, int x, int y, const O
         const int nx = k < 4 ? x + kNBx[k] : x, ny = k < 4 ? y + kNBy[k] : y;
         inb[k] = nx >= 0 && nx < a.H && ny >= 0 && ny < a.W;
         coord[k] = inb[k] ? nx * a.W + ny : x * a.W + y;
-        const int m = inb[k] ? a.map[coord[k]] : 2;
+        const int m = inb[k] ? map2_at(a.map2, coord[k]) : 2;
         valid[k] = inb[k] && (m == 0 || m == 3) && (k == 4 || !occ(coord[k]));
     }
     valid[4] = 1;
@@ -969,6 +997,16 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 #ifndef FFM_LABLATE
 #define FFM_LABLATE 0
 #endif
+// FFM_LSTAMP (diagnostic builds): thread 0 of blocks 0 and gridDim/2 prints the
+// wall-clock ticks (100 MHz) of each phase of the batched step.
+#ifndef FFM_LSTAMP
+#define FFM_LSTAMP 0
+#endif
+#if FFM_LSTAMP
+#define LSTAMP(k) do { __syncthreads(); ts_[k] = wall_clock64(); } while (0)
+#else
+#define LSTAMP(k) do {} while (0)
+#endif
 
 // ===========================================================================
 // Batched step: EPB envs per workgroup, LPE = BS / EPB lanes per env, APT
@@ -1063,6 +1101,10 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
     const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
     float* dff = a.dff_in + (live ? e : 0) * (long long)HW;
+#if FFM_LSTAMP
+    unsigned long long ts_[8];
+#endif
+    LSTAMP(0);
 
     for (int c = tid; c < HW; c += LPE) grid[c] = kNone16;
     for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
@@ -1085,8 +1127,9 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         hs.mx = a.hstat[3];
     }
     __syncthreads();
-    const SmGrid smc{a.map, grid};
+    const SmGrid smc{a.map2, grid};
     auto occ = [&](int c) { return grid[c] != kNone16; };
+    LSTAMP(1);
 
     // ---- decide --------------------------------------------------------------
     unsigned long long skey[APT];
@@ -1102,7 +1145,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         moves5(a, x, y, occ, coord, valid, inb);
         int ex = -1;                               // first exit among the neighbours
 #pragma unroll
-        for (int k = 3; k >= 0; k--) ex = inb[k] && a.map[coord[k]] == 3 ? k : ex;
+        for (int k = 3; k >= 0; k--) ex = inb[k] && map2_at(a.map2, coord[k]) == 3 ? k : ex;
         Policy P;
         if (FFM_LABLATE & 4) {
             req[i * D] = (uint16_t)p[j];
@@ -1114,7 +1157,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             if ((valid[0] | valid[1] | valid[2] | valid[3]) == 0) continue;
             int exv = -1;
 #pragma unroll
-            for (int k = 3; k >= 0; k--) exv = valid[k] && a.map[coord[k]] == 3 ? k : exv;
+            for (int k = 3; k >= 0; k--) exv = valid[k] && map2_at(a.map2, coord[k]) == 3 ? k : exv;
             if (exv >= 0) {
                 wexit[j] = 1;
                 req[i] = (uint16_t)coord[exv];
@@ -1170,6 +1213,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         }
     }
     __syncthreads();
+    LSTAMP(2);
 
     // ---- resolve -----------------------------------------------------------------
     // Requesters of a target stand on it or next to it; a target's owner is its
@@ -1228,12 +1272,13 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
             *c = v;
         }
-        if (a.map[nxt[j]] != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
+        if (map2_at(a.map2, nxt[j]) != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
     }
     __syncthreads();
+    LSTAMP(3);
 
     // ---- learning (TD(0) critic, actor) --------------------------------------------------
-    const SmBits smn{a.map, bits};
+    const SmBits smn{a.map2, bits};
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;
@@ -1265,18 +1310,20 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         }
     }
 
+    LSTAMP(4);
     // ---- exit removal (order preserving), counters ---------------------------------------
     int base_ = 0;
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;
-        const bool keep = i < n && a.map[nxt[j]] != 3;
+        const bool keep = i < n && map2_at(a.map2, nxt[j]) != 3;
         int tot;
         const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
         if (keep) a.pos[e * A + base_ + off] = (uint16_t)nxt[j];
         base_ += tot;
     }
     __syncthreads();     // deposits visible to the whole workgroup before the stencil
+    LSTAMP(5);
 
     // ---- update_dff (model/ffm_unified.py:779-798) into the other buffer ---------------------
     if (live && !(FFM_LABLATE & 8)) {
@@ -1294,6 +1341,13 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             out[c] = acc < 1e-4f ? 0.0f : acc;
         }
     }
+    LSTAMP(6);
+#if FFM_LSTAMP
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        printf("LSTAMP blk %d init %llu decide %llu resolve %llu learn %llu compact %llu stencil %llu\n", (int)blockIdx.x,
+               ts_[1] - ts_[0], ts_[2] - ts_[1], ts_[3] - ts_[2], ts_[4] - ts_[3], ts_[5] - ts_[4], ts_[6] - ts_[5]);
+
+#endif
     if (live && tid == 0) {
         a.cnt[e] = base_;
         a.nstart[e] = n;

@@ -10,6 +10,6 @@ masks = [int(x) for x in sys.argv[1:]] or [0, 1, 2, 4, 6, 8]
 root = os.path.join(os.path.dirname(B.HERE), "build_abl")
 os.makedirs(root, exist_ok=True)
 with ThreadPoolExecutor(3) as ex:
-    list(ex.map(lambda m: B.build(out=os.path.join(root, f"libffm_amd_labl{m}.so"), defines=[f"FFM_LABLATE={m}"]),
+    list(ex.map(lambda m: B.build(out=os.path.join(root, f"libffm_amd_labl{m}.so"), defines=[f"FFM_LABLATE={m}"] + os.environ.get("FFM_EXTRA_DEFINES", "").split()),
                 masks))
 print("built", masks)
