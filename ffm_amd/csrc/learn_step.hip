@@ -1067,12 +1067,15 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 // the map, SFF and DFF in LDS as well measured slower at config 4, 324 vs 295 us:
 // they are L1/L2 hits, and the staging delays every short-lived workgroup.)
 struct BatchCarve {
-    size_t grid, bits, req, ws, total;     // per env
-    size_t shared;                          // per block: EPB env regions
+    size_t dff, grid, bits, req, ws, total;  // per env
+    size_t shared;                           // per block: EPB env regions
 };
-__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB) {
+// DL: the env's DFF is staged in LDS (small maps): the policy's reads, the
+// deposits and the stencil stay on chip; only the stencil's output goes to HBM.
+__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB, bool DL = false) {
     BatchCarve c;
     size_t o = 0;
+    c.dff = o; o += DL ? align16((size_t)HW * 4) : 0;
     c.grid = o; o += align16((size_t)HW * 2);
     c.bits = o; o += align16((size_t)((HW + 31) / 32) * 4);
     c.req = o; o += align16((size_t)A * D * 2);
@@ -1082,12 +1085,12 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB)
     return c;
 }
 
-template <int BS, int EPB, int APT, int D>
+template <int BS, int EPB, int APT, int D, bool DL>
 __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LPE = BS / EPB;
     const int H = a.H, W = a.W, HW = a.HW, A = a.A;
-    const BatchCarve cv = batch_carve(HW, A, D, EPB);
+    const BatchCarve cv = batch_carve(HW, A, D, EPB, DL);
     const int sub = threadIdx.x / LPE, tid = threadIdx.x % LPE;
     unsigned char* base = smem + (size_t)sub * cv.total;
     uint16_t* grid = reinterpret_cast<uint16_t*>(base + cv.grid);
@@ -1100,13 +1103,17 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     const int n = live ? a.cnt[e] : 0;
     const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
     const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
-    float* dff = a.dff_in + (live ? e : 0) * (long long)HW;
+    float* dff = DL ? reinterpret_cast<float*>(base + cv.dff) : a.dff_in + (live ? e : 0) * (long long)HW;
 #if FFM_LSTAMP
     unsigned long long ts_[8];
 #endif
     LSTAMP(0);
 
     for (int c = tid; c < HW; c += LPE) grid[c] = kNone16;
+    if (DL) {
+        const float* src = a.dff_in + (live ? e : 0) * (long long)HW;
+        for (int c = tid; c < HW; c += LPE) dff[c] = src[c];
+    }
     for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
     for (int c = tid; c < A * D; c += LPE) req[c] = kNone16;
     __syncthreads();
@@ -1648,31 +1655,41 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
     *T.mark = *T.n;
 }
 
-template <int BS, int EPB, int APT, int D>
+template <int BS, int EPB, int APT, int D, bool DL>
 hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
-    const size_t smem = batch_carve(a.HW, a.A, D, EPB).shared;
+    const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D>),
+            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D, DL>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
     const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
-    learn_batch_kernel<BS, EPB, APT, D><<<dim3(blocks), dim3(BS), smem, s>>>(a);
+    learn_batch_kernel<BS, EPB, APT, D, DL><<<dim3(blocks), dim3(BS), smem, s>>>(a);
     return hipGetLastError();
 }
 
+// One agent per lane when A <= 1024; beyond that APT agents per lane of a
+// 1024-lane block.  The DFF goes to LDS when it fits beside the rest (DL).
 template <int D>
 hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
-    const int A = a.A;
-    if (A <= 32 && batch_carve(a.HW, A, D, 2).shared <= 64 * 1024) return launch_batch_t<64, 2, 1, D>(a, s);
-    if (A <= 64) return launch_batch_t<64, 1, 1, D>(a, s);
-    if (A <= 256) return launch_batch_t<256, 1, 1, D>(a, s);
-    if (A <= 1024) return launch_batch_t<1024, 1, 1, D>(a, s);
-    if (A <= 2048) return launch_batch_t<1024, 1, 2, D>(a, s);
-    if (A <= 4096) return launch_batch_t<1024, 1, 4, D>(a, s);
-    if (A <= 8192) return launch_batch_t<1024, 1, 8, D>(a, s);
-    return launch_batch_t<1024, 1, 16, D>(a, s);
+    const int A = a.A, HW = a.HW;
+    constexpr size_t kLds = 64 * 1024;
+    if (A <= 32 && batch_carve(HW, A, D, 2, true).shared <= kLds) return launch_batch_t<64, 2, 1, D, true>(a, s);
+    if (A <= 32 && batch_carve(HW, A, D, 2).shared <= kLds) return launch_batch_t<64, 2, 1, D, false>(a, s);
+    if (A <= 64) {
+        if (batch_carve(HW, A, D, 1, true).shared <= kLds) return launch_batch_t<64, 1, 1, D, true>(a, s);
+        return launch_batch_t<64, 1, 1, D, false>(a, s);
+    }
+    if (A <= 256) {
+        if (batch_carve(HW, A, D, 1, true).shared <= kLds) return launch_batch_t<256, 1, 1, D, true>(a, s);
+        return launch_batch_t<256, 1, 1, D, false>(a, s);
+    }
+    if (A <= 1024) return launch_batch_t<1024, 1, 1, D, false>(a, s);
+    if (A <= 2048) return launch_batch_t<1024, 1, 2, D, false>(a, s);
+    if (A <= 4096) return launch_batch_t<1024, 1, 4, D, false>(a, s);
+    if (A <= 8192) return launch_batch_t<1024, 1, 8, D, false>(a, s);
+    return launch_batch_t<1024, 1, 16, D, false>(a, s);
 }
 
 }  // namespace
