@@ -82,8 +82,7 @@ struct ffm_learner {
 };
 
 static void free_table(DevTable& T) {
-    (void)hipFree(T.t.keys);
-    (void)hipFree(T.t.vals);
+    (void)hipFree(T.t.rec);
     (void)hipFree(T.t.acc);
     (void)hipFree(T.t.order);
     (void)hipFree(T.t.n);
@@ -117,8 +116,8 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     T.t.dense_by = dense_by;
     T.t.limit = (uint32_t)(T.cap - T.cap / 8);
     hipError_t e;
-    if ((e = hipMalloc((void**)&T.t.keys, T.cap * 8)) != hipSuccess) return e;
-    if ((e = hipMalloc((void**)&T.t.vals, T.cap * width * 8)) != hipSuccess) return e;
+    T.t.stride = width == 1 ? 2 : 8;        // 16 B / 64 B records (key + values [+ pad])
+    if ((e = hipMalloc((void**)&T.t.rec, T.cap * T.t.stride * 8)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.acc, T.cap * width * 8)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.order, T.cap * 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.n, 4)) != hipSuccess) return e;
@@ -177,18 +176,12 @@ static int check_overflow(ffm_learner* l, hipStream_t s) {
 
 static hipError_t clear_table(ffm_learner* l, DevTable& T, double dflt, hipStream_t s) {
     hipError_t e;
-    if ((e = hipMemsetAsync(T.t.keys, 0xFF, T.cap * 8, s)) != hipSuccess) return e;
+    (void)l;
     if (T.t.present && (e = hipMemsetAsync(T.t.present, 0, T.cap / 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(T.t.vals, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.n, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.mark, 0, 4, s)) != hipSuccess) return e;
-    if (T.width == 1 && dflt != 0.0) {
-        ffm::LearnArgs a = make_args(l);
-        a.v_default = dflt;
-        return ffm::launch_learn_fill_default(a, s);
-    }
-    return hipSuccess;
+    return ffm::launch_learn_clear(T.t, T.width, T.width == 1 ? dflt : 0.0, s);
 }
 
 extern "C" {
@@ -648,16 +641,15 @@ int ffm_learner_export_table(ffm_learner* l, int32_t which, uint64_t* keys, doub
     if ((int64_t)cnt > cap) return fail(FFM_E_INVALID, "export buffer too small");
     if (cnt == 0) return FFM_OK;
     std::vector<uint32_t> order(cnt);
-    std::vector<unsigned long long> k(T->cap);
-    std::vector<double> v(T->cap * T->width);
+    const size_t st = T->t.stride;
+    std::vector<unsigned long long> rec(T->cap * st);
     HIP_TRY(hipMemcpyAsync(order.data(), T->t.order, (size_t)cnt * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(k.data(), T->t.keys, T->cap * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(v.data(), T->t.vals, T->cap * T->width * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(rec.data(), T->t.rec, T->cap * st * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     for (uint32_t i = 0; i < cnt; i++) {
         const size_t slot = order[i];
-        if (keys) keys[i] = k[slot];
-        if (vals) std::memcpy(vals + (size_t)i * T->width, v.data() + slot * T->width, 8 * (size_t)T->width);
+        if (keys) keys[i] = rec[slot * st];
+        if (vals) std::memcpy(vals + (size_t)i * T->width, rec.data() + slot * st + 1, 8 * (size_t)T->width);
     }
     return FFM_OK;
 }

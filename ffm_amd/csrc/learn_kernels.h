@@ -21,8 +21,11 @@ struct LearnRec {
 };
 
 struct LearnTable {
-    unsigned long long* keys;   // [cap], ~0 = empty
-    double* vals;               // [cap * width]; empty slots hold the default
+    // [cap][stride] 64-bit words, one record per slot: the key (~0 = empty), then
+    // its `width` values (empty slots hold the default).  A lookup's probe and the
+    // values it then reads share one line: 16 B records for V, 64 B for H.
+    unsigned long long* rec;
+    uint32_t stride;
     long long* acc;             // [cap * width] fixed-point (2^-32) increments of the batched step
     uint32_t* order;            // [cap] slot of the i-th inserted key
     uint32_t* n;                // [1] keys inserted
@@ -93,6 +96,7 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_clear(const LearnTable& T, int width, double dflt, hipStream_t s);
 hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
                                     long long cap, unsigned long long* count, hipStream_t s);
 hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsigned long long* keys,

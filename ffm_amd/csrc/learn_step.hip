@@ -29,6 +29,11 @@ constexpr unsigned long long kEmptyKey = ~0ull;
 constexpr double kFxOne = 4294967296.0;
 constexpr uint16_t kNone16 = 0xFFFF;
 
+__device__ __forceinline__ unsigned long long& tkey(const LearnTable& T, size_t h) { return T.rec[h * T.stride]; }
+__device__ __forceinline__ double* tval(const LearnTable& T, size_t h) {
+    return reinterpret_cast<double*>(T.rec + h * T.stride + 1);
+}
+
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
     z ^= z >> 33; z *= 0xff51afd7ed558ccdULL;
     z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ULL;
@@ -97,7 +102,7 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
         uint32_t* w = T.present + (h >> 5);
         if (*w & bit) return (int)h;                    // stale 0 only costs the atomic
         if (atomicOr(w, bit) & bit) return (int)h;
-        T.keys[h] = key;
+        tkey(T, h) = key;
         T.order[wave_claim(T.n)] = h;
         return (int)h;
     }
@@ -106,13 +111,13 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
         // A plain load may see a slot empty that another CU has just filled; the CAS
         // below then reports the key actually there.  Keys are never removed during
         // a step, so a non-empty value read is never stale.
-        const unsigned long long k = T.keys[h];
+        const unsigned long long k = tkey(T, h);
         if (k == key) return (int)h;
         if (k == kEmptyKey) {
             // A hashed table past 7/8 load refuses new keys (probe chains would grow
             // without bound); the host reports FFM_E_NOMEM.
             if (!T.dense_by && __hip_atomic_load(T.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= T.limit) break;
-            const unsigned long long old = atomicCAS(&T.keys[h], kEmptyKey, key);
+            const unsigned long long old = atomicCAS(&tkey(T, h), kEmptyKey, key);
             if (old == kEmptyKey) {
                 const uint32_t idx = wave_claim(T.n);
                 T.order[idx] = h;
@@ -134,7 +139,7 @@ __device__ int tab_find(const LearnTable& T, unsigned long long key) {
     }
     uint32_t h = (uint32_t)mix64(key) & T.mask;
     for (uint32_t probe = 0; probe < kMaxProbe; probe++) {
-        const unsigned long long k = T.keys[h];
+        const unsigned long long k = tkey(T, h);
         if (k == key) return (int)h;
         if (k == kEmptyKey) return -1;
         h = (h + 1) & T.mask;
@@ -509,7 +514,7 @@ __device__ void h_stats_seq(const LearnArgs& a, HStat& hs) {
     hs.mn = __builtin_inf();
     hs.mx = -__builtin_inf();
     for (uint32_t i = 0; i < n; i++) {
-        const double* v = a.Ht.vals + (size_t)a.Ht.order[i] * 5;
+        const double* v = tval(a.Ht, a.Ht.order[i]);
         for (int k = 0; k < 5; k++) {
             if (!__builtin_isfinite(v[k])) hs.nonfinite = 1;
             hs.mn = v[k] < hs.mn ? v[k] : hs.mn;
@@ -731,7 +736,7 @@ __device__ __forceinline__ void trained_policy(const LearnArgs& a, int hslot, co
     float h[5], score[5], e[5];
     double p[5];
 #pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = hslot >= 0 ? (float)a.Ht.vals[(size_t)hslot * 5 + k] : 0.0f;
+    for (int k = 0; k < 5; k++) h[k] = hslot >= 0 ? (float)tval(a.Ht, hslot)[k] : 0.0f;
     if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
         const float hmax = (float)hs.mx, den = (float)(hs.mx - hs.mn);
         const float srange = (float)((double)a.smax - (double)a.smin), smin = a.smin;
@@ -883,7 +888,7 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                         hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
                         hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
                     }
-                    k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, false, rng);
+                    k = actor_choose(a, tval(a.Ht, hsl), coord, valid, dff, hs, false, rng);
                 }
                 S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
                 S.act[i] = k; S.avalid[i] = valid[k];
@@ -905,7 +910,7 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                             hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
                             hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
                         }
-                        k = actor_choose(a, a.Ht.vals + (size_t)hsl * 5, coord, valid, dff, hs, true, rng);
+                        k = actor_choose(a, tval(a.Ht, hsl), coord, valid, dff, hs, true, rng);
                     }
                     S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
                     S.act[i] = k; S.avalid[i] = valid[k];
@@ -944,14 +949,14 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
             if (!S.wexit[i]) {
                 const int sn = tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow);
                 if (sn < 0) return;
-                vn = a.V.vals[sn];
+                vn = tval(a.V, sn)[0];
             }
             const int sv = tab_get(a.V, S.skey[i], a.overflow);
             if (sv < 0) return;
-            const double v = a.V.vals[sv];
+            const double v = tval(a.V, sv)[0];
             const double td = (r + a.gamma * vn) - v;
             S.td[i] = td;
-            a.V.vals[sv] = v + a.alpha_v * td;
+            tval(a.V, sv)[0] = v + a.alpha_v * td;
         }
         if (post_update) {        // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
             for (int i = 0; i < n; i++) {
@@ -960,8 +965,8 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                 if (S.coll[i] >= 0) r = r + (double)S.coll[i] * a.collision_penalty;
                 double vn = 0.0;
                 if (!S.wexit[i])
-                    vn = a.V.vals[tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow)];
-                const double v = a.V.vals[tab_get(a.V, S.skey[i], a.overflow)];
+                    vn = tval(a.V, tab_get(a.V, encode(a, SmArray{S.smn}, S.nxt[i] / W, S.nxt[i] % W), a.overflow))[0];
+                const double v = tval(a.V, tab_get(a.V, S.skey[i], a.overflow))[0];
                 S.td[i] = (r + a.gamma * vn) - v;
             }
         }
@@ -971,7 +976,7 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                 const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);    // :769-773
                 if (hsl < 0) return;
                 if (!S.avalid[i]) continue;
-                double* hv = a.Ht.vals + (size_t)hsl * 5 + S.act[i];
+                double* hv = tval(a.Ht, hsl) + S.act[i];
                 *hv = *hv + a.alpha_h * S.td[i];
             }
         }
@@ -1189,7 +1194,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                 } else {
                     hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
                     if (hsl[j] < 0) continue;
-                    actor_policy(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, false, P);
+                    actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, false, P);
                 }
                 DrawPh rng(a, genv, (uint32_t)i);
                 k = policy_draw(P, eps, rng);
@@ -1202,7 +1207,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             if (ex != 0) {
                 hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
                 if (hsl[j] < 0) continue;
-                actor_policy(a, a.Ht.vals + (size_t)hsl[j] * 5, coord, valid, dff, hs, true, P);
+                actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, true, P);
             }
             int k = 4;
 #pragma unroll
@@ -1298,11 +1303,11 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         if (!wexit[j]) {
             const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
             sn = tab_get(a.V, encode(a, smn, nx, ny), a.overflow);
-            vn = sn >= 0 ? a.V.vals[sn] : 0.0;
+            vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
         }
         const int sv = tab_get(a.V, skey[j], a.overflow);
         if (sv < 0) continue;
-        const double td = (r + a.gamma * vn) - a.V.vals[sv];
+        const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
         if (!(FFM_LABLATE & 1)) acc_add(a.V.acc + sv, fx(a.alpha_v * td));
         if (!actor) continue;
         if (act[j] < 0) continue;
@@ -1404,7 +1409,7 @@ __global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const double* v = a.Ht.vals + (size_t)a.Ht.order[i] * 5;
+        const double* v = tval(a.Ht, a.Ht.order[i]);
 #pragma unroll
         for (int k = 0; k < 5; k++) {
             nf |= !__builtin_isfinite(v[k]);
@@ -1448,14 +1453,16 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const size_t s = (size_t)T.order[i] * WIDTH;
+        const uint32_t slot = T.order[i];
+        const size_t s = (size_t)slot * WIDTH;
+        double* vp = tval(T, slot);
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
             const long long q = T.acc[s + k];
-            double v = T.vals[s + k];
+            double v = vp[k];
             if (q != 0) {
                 v = v + (double)q * (1.0 / kFxOne);
-                T.vals[s + k] = v;
+                vp[k] = v;
                 T.acc[s + k] = 0;
             }
             if (STATS) {
@@ -1478,14 +1485,25 @@ __global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
     if (i >= a.nstart[e]) return;
     const LearnRec rc = a.recs[g];
     if (rc.k < 0) return;
-    const double vn = rc.snv >= 0 ? a.V.vals[rc.snv] : 0.0;
-    const double td = (rc.r + a.gamma * vn) - a.V.vals[rc.sv];
+    const double vn = rc.snv >= 0 ? tval(a.V, rc.snv)[0] : 0.0;
+    const double td = (rc.r + a.gamma * vn) - tval(a.V, rc.sv)[0];
     acc_add(a.Ht.acc + (size_t)rc.hslot * 5 + rc.k, fx(a.alpha_h * td));
 }
 
 __global__ __launch_bounds__(256) void learn_fill_default_kernel(LearnTable T, double v) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i <= T.mask; i += (size_t)gridDim.x * 256)
-        if (T.keys[i] == kEmptyKey) T.vals[i] = v;
+        if (tkey(T, i) == kEmptyKey) tval(T, i)[0] = v;
+}
+
+// Every record empty: key ~0, `width` values `v` (the default), padding zero.
+__global__ __launch_bounds__(256) void learn_clear_kernel(LearnTable T, int width, double v) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i <= T.mask; i += (size_t)gridDim.x * 256) {
+        unsigned long long* r = T.rec + i * T.stride;
+        r[0] = kEmptyKey;
+        for (uint32_t k = 1; k < T.stride; k++) r[k] = 0ull;
+        double* vp = reinterpret_cast<double*>(r + 1);
+        for (int k = 0; k < width; k++) vp[k] = v;
+    }
 }
 
 // Philox placement: the N free cells with the smallest
@@ -1576,7 +1594,7 @@ __global__ __launch_bounds__(256) void learn_delta_export_kernel(LearnTable T, u
         if (!touched) continue;
         const unsigned long long r = atomicAdd(count, 1ull);
         if ((long long)r >= cap) continue;
-        keys[r] = T.keys[s];
+        keys[r] = tkey(T, s);
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) acc[r * WIDTH + k] = q[k];
     }
@@ -1650,7 +1668,7 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
     for (long long i = 0; i < n; i++) {
         const int s = tab_get(T, keys[i], overflow);
         if (s < 0) break;
-        for (int k = 0; k < width; k++) T.vals[(size_t)s * width + k] = vals[i * width + k];
+        for (int k = 0; k < width; k++) tval(T, s)[k] = vals[i * width + k];
     }
     *T.mark = *T.n;
 }
@@ -1770,6 +1788,11 @@ hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsign
 hipError_t launch_learn_import(const LearnTable& T, int width, const unsigned long long* keys, const double* vals,
                               long long n, int* overflow, hipStream_t s) {
     learn_import_kernel<<<dim3(1), dim3(64), 0, s>>>(T, width, keys, vals, n, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_clear(const LearnTable& T, int width, double dflt, hipStream_t s) {
+    learn_clear_kernel<<<dim3(2048), dim3(256), 0, s>>>(T, width, dflt);
     return hipGetLastError();
 }
 
