@@ -1,11 +1,12 @@
 #!/bin/bash
-# A/B timing of two library builds, interleaved (GPU box): bash tools/ab.sh libA.so libB.so [bench args...]
+# A/B timing of library builds, interleaved (GPU box):
+#   bash tools/ab.sh "libA.so libB.so ..." [bench args...]
 set -o pipefail
 export TMPDIR=/tmp
-A=$1; B=$2; shift 2
+LIBS=$1; shift
 for r in 1 2 3; do
-  for f in $A $B; do
-    v=$(FFM_LIB_PATH=$PWD/$f timeout -k 10 120 python3 bench.py --no-cpu "$@" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['step_ms_events']*1000,1), 'us')") || exit 1
+  for f in $LIBS; do
+    v=$(FFM_LIB_PATH=$PWD/$f timeout -k 10 120 python3 bench.py --no-cpu "$@" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['step_ms_events']*1000,1), 'us')") || exit 1
     echo "$(basename $f .so) $v"
   done
 done
