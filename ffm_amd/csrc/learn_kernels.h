@@ -83,7 +83,7 @@ struct LearnArgs {
     long long eplog_cap;
 };
 
-constexpr int kHstatBlocks = 512;
+constexpr int kHstatBlocks = 2048;
 
 size_t learn_exact_scratch_bytes(int HW, int A);
 int learn_batch_block_size(int A);

@@ -1475,6 +1475,38 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
     if (STATS) hstat_block_reduce(mn, mx, nf, n, hpart);
 }
 
+// Dense tables: the same pass in slot order over the presence bitmap.  Most
+// slots of a long run are present, so streaming the records beats gathering
+// them through the insertion order; min / max / non-finite do not depend on order.
+template <int WIDTH, bool STATS>
+__global__ __launch_bounds__(256) void learn_apply_dense_kernel(LearnTable T, double* hpart) {
+    const uint32_t n = *T.n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *T.mark = n;
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    int nf = 0;
+    for (size_t slot = (size_t)blockIdx.x * 256 + threadIdx.x; slot <= T.mask; slot += (size_t)gridDim.x * 256) {
+        if (!((T.present[slot >> 5] >> (slot & 31)) & 1u)) continue;
+        const size_t s = slot * WIDTH;
+        double* vp = tval(T, slot);
+#pragma unroll
+        for (int k = 0; k < WIDTH; k++) {
+            const long long q = T.acc[s + k];
+            double v = vp[k];
+            if (q != 0) {
+                v = v + (double)q * (1.0 / kFxOne);
+                vp[k] = v;
+                T.acc[s + k] = 0;
+            }
+            if (STATS) {
+                nf |= !__builtin_isfinite(v);
+                mn = v < mn ? v : mn;
+                mx = v > mx ? v : mx;
+            }
+        }
+    }
+    if (STATS) hstat_block_reduce(mn, mx, nf, n, hpart);
+}
+
 // _get_td_errors with the updated V, then the actor (model/ffm_unified.py:559-598).
 // One lane per (env, agent) slot.
 __global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
@@ -1738,9 +1770,13 @@ hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s) {
-    if (v) learn_apply_kernel<1, false><<<dim3(512), dim3(256), 0, s>>>(a.V, nullptr);
+    if (v) {
+        if (a.V.dense_by) learn_apply_dense_kernel<1, false><<<dim3(2048), dim3(256), 0, s>>>(a.V, nullptr);
+        else learn_apply_kernel<1, false><<<dim3(512), dim3(256), 0, s>>>(a.V, nullptr);
+    }
     if (h) {     // H increments + the next step's statistics
-        learn_apply_kernel<5, true><<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        if (a.Ht.dense_by) learn_apply_dense_kernel<5, true><<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        else learn_apply_kernel<5, true><<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a.Ht, a.hpart);
         learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a);
     }
     return hipGetLastError();
