@@ -999,6 +999,9 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 // Diagnostic builds only (tools/learn_ablate.sh): FFM_LABLATE bits drop parts of the
 // batched step to time them.  1: table increments, 2: learning phase,
 // 4: policy (agents stay; no H lookup), 8: DFF stencil.
+#ifndef FFM_SMALL_EPB
+#define FFM_SMALL_EPB 8
+#endif
 #ifndef FFM_LABLATE
 #define FFM_LABLATE 0
 #endif
@@ -1725,7 +1728,10 @@ template <int D>
 hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
     const int A = a.A, HW = a.HW;
     constexpr size_t kLds = 64 * 1024;
-    if (A <= 32 && batch_carve(HW, A, D, 2, true).shared <= kLds) return launch_batch_t<64, 2, 1, D, true>(a, s);
+    // 32-lane envs: FFM_SMALL_EPB of them per workgroup (a CU holds a limited
+    // number of workgroups; one-wave workgroups would leave most of its wave slots idle)
+    if (A <= 32 && batch_carve(HW, A, D, FFM_SMALL_EPB, true).shared <= kLds)
+        return launch_batch_t<32 * FFM_SMALL_EPB, FFM_SMALL_EPB, 1, D, true>(a, s);
     if (A <= 32 && batch_carve(HW, A, D, 2).shared <= kLds) return launch_batch_t<64, 2, 1, D, false>(a, s);
     if (A <= 64) {
         if (batch_carve(HW, A, D, 1, true).shared <= kLds) return launch_batch_t<64, 1, 1, D, true>(a, s);
