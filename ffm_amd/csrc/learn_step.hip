@@ -1423,10 +1423,10 @@ __global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
     hstat_block_reduce(mn, mx, nf, n, a.hpart);
 }
 
-__global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a) {
+__global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a, int nb) {
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
-    for (int b = threadIdx.x; b < kHstatBlocks; b += 64) {
+    for (int b = threadIdx.x; b < nb; b += 64) {
         const double* o = a.hpart + b * 4;
         mn = o[2] < mn ? o[2] : mn;
         mx = o[3] > mx ? o[3] : mx;
@@ -1762,7 +1762,7 @@ bool learn_batch_supported(int HW, int A, int D) {
 
 hipError_t launch_learn_hstat(const LearnArgs& a, hipStream_t s) {
     learn_hstat_partial<<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a);
-    learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a);
+    learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, kHstatBlocks);
     return hipGetLastError();
 }
 
@@ -1781,9 +1781,12 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
         else learn_apply_kernel<1, false><<<dim3(512), dim3(256), 0, s>>>(a.V, nullptr);
     }
     if (h) {     // H increments + the next step's statistics
-        if (a.Ht.dense_by) learn_apply_dense_kernel<5, true><<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a.Ht, a.hpart);
-        else learn_apply_kernel<5, true><<<dim3(kHstatBlocks), dim3(256), 0, s>>>(a.Ht, a.hpart);
-        learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a);
+        // dense: a streaming pass over every slot wants the whole chip; hashed: the
+        // insertion-order pass over n entries needs far fewer partials
+        const int nb = a.Ht.dense_by ? kHstatBlocks : kHstatBlocks / 4;
+        if (a.Ht.dense_by) learn_apply_dense_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        else learn_apply_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, nb);
     }
     return hipGetLastError();
 }
