@@ -83,8 +83,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # FFM_BENCH_REHEARSE=1 (diagnostic): every rank on cuda:0 over gloo, to rehearse
+        # the multi-rank path on a one-GPU box; the real runs use RCCL, one GPU per rank.
+        if os.environ.get("FFM_BENCH_REHEARSE") == "1":
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
 
@@ -268,7 +274,8 @@ def bench_learner(args, world, rank, torch, dist):
     if world > 1:
         from ffm_amd.dist import reduce_counters, reduce_max
         elapsed = reduce_max(elapsed, device="cuda")
-        agent_steps = reduce_counters({"agent_steps": agent_steps}, device="cuda")["agent_steps"]
+        d = {k: c1[k] - c0[k] for k in ("agent_steps", "exits", "resets", "steps")}
+        agent_steps = reduce_counters(d, device="cuda")["agent_steps"]
     if rank == 0:
         D = 4 if cfg["variant"] == "actor_only" else 1
         bpe = learner_bytes_per_env_step(H, W, A, D)
