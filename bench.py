@@ -280,6 +280,14 @@ def bench_learner(args, world, rank, torch, dist):
         D = 4 if cfg["variant"] == "actor_only" else 1
         bpe = learner_bytes_per_env_step(H, W, A, D)
         achieved = E * bpe / (step_ms / 1e3) / 1e9
+        # PMC HBM bytes of the batch kernel (tools/traffic.sh <out> --config 4|5)
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", f"traffic_{H}x{W}_A{A}_E{E}_learn{args.config}.json")
+        if os.path.exists(tpath):
+            with open(tpath) as f:
+                tj = json.load(f)
+            if tj.get("config") == f"{H}x{W}_A{A}_E{E}_learn{args.config}":
+                traffic = tj.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC, "value": agent_steps / elapsed, "unit": "agent-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -297,7 +305,8 @@ def bench_learner(args, world, rank, torch, dist):
             "step_ms_events": step_ms,
             "tables": {"V": v_size, "H": h_size},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "traffic_kernel": "learn_batch_kernel (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "bytes_per_launch_algorithmic": E * bpe,
                          "note": "whole learning step (all kernels) timed with HIP events"},
             "cpu_baseline": None,

@@ -1,4 +1,5 @@
-"""Per-launch HBM bytes of the step kernel from the two PMC passes of tools/traffic.sh.
+"""Per-launch HBM bytes of the step kernel (configs 2, 3) or of the learner's batch
+kernel (configs 4, 5) from the two PMC passes of tools/traffic.sh.
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md,
 HBM/rocprofv3 section): FETCH_SIZE counts 128-B streaming requests at 64 B, so
@@ -13,6 +14,14 @@ out = sys.argv[1]
 args = sys.argv[2:]
 
 
+def arg(name, default):
+    return args[args.index(name) + 1] if name in args else default
+
+
+cfg = int(arg("--config", 2))
+KERNELS = ("learn_batch_kernel",) if cfg in (4, 5) else ("core_wave_kernel", "core_block_kernel")
+
+
 def per_dispatch(path, counter):
     vals = []
     for root, _, files in os.walk(path):
@@ -20,7 +29,7 @@ def per_dispatch(path, counter):
             if f.endswith("counter_collection.csv"):
                 with open(os.path.join(root, f)) as fh:
                     for r in csv.DictReader(fh):
-                        if "core_wave_kernel" in r["Kernel_Name"] or "core_block_kernel" in r["Kernel_Name"]:
+                        if any(k in r["Kernel_Name"] for k in KERNELS):
                             if r["Counter_Name"] == counter:
                                 vals.append(float(r["Counter_Value"]))
     return vals
@@ -33,15 +42,13 @@ w = w[10:] or w
 fk = sum(f) / len(f)
 wk = sum(w) / len(w)
 
-def arg(name, default):
-    return args[args.index(name) + 1] if name in args else default
-
-cfg = int(arg("--config", 2))
-dS, dA, dE = {2: (12, 32, 65536), 3: (64, 512, 8192)}[cfg]
+dS, dA, dE = {2: (12, 32, 65536), 3: (64, 512, 8192), 4: (12, 32, 65536), 5: (256, 8192, 512)}[cfg]
 E = int(arg("--envs", dE)); S = int(arg("--size", dS)); A = int(arg("--agents", dA))
 alg = E * 2 * (2 * A + 4 * S * S + 4)
+if cfg in (4, 5):      # bench.py learner_bytes_per_env_step
+    alg += E * A * (2 * 16 + 16 + (8 + 40 + 16))
 res = {
-    "config": f"{S}x{S}_A{A}_E{E}",
+    "config": f"{S}x{S}_A{A}_E{E}" + (f"_learn{cfg}" if cfg in (4, 5) else ""),
     "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
     "fetch_size_kib_raw": fk, "write_size_kib_raw": wk,
     "read_bytes_corrected": 2 * fk * 1024, "write_bytes": wk * 1024,
