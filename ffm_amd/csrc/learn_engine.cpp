@@ -103,7 +103,7 @@ static void release(ffm_learner* l) {
 }
 
 // dense_by > 0: ffm_unified's rank keys map injectively onto
-// ranks | (bx * dense_by + by) << 8 (learn_step.hip dense_slot); the capacity is
+// ranks * (cap / 256) + bx * dense_by + by (learn_step.hip dense_slot); the capacity is
 // the next power of two >= 256 * Bx * By and the table can never fill.
 static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dense_by = 0, size_t dense_n = 0) {
     T.width = width;

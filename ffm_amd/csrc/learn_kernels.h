@@ -31,7 +31,7 @@ struct LearnTable {
     uint32_t* n;                // [1] keys inserted
     uint32_t* mark;             // [1] n at the start of the current batched step (delta export)
     uint32_t mask;              // cap - 1
-    // Dense layout (ffm_unified's rank keys): slot = ranks | (bx * dense_by + by) << 8,
+    // Dense layout (ffm_unified's rank keys): slot = ranks * (cap / 256) + bx * dense_by + by,
     // injective, so no probing and never full.  0 = hashed (13-cell keys).
     uint32_t dense_by;
     uint32_t* present;          // dense: [cap / 32] occupancy bits (lookups hit L2, not the key array)

@@ -77,9 +77,12 @@ __device__ __forceinline__ void acc_add(long long* p, long long q) {
 // Slot of `key`, inserting it when absent (a defaultdict read inserts,
 // model/ffm_unified.py:658).  Empty slots already hold the default value, so
 // an inserter never has to publish a value.  -1 only when the table is full.
-__device__ __forceinline__ uint32_t dense_slot(unsigned long long key, uint32_t by_count) {
+// Dense slot of a rank key, rank-major: the records of one rank pattern lie in
+// block order, so agents in neighbouring blocks with the same pattern share lines
+// (C5: 2.33 -> 2.17 ms per step against block-major).
+__device__ __forceinline__ uint32_t dense_slot(unsigned long long key, const LearnTable& T) {
     const uint32_t bx = (uint32_t)(key >> 26) & 0x7FFFFu, by = (uint32_t)(key >> 45) & 0x7FFFFu;
-    return (uint32_t)(key & 0xFFu) | ((bx * by_count + by) << 8);
+    return (uint32_t)(key & 0xFFu) * ((T.mask + 1) >> 8) + bx * T.dense_by + by;
 }
 
 // Next index of T.order for each calling lane: one atomic per wave on the shared
@@ -98,7 +101,7 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
     if (T.dense_by) {
         // The slot is the key: presence is one bit of a 2 MB-scale bitmap that stays
         // in L2, so a lookup touches no key line (the key is stored for export only).
-        const uint32_t h = dense_slot(key, T.dense_by), bit = 1u << (h & 31);
+        const uint32_t h = dense_slot(key, T), bit = 1u << (h & 31);
         uint32_t* w = T.present + (h >> 5);
         if (*w & bit) return (int)h;                    // stale 0 only costs the atomic
         if (atomicOr(w, bit) & bit) return (int)h;
@@ -134,7 +137,7 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
 // Slot of `key`, or -1 when absent (read-only tables: ffm_trained_core).
 __device__ int tab_find(const LearnTable& T, unsigned long long key) {
     if (T.dense_by) {
-        const uint32_t h = dense_slot(key, T.dense_by);
+        const uint32_t h = dense_slot(key, T);
         return (T.present[h >> 5] >> (h & 31)) & 1u ? (int)h : -1;
     }
     uint32_t h = (uint32_t)mix64(key) & T.mask;
