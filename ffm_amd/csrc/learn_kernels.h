@@ -46,6 +46,7 @@ struct LearnArgs {
     long long E, env_base;
     int variant, mode, bs;      // bs: block size of the state keys
     int D;                      // decisions per agent: 4 for ffm_actor_only, else 1
+    int sep_stencil;            // large maps: the DFF stencil runs as its own kernel (set by the launcher)
     const uint8_t* map;         // [HW] raw map values (0 free, 1/2 blocked, 3 exit)
     const uint32_t* map2;       // the same, 2 bits per cell (16 KB at 256x256: stays in L1)
     const float* sff32;         // [HW] raw SFF or nullptr

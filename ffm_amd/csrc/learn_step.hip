@@ -1344,7 +1344,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     LSTAMP(5);
 
     // ---- update_dff (model/ffm_unified.py:779-798) into the other buffer ---------------------
-    if (live && !(FFM_LABLATE & 8)) {
+    if (live && !a.sep_stencil && !(FFM_LABLATE & 8)) {
         float* out = a.dff_out + e * (long long)HW;
         for (int c = tid; c < HW; c += LPE) {
             const int x = fdiv(c, a.mW), y = c - x * W;
@@ -1711,8 +1711,35 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
     *T.mark = *T.n;
 }
 
+// update_dff of the batched step as its own launch (large maps): the batch
+// kernel's workgroup per env would run it at one CU's bandwidth after its
+// latency-bound phases; here every cell of every env is a lane.  Same arithmetic
+// as the in-kernel stencil (model/ffm_unified.py:779-798).
+__global__ __launch_bounds__(256) void learn_stencil_kernel(LearnArgs a) {
+    const int c = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (c >= a.HW) return;
+    const int H = a.H, W = a.W;
+    const long long e = blockIdx.y;
+    const float* dff = a.dff_in + e * (long long)a.HW;
+    const int x = fdiv(c, a.mW), y = c - x * W;
+    float acc = a.c0 * dff[c];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int nx = x + kNBx[k], ny = y + kNBy[k];
+        const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? a.c0 * dff[nx * W + ny] : 0.0f;
+        const float t = a.c1 * v;
+        acc = acc + t;
+    }
+    a.dff_out[e * (long long)a.HW + c] = acc < 1e-4f ? 0.0f : acc;
+}
+
+constexpr int kSepStencilHW = 16384;
+
 template <int BS, int EPB, int APT, int D, bool DL>
-hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
+hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
+    LearnArgs a = a0;
+    // the DFF lives in global memory (not DL) and the map is large: stencil apart
+    a.sep_stencil = !DL && a.HW >= kSepStencilHW && a.E <= 65535;
     const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
@@ -1722,6 +1749,8 @@ hipError_t launch_batch_t(const LearnArgs& a, hipStream_t s) {
     }
     const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
     learn_batch_kernel<BS, EPB, APT, D, DL><<<dim3(blocks), dim3(BS), smem, s>>>(a);
+    if (a.sep_stencil)
+        learn_stencil_kernel<<<dim3((unsigned)((a.HW + 255) / 256), (unsigned)a.E), dim3(256), 0, s>>>(a);
     return hipGetLastError();
 }
 
