@@ -1715,11 +1715,16 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
 // kernel's workgroup per env would run it at one CU's bandwidth after its
 // latency-bound phases; here every cell of every env is a lane.  Same arithmetic
 // as the in-kernel stencil (model/ffm_unified.py:779-798).
-__global__ __launch_bounds__(256) void learn_stencil_kernel(LearnArgs a) {
-    const int c = (int)(blockIdx.x * 256 + threadIdx.x);
+// XCD-aware: hardware deals consecutive workgroups round-robin over the 8 XCDs, so
+// workgroup b takes logical tile (b % 8) * (B / 8) + b / 8; each XCD then sweeps a
+// contiguous run of rows and finds the rows above and below in its own L2.
+__global__ __launch_bounds__(256) void learn_stencil_kernel(LearnArgs a, int tiles_per_env) {
+    const unsigned B = gridDim.x, b = blockIdx.x;
+    const unsigned lt = (B & 7u) ? b : (b & 7u) * (B >> 3) + (b >> 3);
+    const long long e = lt / (unsigned)tiles_per_env;
+    const int c = (int)((lt - (unsigned)e * (unsigned)tiles_per_env) * 256 + threadIdx.x);
     if (c >= a.HW) return;
     const int H = a.H, W = a.W;
-    const long long e = blockIdx.y;
     const float* dff = a.dff_in + e * (long long)a.HW;
     const int x = fdiv(c, a.mW), y = c - x * W;
     float acc = a.c0 * dff[c];
@@ -1739,7 +1744,7 @@ template <int BS, int EPB, int APT, int D, bool DL>
 hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     LearnArgs a = a0;
     // the DFF lives in global memory (not DL) and the map is large: stencil apart
-    a.sep_stencil = !DL && a.HW >= kSepStencilHW && a.E <= 65535;
+    a.sep_stencil = !DL && a.HW >= kSepStencilHW && (long long)((a.HW + 255) / 256) * a.E < (1ll << 31);
     const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
@@ -1749,8 +1754,10 @@ hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     }
     const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
     learn_batch_kernel<BS, EPB, APT, D, DL><<<dim3(blocks), dim3(BS), smem, s>>>(a);
-    if (a.sep_stencil)
-        learn_stencil_kernel<<<dim3((unsigned)((a.HW + 255) / 256), (unsigned)a.E), dim3(256), 0, s>>>(a);
+    if (a.sep_stencil) {
+        const int tiles = (a.HW + 255) / 256;
+        learn_stencil_kernel<<<dim3((unsigned)(tiles * a.E)), dim3(256), 0, s>>>(a, tiles);
+    }
     return hipGetLastError();
 }
 
