@@ -1738,6 +1738,42 @@ __global__ __launch_bounds__(256) void learn_stencil_kernel(LearnArgs a, int til
     a.dff_out[e * (long long)a.HW + c] = acc < 1e-4f ? 0.0f : acc;
 }
 
+// The same stencil four cells of a row per lane (W % 4 == 0): 16-B loads of the
+// quad and the quads above and below, scalar loads of its left and right
+// neighbours, one 16-B store; per cell the identical operation sequence.
+__global__ __launch_bounds__(256) void learn_stencil4_kernel(LearnArgs a, int tiles_per_env) {
+    const unsigned B = gridDim.x, b = blockIdx.x;
+    const unsigned lt = (B & 7u) ? b : (b & 7u) * (B >> 3) + (b >> 3);
+    const long long e = lt / (unsigned)tiles_per_env;
+    const int c = 4 * (int)((lt - (unsigned)e * (unsigned)tiles_per_env) * 256 + threadIdx.x);
+    if (c >= a.HW) return;
+    const int H = a.H, W = a.W;
+    const float* dff = a.dff_in + e * (long long)a.HW;
+    const int x = fdiv(c, a.mW), y = c - x * W;
+    const float c0 = a.c0, c1 = a.c1;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 m = *reinterpret_cast<const float4*>(dff + c);
+    const float4 u = x > 0 ? *reinterpret_cast<const float4*>(dff + c - W) : z4;
+    const float4 d = x < H - 1 ? *reinterpret_cast<const float4*>(dff + c + W) : z4;
+    const float l = y > 0 ? dff[c - 1] : 0.f, r = y + 4 < W ? dff[c + 4] : 0.f;
+    const float mv[4] = {m.x, m.y, m.z, m.w}, uv[4] = {u.x, u.y, u.z, u.w}, dv[4] = {d.x, d.y, d.z, d.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        float acc = c0 * mv[k];
+        const float nb[4] = {uv[k], dv[k], k > 0 ? mv[k - 1] : l, k < 3 ? mv[k + 1] : r};
+        const bool in[4] = {x > 0, x < H - 1, k > 0 || y > 0, k < 3 || y + 4 < W};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {                    // U, D, L, R as kNBx / kNBy
+            const float v = in[q] ? c0 * nb[q] : 0.0f;
+            const float t = c1 * v;
+            acc = acc + t;
+        }
+        o[k] = acc < 1e-4f ? 0.0f : acc;
+    }
+    *reinterpret_cast<float4*>(a.dff_out + e * (long long)a.HW + c) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
 constexpr int kSepStencilHW = 16384;
 
 template <int BS, int EPB, int APT, int D, bool DL>
@@ -1756,7 +1792,12 @@ hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     learn_batch_kernel<BS, EPB, APT, D, DL><<<dim3(blocks), dim3(BS), smem, s>>>(a);
     if (a.sep_stencil) {
         const int tiles = (a.HW + 255) / 256;
-        learn_stencil_kernel<<<dim3((unsigned)(tiles * a.E)), dim3(256), 0, s>>>(a, tiles);
+        if (a.W % 4 == 0) {
+            const int tiles4 = (a.HW / 4 + 255) / 256;
+            learn_stencil4_kernel<<<dim3((unsigned)(tiles4 * a.E)), dim3(256), 0, s>>>(a, tiles4);
+        } else {
+            learn_stencil_kernel<<<dim3((unsigned)(tiles * a.E)), dim3(256), 0, s>>>(a, tiles);
+        }
     }
     return hipGetLastError();
 }
