@@ -1491,13 +1491,20 @@ __global__ __launch_bounds__(256) void learn_apply_dense_kernel(LearnTable T, do
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
     for (size_t slot = (size_t)blockIdx.x * 256 + threadIdx.x; slot <= T.mask; slot += (size_t)gridDim.x * 256) {
-        if (!((T.present[slot >> 5] >> (slot & 31)) & 1u)) continue;
+        // the record and accumulators are loaded with the presence word, not after it
+        // (an absent slot holds the default and a zero accumulator)
+        const bool pres = (T.present[slot >> 5] >> (slot & 31)) & 1u;
         const size_t s = slot * WIDTH;
         double* vp = tval(T, slot);
+        long long qa[WIDTH];
+        double va[WIDTH];
+#pragma unroll
+        for (int k = 0; k < WIDTH; k++) { qa[k] = T.acc[s + k]; va[k] = vp[k]; }
+        if (!pres) continue;
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
-            const long long q = T.acc[s + k];
-            double v = vp[k];
+            const long long q = qa[k];
+            double v = va[k];
             if (q != 0) {
                 v = v + (double)q * (1.0 / kFxOne);
                 vp[k] = v;
