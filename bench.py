@@ -58,7 +58,10 @@ def parse():
     ap.add_argument("--envs-per-block", type=int, default=0)
     ap.add_argument("--cpu-envs", type=int, default=4096)
     ap.add_argument("--cpu-steps", type=int, default=0, help="0 = size the sample to ~15 s")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = this process's CPU share (OMP_NUM_THREADS, else its affinity set)")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed regions of K steps each, back to back; value = their median (BASELINE.md 3)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--log2-table", type=int, default=0, help="learner V/H hash capacity (0 = engine default)")
     ap.add_argument("--traffic-json", default=None,
@@ -113,21 +116,11 @@ def main():
     eng.reset(stream)
     eng.step(args.warmup, stream)
     torch.cuda.synchronize()
-    c0 = eng.counters(stream)
 
-    # Timed region: K back-to-back step launches on the stream, nothing in between.
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.step(args.steps, stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    c1 = eng.counters(stream)
-    elapsed = t1 - t0
-    agent_steps = c1["agent_steps"] - c0["agent_steps"]
+    # Timed regions: K back-to-back step launches on the stream, nothing in between.
+    reps = timed_repeats(args, world, dist, torch, lambda: eng.step(args.steps, stream),
+                         lambda: eng.counters(stream))
+    elapsed, agent_steps = reps["elapsed"], reps["agent_steps"]
 
     # Kernel time for the roofline: HIP events on the launch stream bracketing
     # nk back-to-back launches (a separate pass, so events do not perturb
@@ -144,12 +137,6 @@ def main():
     # Achievable HBM bandwidth on this box: a device-to-device copy of the same
     # number of bytes one launch moves (read + write), for context beside `peak`.
     copy_gbs = copy_bandwidth(torch, stream, E * (2 * A + 4 * H * W + 4))
-
-    if world > 1:
-        from ffm_amd.dist import reduce_counters, reduce_max
-        elapsed = reduce_max(elapsed, device="cuda")
-        d = {k: c1[k] - c0[k] for k in ("agent_steps", "exits", "resets", "steps")}
-        agent_steps = reduce_counters(d, device="cuda")["agent_steps"]
 
     if rank == 0:
         bytes_per_env_step = 2 * (2 * A + 4 * H * W + 4)
@@ -182,6 +169,8 @@ def main():
                 "global_envs": E * world, "parallelism": f"env-sharded x{world}",
             },
             "env_steps_per_s": E * world * args.steps / elapsed,
+            "mean_live_agents_per_env_step": agent_steps / (E * world * args.steps),
+            "repeats": reps["summary"],
             "kernel_ms_mean": float(np.mean(kern_ms)),
             "kernel_ms_median": float(np.median(kern_ms)),
             "roofline": {
@@ -212,6 +201,61 @@ LEARN_CONFIGS = {
                     "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0,
                     "neighborhood": "neumann", "block_size": 1, "epsilon": 0.2}),
 }
+
+
+def timed_repeats(args, world, dist, torch, run_k, counters):
+    """args.repeats timed regions of exactly K steps, each bracketed by a barrier and
+    a device sync on both sides; per region the time is the max over ranks and the
+    agent-steps the sum.  Returns the median region (by rate) and a summary."""
+    rows = []
+    for _ in range(max(1, args.repeats)):
+        c0 = counters()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_k()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        c1 = counters()
+        n = c1["agent_steps"] - c0["agent_steps"]
+        if world > 1:
+            from ffm_amd.dist import reduce_counters, reduce_max
+            el = reduce_max(el, device="cuda")
+            n = reduce_counters({k: c1[k] - c0[k] for k in ("agent_steps", "exits", "resets", "steps")},
+                                device="cuda")["agent_steps"]
+        rows.append((n / el, el, n))
+    med = sorted(rows)[(len(rows) - 1) // 2]
+    return {"elapsed": med[1], "agent_steps": med[2],
+            "summary": {"n": len(rows), "pick": "median rate",
+                        "values": [r[0] for r in rows], "elapsed_s": [round(r[1], 6) for r in rows]}}
+
+
+def cpu_share():
+    """Threads for the CPU baseline and the host facts reported beside it.
+
+    The GPU box gives each GPU a share of the host (OMP_NUM_THREADS is set to it
+    there); os.cpu_count() reports the whole machine, whose other cores belong to
+    other jobs, so the baseline runs on the share and reports nproc next to it."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = int(omp) if omp.isdigit() and int(omp) > 0 else aff
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return min(threads, aff), {"nproc": os.cpu_count(), "affinity_cpus": aff,
+                               "omp_num_threads": omp or None, "cpu_model": model}
 
 
 def learner_bytes_per_env_step(H, W, A, D):
@@ -247,21 +291,10 @@ def bench_learner(args, world, rank, torch, dist):
         run = lambda k: L.step(k, stream)  # noqa: E731
     run(args.warmup)
     torch.cuda.synchronize()
-    c0 = L.counters(stream)
     print(f"[bench] config {args.config}: warmup done", file=sys.stderr, flush=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    c1 = L.counters(stream)
-    elapsed = t1 - t0
-    agent_steps = c1["agent_steps"] - c0["agent_steps"]
-    print(f"[bench] timed region {elapsed:.3f} s", file=sys.stderr, flush=True)
+    reps = timed_repeats(args, world, dist, torch, lambda: run(args.steps), lambda: L.counters(stream))
+    elapsed, agent_steps = reps["elapsed"], reps["agent_steps"]
+    print(f"[bench] timed regions {reps['summary']['elapsed_s']} s", file=sys.stderr, flush=True)
     nk = min(args.steps, 100)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -271,11 +304,6 @@ def bench_learner(args, world, rank, torch, dist):
     torch.cuda.synchronize()
     step_ms = ev0.elapsed_time(ev1) / nk
     v_size, h_size = L.table_size("V"), L.table_size("H")
-    if world > 1:
-        from ffm_amd.dist import reduce_counters, reduce_max
-        elapsed = reduce_max(elapsed, device="cuda")
-        d = {k: c1[k] - c0[k] for k in ("agent_steps", "exits", "resets", "steps")}
-        agent_steps = reduce_counters(d, device="cuda")["agent_steps"]
     if rank == 0:
         D = 4 if cfg["variant"] == "actor_only" else 1
         bpe = learner_bytes_per_env_step(H, W, A, D)
@@ -302,6 +330,8 @@ def bench_learner(args, world, rank, torch, dist):
                 "parallelism": f"env-sharded x{world}",
             },
             "env_steps_per_s": E * world * args.steps / elapsed,
+            "mean_live_agents_per_env_step": agent_steps / (E * world * args.steps),
+            "repeats": reps["summary"],
             "step_ms_events": step_ms,
             "tables": {"V": v_size, "H": h_size},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -329,7 +359,8 @@ def cpu_baseline_learner(args, cfg, m, s):
     H, W = m.shape
     A = args.agents
     E = min(args.cpu_envs, 1024) if args.config == 4 else 2
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    share, host = cpu_share()
+    threads = args.cpu_threads or share
     cpu = LO.Learn(m, s, cfg["variant"], cfg["mode"], cfg["params"], log2_cap=22 if args.config == 4 else 24)
     core = O.Core(m, s, {"neighborhood": "neumann"})
     pos = np.full((E, A), 0xFFFF, np.uint16)
@@ -351,18 +382,27 @@ def cpu_baseline_learner(args, cfg, m, s):
     g.reset()
     g.step(t - 1)
     gp, gc, gd = g.get_state()
-    gk, gv = g.export_table("V")
+    tables = {"V": (g.export_table("V"), cpu.V.export())}
+    if cfg["variant"] == "actor_only" or cfg["mode"] in ("actor_only", "both"):
+        tables["H"] = (g.export_table("H"), cpu.Ht.export())
     g.close()
-    ck, cv = cpu.V.export()
-    ok = bool(np.array_equal(gc, cnt) and np.array_equal(gd.view(np.uint32), dff.view(np.uint32))
-              and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(E))
-              and np.array_equal(np.sort(gk), np.sort(ck))
-              and np.array_equal(gv[np.argsort(gk)].view(np.uint64), cv[np.argsort(ck)].view(np.uint64)))
+
+    def same_table(gkv, ckv):
+        (gk, gv), (ck, cv) = gkv, ckv
+        return (np.array_equal(np.sort(gk), np.sort(ck))
+                and np.array_equal(gv[np.argsort(gk)].view(np.uint64), cv[np.argsort(ck)].view(np.uint64)))
+
+    state_ok = bool(np.array_equal(gc, cnt) and np.array_equal(gd.view(np.uint32), dff.view(np.uint32))
+                    and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(E)))
+    tab_ok = {k: bool(same_table(*v)) for k, v in tables.items()}
+    ok = state_ok and all(tab_ok.values())
     return {
         "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
         "sample": (f"oracle/ffm_learn_oracle.c batched Philox mode, {E} envs x {t - 1} steps of the same "
-                   f"workload (OpenMP {threads} threads); state and V table bit-exact vs GPU: {ok}"),
-        "seconds": elapsed, "bit_exact_vs_gpu": ok,
+                   f"workload (OpenMP {threads} threads, {host['cpu_model']}); positions, counts, DFF and "
+                   f"tables {'/'.join(tables)} bit-exact vs GPU: {ok}"),
+        "seconds": elapsed, "bit_exact_vs_gpu": ok, "bit_exact_tables": tab_ok, "host": host,
+        "threads_note": "the GPU's host-CPU share on the box (OMP_NUM_THREADS); nproc is the whole machine",
     }
 
 
@@ -393,7 +433,8 @@ def cpu_baseline(args, m, s, params, torch):
     from ffm_amd.engine import Engine
     A, E = args.agents, args.cpu_envs
     H, W = m.shape
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    share, host = cpu_share()
+    threads = args.cpu_threads or share
     core = O.Core(m, s, params)
     pos = np.stack([core.reset_philox(A, args.seed, 0, e) for e in range(E)])
     cnt = np.full(E, A, np.int32)
@@ -427,20 +468,14 @@ def cpu_baseline(args, m, s, params, torch):
     g.close()
     ok = bool(np.array_equal(gc, cnt[:nchk]) and np.array_equal(gd.view(np.uint32), dff[:nchk].view(np.uint32))
               and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(nchk)))
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     return {
         "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
         "sample": (f"oracle/ffm_oracle.c Philox mode, {E} envs x {steps} steps of the same workload "
-                   f"(OpenMP {threads} threads, {model}); first {nchk} envs bit-exact vs GPU: {ok}"),
+                   f"(OpenMP {threads} threads, {host['cpu_model']}); first {nchk} envs bit-exact vs GPU: {ok}"),
         "seconds": elapsed, "bit_exact_vs_gpu": ok, "value_1thread": one_thread,
+        "value_per_core_x_nproc": one_thread * (host["nproc"] or 1), "host": host,
+        "threads_note": ("the GPU's host-CPU share on the box (OMP_NUM_THREADS); nproc is the whole machine, "
+                         "value_per_core_x_nproc extrapolates the 1-thread rate to every core"),
     }
 
 

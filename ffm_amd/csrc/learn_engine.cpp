@@ -67,6 +67,7 @@ struct ffm_learner {
     double* d_hpart = nullptr;
     ffm::LearnRec* d_recs = nullptr;
     int32_t* d_overflow = nullptr;
+    int32_t* h_overflow = nullptr;     // pinned: d_overflow as of the end of the last ffm_learner_step
     uint32_t* d_mt_np = nullptr;
     uint32_t* d_mt_py = nullptr;
     unsigned char* d_scratch = nullptr;
@@ -97,6 +98,7 @@ static void release(ffm_learner* l) {
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
                     l->d_eplog, l->d_eplog_n};
     for (void* p : bufs) (void)hipFree(p);
+    if (l->h_overflow) (void)hipHostFree(l->h_overflow);
     free_table(l->V);
     free_table(l->H);
     delete l;
@@ -291,6 +293,8 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     ALLOC(l->d_hpart, (size_t)ffm::kHstatBlocks * 4 * 8);
     if (l->post_update && !l->mt) ALLOC(l->d_recs, E * A * sizeof(ffm::LearnRec));
     ALLOC(l->d_overflow, 4);
+    if (hipHostMalloc((void**)&l->h_overflow, 4, hipHostMallocDefault) == hipSuccess) *l->h_overflow = 0;
+    else l->h_overflow = nullptr;
     ALLOC(l->d_count, 8);
     // an env ends at most one episode per step: 16 steps between drains always fit
     l->eplog_cap = std::max<long long>(16 * (long long)E, 4096);
@@ -414,6 +418,11 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
     if (!l || n_steps < 0) return fail(FFM_E_INVALID, "bad learner/n_steps");
     if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
     hipStream_t s = (hipStream_t)stream;
+    // Overflow without a host sync: the previous call queued a copy of the flag
+    // into pinned memory behind its steps; whatever of it has landed is reported
+    // here (every sync point -- counters, export, get_state -- reports it exactly).
+    if (l->h_overflow && (__atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) & 1))
+        return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
     for (int i = 0; i < n_steps; i++) {
         if (l->mt) {
             HIP_TRY(ffm::launch_learn_exact(make_args(l), s));
@@ -426,6 +435,8 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
         if (!rc) rc = phase_end(l, s);
         if (rc) return rc;
     }
+    if (l->h_overflow && n_steps > 0 && !l->mt)
+        HIP_TRY(hipMemcpyAsync(l->h_overflow, l->d_overflow, 4, hipMemcpyDeviceToHost, s));
     return FFM_OK;
 }
 
@@ -659,7 +670,10 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
     if (!l || (n > 0 && (!keys || !vals))) return fail(FFM_E_INVALID, "null argument");
     DevTable* T = pick(l, which);
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
-    if ((size_t)n > T->t.limit) return fail(FFM_E_NOMEM, "table capacity too small for import");
+    // hashed tables refuse inserts past 7/8 load; a dense table's slots are injective
+    // in the key, so any n <= cap valid keys fit
+    if ((size_t)n > (T->t.dense_by ? T->cap : (size_t)T->t.limit))
+        return fail(FFM_E_NOMEM, "table capacity too small for import");
     for (int64_t i = 0; i < n; i++) {
         if (keys[i] == ~0ull) return fail(FFM_E_INVALID, "invalid key");
         if (T->t.dense_by) {     // rank keys: 8 bits of ranks, blocks inside the map

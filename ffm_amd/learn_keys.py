@@ -17,9 +17,28 @@ and marks an empty hash slot.
 """
 from __future__ import annotations
 
+import importlib.util
 import pickle
+import sys
 
 import numpy as np
+
+
+def ensure_numpy_core_alias() -> None:
+    """Let table pickles written under NumPy 2 load under NumPy 1.x.
+
+    NumPy 2 pickles its scalars as ``numpy._core.multiarray.scalar``; NumPy 1.x
+    has no ``numpy._core`` package.  The reference aliases the module at import
+    (model/ffm_unified.py:8-10, model/ffm_actor_only.py:8-10); every loader of
+    this package goes through here, so one guarded alias serves them all.
+    Under NumPy 2 the real package exists and nothing changes."""
+    if "numpy._core" in sys.modules or importlib.util.find_spec("numpy._core") is not None:
+        return
+    sys.modules["numpy._core"] = np.core
+    sys.modules["numpy._core.multiarray"] = np.core.multiarray
+
+
+ensure_numpy_core_alias()
 
 EMPTY_KEY = (1 << 64) - 1
 _BX_SHIFT, _BY_SHIFT = 26, 45

@@ -198,6 +198,11 @@ int ffm_learner_destroy(ffm_learner* l);
  * zero the DFF and the per-env episode counters.  MT: zero the DFF and counts only (the caller uploads
  * positions drawn from its own generators, like ffm_engine_reset). */
 int ffm_learner_reset(ffm_learner* l, void* stream);
+/* Asynchronous: returns once the steps are queued on `stream`.  A hashed V / H
+ * table that passes 7/8 load drops the updates that would insert (the step goes
+ * on); that condition (FFM_E_NOMEM) is reported exactly at the next sync point
+ * (counters, table export / size, get_state) and, without a sync, by the next
+ * ffm_learner_step once the previous call's queued flag copy has landed. */
 int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream);
 int ffm_learner_set_state(ffm_learner* l, int64_t env0, int64_t n, const uint16_t* positions,
                           const int32_t* counts, const float* dff, void* stream);
