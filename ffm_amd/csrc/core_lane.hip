@@ -1,0 +1,452 @@
+// core_lane.hip -- the production (Philox) ffm_core step for small envs, one
+// wavefront per env pair, written for CDNA4 issue economy.
+//
+// One launch advances every env by one FloorFieldModel.step()
+// (model/ffm_core.py:36-117 of SoraKurihara/FFM).  Same semantics and RNG
+// definition as core_wave_kernel<.., MT=false, ..>, and the
+// same LDS picture: a padded direction-coded occupancy grid and a zero-halo DFF
+// tile per env.  What differs is how the work maps onto the wave:
+//
+//  * conflicts are settled by every requester for itself.  A moving agent reads
+//    the four (eight) codes around its target, which give the number of
+//    requesters m, its own rank k among them and the owner o (smallest index);
+//    with m > 1 it reads the owner's two friction words and evaluates the
+//    owner's draw (philox_friction, keyed by o as before).  It moves iff m == 1
+//    or the draw picks rank k.  No owner scatters a winner, so there is no
+//    next-position array and no per-target selection loop;
+//  * every granted request deposits at the mover's own source cell
+//    (model/ffm_core.py:91-98: dff[positions[i]] += 1, and a cell holds one
+//    agent), so deposits never collide: one LDS float add each, no read-back;
+//  * per-lane state (position, count, DFF slots) lives in registers from the
+//    prefetch to the store; LDS holds only what other lanes gather;
+//  * the stencil scales on the fly (B = c0 * D per operand, rounded exactly as
+//    the reference's separate pass) instead of a scale pass over the tile;
+//  * the per-agent code is nearly branch-free: decide evaluates every slot with
+//    selects and only the rare exact-arithmetic fallback branches; LDS writes of
+//    idle lanes are exec-masked (a shared dummy address would serialise them);
+//  * the DFF tile has no halo columns, so consecutive lanes' float4 slots are
+//    consecutive in LDS and the 16-B stage / stencil accesses are conflict free.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "core_common.h"
+#include "kernels.h"
+#include "wave_reset.h"
+
+namespace ffm {
+
+namespace {
+
+__host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// DFF tile of one env: 4 leading zero floats, H + 2 rows of W floats (a zero row
+// above and below the map; no halo columns, so the float4 slots of consecutive lanes
+// are consecutive and the 16-B accesses are bank-conflict free), 4 trailing zeros.
+// Cell (x, y) at 4 + (x + 1) * W + y.  Left / right neighbours across the map edge
+// are read from a zero word instead (the stencil) or belong to blocked cells whose
+// score is masked (decide).
+__host__ __device__ inline int lane_tile_floats(int H, int W) { return 4 + (H + 2) * W + 4; }
+
+struct LaneCarve {
+    size_t grid, tile, words, keys, per_wave;
+};
+
+// Per-wave LDS: two grids, two tiles, the 64 lanes' friction words, the placement keys.
+__host__ __device__ inline LaneCarve lane_carve(int PHW, int TS, int F) {
+    LaneCarve c;
+    size_t o = 0;
+    c.grid = o;  o += a16((size_t)(2 * PHW) * 2);
+    c.tile = o;  o += a16((size_t)(2 * TS) * 4);
+    c.words = o; o += 64 * 8;
+    c.keys = o;  o += a16((size_t)(F > 0 ? F : 1) * 8);
+    c.per_wave = o;
+    return c;
+}
+
+__host__ __device__ inline size_t lane_shared_bytes(int PHW, int F) {
+    return a16((size_t)PHW) + a16((size_t)PHW * 4) + a16((size_t)(F > 0 ? F : 1) * 2);
+}
+
+struct LaneState {
+    float4 d0, d1;   // the lane's two DFF float4 slots
+    int pos;         // agent al's cell (unpadded)
+    int cnt;         // the env's agent count
+};
+
+// decide() of model/ffm_core.py:41-88 for one agent at padded cell pp, Philox draw
+// words (wx, wy).  Returns the slot (0..NB-1 neighbour, NB stay) or kNoReq, and
+// whether the requested cell is an exit.  The fast path compares a float32 copy of
+// u (|error| < 2^-24) inside the 1e-4 margin of fast_choice; otherwise the exact
+// NumPy pipeline runs on the float64 u53.
+template <int NB>
+__device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
+                                                const float* dk, int dd0, float kS, float kD, uint32_t wx,
+                                                uint32_t wy, bool& to_exit) {
+    int cell[NB + 1], dcell[NB + 1];
+    uint32_t g[NB];
+    float sf[NB + 1], df[NB + 1];
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
+        dcell[s] = cell[s] + dd0 - nb_dx<NB>(s) * 2;   // the tile row is 2 shorter than the grid row
+        g[s] = gk[cell[s]];
+    }
+    cell[NB] = pp;
+    dcell[NB] = pp + dd0;
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        sf[k] = psff[cell[k]];
+        df[k] = dk[dcell[k]];
+    }
+    bool v[NB + 1];
+    v[NB] = true;
+    int nvalid = 0, exit_slot = -1;
+#pragma unroll
+    for (int s = NB - 1; s >= 0; s--) {
+        v[s] = g[s] == 0u || g[s] == 3u;                                 // :52-60
+        nvalid += v[s] ? 1 : 0;
+        exit_slot = g[s] == 3u ? s : exit_slot;                          // :66-72
+    }
+    float sc[NB + 1];
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        const float a = kS * sf[k];
+        const float b = kD * df[k];
+        sc[k] = a + b;                                                   // :77
+    }
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int k = 0; k <= NB; k++) mx = (v[k] && sc[k] > mx) ? sc[k] : mx;   // :78
+    float xs[NB + 1];
+#pragma unroll
+    for (int k = 0; k <= NB; k++) xs[k] = v[k] ? sc[k] - mx : -__builtin_inff();
+    // fast_choice with the float32 u, evaluated for every lane (selects only)
+    float cum[NB + 1];
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        const float e = __builtin_amdgcn_exp2f(xs[k] * 1.44269504088896341f);
+        acc += v[k] ? e : 0.0f;
+        cum[k] = v[k] ? acc : -1.0f;
+    }
+    const float uf = (float)(wx >> 8) * 0x1p-24f;
+    const float t = uf * acc;
+    const float d = kFastMargin * acc;
+    int slot = NB;
+    float cs = cum[NB];
+#pragma unroll
+    for (int k = NB - 1; k >= 0; k--) {
+        const bool ge = cum[k] >= t - d;
+        slot = ge ? k : slot;
+        cs = ge ? cum[k] : cs;
+    }
+    to_exit = exit_slot >= 0;
+    const bool forced = nvalid == 0 || exit_slot >= 0;               // :63, :66-72: no draw decides
+    uint32_t res = nvalid == 0 ? (uint32_t)kNoReq : exit_slot >= 0 ? (uint32_t)exit_slot : (uint32_t)slot;
+    if (!forced && !(cs > t + d)) {
+        // u within the margin of a boundary: the exact NumPy arithmetic decides (rare).
+        // Two passes over the running float64 sum (cumsum, then cdf /= cdf[-1] and the
+        // search) instead of a cdf array: this path sets the kernel's register peak.
+        const double u = u53(wx, wy);
+        float e[NB + 1];
+#pragma unroll
+        for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;   // :80
+        const float sum = np_sum<NB, float>(e, v, nvalid + 1);               // :81
+        double last = 0.0;
+#pragma unroll
+        for (int k = 0; k <= NB; k++)
+            if (v[k]) last += (double)(e[k] / sum);                          // :83, cumsum in choice
+        const double inv = 1.0 / last;
+        double run = 0.0;
+        uint32_t pick = NB;                                                  // cdf[-1] == 1 > u
+        bool found = false;
+#pragma unroll
+        for (int k = 0; k < NB; k++) {
+            if (v[k]) run += (double)(e[k] / sum);
+            if (v[k] && !found && cdf_gt(run, last, inv, u)) {
+                found = true;
+                pick = (uint32_t)k;
+            }
+        }
+        res = pick;
+    }
+    return res;
+}
+
+}  // namespace
+
+template <int NB, int HT, int WT>
+__global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int H = HT ? HT : a.H, W = WT ? WT : a.W;
+    const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
+    const int TS = lane_tile_floats(H, W);
+    const int A = a.A;
+    const int lane = (int)(threadIdx.x & 63);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int sub = lane >> 5, al = lane & 31;
+
+    const LaneCarve cv = lane_carve(PHW, TS, a.F);
+    uint8_t* pmap = smem;
+    float* psff = reinterpret_cast<float*>(smem + a16((size_t)PHW));
+    uint16_t* pfree = reinterpret_cast<uint16_t*>(smem + a16((size_t)PHW) + a16((size_t)PHW * 4));
+    unsigned char* wbase = smem + lane_shared_bytes(PHW, a.F) + (size_t)wv * cv.per_wave;
+    uint16_t* grid = reinterpret_cast<uint16_t*>(wbase + cv.grid);
+    float* tile = reinterpret_cast<float*>(wbase + cv.tile);
+    uint2* words = reinterpret_cast<uint2*>(wbase + cv.words);
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
+    uint16_t* gk = grid + sub * PHW;
+    float* dk = tile + sub * TS;
+
+    // The lane's two float4 DFF slots: cells 4q..4q+3 of the pair (q = lane, lane + 64).
+    int tb0 = -1, tb1 = -1;
+    {
+        const int c0 = 4 * lane, c1 = 4 * (lane + 64);
+        if (c0 < 2 * HW) {
+            const int s = c0 / HW, cell = c0 - s * HW, x = cell / W, y = cell - x * W;
+            tb0 = s * TS + 4 + (x + 1) * W + y;
+        }
+        if (c1 < 2 * HW) {
+            const int s = c1 / HW, cell = c1 - s * HW, x = cell / W, y = cell - x * W;
+            tb1 = s * TS + 4 + (x + 1) * W + y;
+        }
+    }
+    // A slot at a row start / end takes its left / right stencil operand from a zero
+    // word (tile index 0) instead of the neighbouring row.
+    const bool yl0 = tb0 >= 0 && ((tb0 - 4) % TS) % W == 0, yr0 = tb0 >= 0 && ((tb0 - 4) % TS) % W == W - 4;
+    const bool yl1 = tb1 >= 0 && ((tb1 - 4) % TS) % W == 0, yr1 = tb1 >= 0 && ((tb1 - 4) % TS) % W == W - 4;
+    // Which env each slot's cells belong to (for the reset zeroing): 0, 1 or 2 (none).
+    const int zs0 = min((4 * lane) / HW, 2), zs1 = min((4 * (lane + 64)) / HW, 2);
+
+    const int ngroups = (int)((a.E + 1) / 2);
+    const int wstride = (int)gridDim.x * 4;
+    int g = (int)blockIdx.x * 4 + wv;
+
+    auto load = [&](int gg, LaneState& st) {
+        st.d0 = st.d1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        st.pos = 0;
+        st.cnt = 0;
+        if (gg < 0) return;
+        const long long e0 = (long long)gg * 2;
+        const int nenv = (int)((a.E - e0) < 2 ? (a.E - e0) : 2);
+        const float4* dp = reinterpret_cast<const float4*>(a.dff + e0 * HW);
+        const int n4 = nenv * HW / 4;
+        if (sub < nenv) {
+            st.cnt = a.cnt[e0 + sub];
+            if (al < A) st.pos = a.pos[(e0 + sub) * A + al];
+        }
+        if (lane < n4) st.d0 = dp[lane];
+        if (lane + 64 < n4) st.d1 = dp[lane + 64];
+    };
+
+    LaneState cur;
+    load(g < ngroups ? g : -1, cur);
+    for (int i = threadIdx.x; i < PHW; i += 256) {
+        pmap[i] = a.pmap[i];
+        psff[i] = reinterpret_cast<const float*>(a.psff)[i];
+    }
+    for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
+    for (int i = lane; i < 2 * TS; i += 64) tile[i] = 0.0f;
+    __syncthreads();
+    for (int i = lane; i < 2 * PHW; i += 64) grid[i] = pmap[i - (i / PHW) * PHW];
+    wave_sync();
+
+    unsigned c_steps = 0, c_exits = 0, c_resets = 0;
+    const uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W for c < 2^16
+
+    for (; g < ngroups; g += wstride) {
+        const long long e0 = (long long)g * 2;
+        const int nenv = (int)((a.E - e0) < 2 ? (a.E - e0) : 2);
+        const bool env_ok = sub < nenv;
+        const uint32_t genv = (uint32_t)(a.env_base + e0 + sub);
+
+        // ---- stage this group's DFF; agent cell and occupancy mark --------------------
+        if (tb0 >= 0) *reinterpret_cast<float4*>(tile + tb0) = cur.d0;
+        if (tb1 >= 0) *reinterpret_cast<float4*>(tile + tb1) = cur.d1;
+        const int cnt = cur.cnt;
+        const bool live = env_ok && al < cnt;
+        const uint32_t cpos = (uint32_t)cur.pos;
+        const int x = (int)__umulhi(cpos, mW);   // exact for cpos < 2^16
+        const int y = (int)cpos - x * W;
+        const int pp = live ? (x + 1) * PW + y + 1 : PW + 1;       // idle lanes: an in-bounds cell
+        const int dd0 = 3 - (x + 1) * 2;                           // tile index = grid index + dd0 - 2/row
+        uint16_t* const mine = gk + pp;
+        if (live) *mine = (uint16_t)(DirCodes::kAgent | (uint32_t)al | (DirCodes::kNoDir << 8));
+        {
+            const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 32);
+            c_steps += (unsigned)(c0 + (nenv > 1 ? c1 : 0));
+        }
+        wave_sync();
+
+        // ---- decide (model/ffm_core.py:40-88) -------------------------------------------
+        const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
+        words[lane] = make_uint2(pb.z, pb.w);   // the friction draw, if this agent owns a contested target
+        bool to_exit = false;
+        uint32_t slot = lane_decide<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, pb.y, to_exit);
+        slot = live ? slot : kNoReq;
+        // the request goes into the agent's own grid cell: direction code in the high byte
+        if (live)
+            *mine = (uint16_t)(DirCodes::kAgent | (uint32_t)al |
+                               ((slot <= (uint32_t)NB ? slot : DirCodes::kNoDir) << 8));
+        wave_sync();
+
+        // ---- next group's HBM loads, in flight across resolve / stencil / stores ---------
+        // ---- resolve (model/ffm_core.py:90-98), by each requester ------------------------
+        const int r = (int)slot_cell<NB>(slot, pp, PW);          // kNoReq passes through
+        const bool req = slot <= (uint32_t)NB;
+        const bool moving = req && r != pp;
+        bool granted = req && !moving;                            // a stay is always granted
+        {
+            const int rt = moving ? r : pp;                       // in-bounds for every lane
+            int m = 0, k = 0, o = 0x7F;
+#pragma unroll
+            for (int s = 0; s < NB; s++) {
+                const uint32_t c = gk[rt - nb_dx<NB>(s) * PW - nb_dy<NB>(s)];
+                const bool is = (c & DirCodes::kAgent) != 0u && ((c >> 8) & 0xFu) == (uint32_t)s;
+                const int who = (int)(c & DirCodes::kIdx);
+                m += is ? 1 : 0;
+                k += (is && who < al) ? 1 : 0;
+                o = (is && who < o) ? who : o;
+            }
+            if (moving) {
+                if (m == 1) {
+                    granted = true;
+                } else {
+                    const uint2 f = words[sub * 32 + o];
+                    const int kk = philox_friction(f.x, f.y, (uint32_t)m, a.key0, a.key1, a.t, genv, (uint32_t)o);
+                    granted = kk == k;                                 // :95-96
+                }
+            }
+        }
+        // :91-98 -- the mover's source cell gains 1 (one agent per cell: no collisions)
+        if (granted) __hip_atomic_fetch_add(dk + pp + dd0, 1.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const int np = granted ? r : pp;
+
+        // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) ---------------
+        const bool keep = live && !(granted && to_exit);
+        const unsigned long long km = __ballot(keep);
+        const unsigned long long segm = sub ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+        const int newidx = lanes_below(km & segm);
+        const int newcnt = __popcll(km & segm);
+        {
+            const int n0 = __popcll(km & 0xFFFFFFFFull), n1 = __popcll(km >> 32);
+            const int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 32);
+            c_exits += (unsigned)((c0 - n0) + (nenv > 1 ? c1 - n1 : 0));
+        }
+        if (live) *mine = 0;   // unmark: agents only ever stand on free cells
+        const bool rs = a.auto_reset && env_ok && newcnt == 0;
+        const unsigned long long rsm = __ballot(rs);
+        c_resets += (unsigned)(((rsm & 1ull) ? 1 : 0) + ((rsm >> 32) & 1ull ? 1 : 0));
+        wave_sync();
+
+        // ---- positions and counts; auto-reset (rare, wave-uniform) -------
+        // Before the next group's loads are issued, so that the reset's registers and the
+        // prefetched state are never live together.
+        {
+            uint16_t* gp = a.pos + e0 * A;
+            if (keep) gp[sub * A + newidx] = (uint16_t)unpad(np, PW);
+            if (al == 0 && env_ok) {
+                a.cnt[e0 + sub] = rs ? a.N : newcnt;
+                if (rs && a.episodes) a.episodes[e0 + sub] += 1;
+            }
+        }
+        if (rsm) {
+            for (int s = 0; s < 2; s++)
+                if ((rsm >> (s * 32)) & 1ull)
+                    wave_reset_env(a, (uint32_t)(a.env_base + e0 + s), keys, pfree, a.pos + (e0 + s) * A, lane);
+        }
+
+        // ---- next group's HBM loads, in flight across the stencil, the stores and the
+        // next group's head ------------------------------------------------------------
+        LaneState nxt;
+        load(g + wstride < ngroups ? g + wstride : -1, nxt);
+
+        // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb] -----
+        auto stencil = [&](int tb, bool yl, bool yr, float4& out) {
+            const float* p = tile + tb;
+            float b[3][6];   // rows dx = -1..1, columns -1..4 (B values)
+#pragma unroll
+            for (int dx = -1; dx <= 1; dx++) {
+                const float4 u = *reinterpret_cast<const float4*>(p + dx * W);
+                b[dx + 1][1] = a.c0 * u.x; b[dx + 1][2] = a.c0 * u.y;
+                b[dx + 1][3] = a.c0 * u.z; b[dx + 1][4] = a.c0 * u.w;
+                if (NB == 4 && dx != 0) continue;
+                b[dx + 1][0] = a.c0 * tile[yl ? 0 : tb + dx * W - 1];   // tile[0] == 0
+                b[dx + 1][5] = a.c0 * tile[yr ? 0 : tb + dx * W + 4];
+            }
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float acc = b[1][j + 1];
+#pragma unroll
+                for (int s = 0; s < NB; s++) {
+                    const float t = a.c1 * b[1 + nb_dx<NB>(s)][j + 1 + nb_dy<NB>(s)];   // :113
+                    acc = acc + t;
+                }
+                o[j] = acc < 1e-4f ? 0.0f : acc;                                       // :116-117
+            }
+            out = make_float4(o[0], o[1], o[2], o[3]);
+        };
+        float4 o0 = make_float4(0.f, 0.f, 0.f, 0.f), o1 = o0;
+        if (tb0 >= 0) stencil(tb0, yl0, yr0, o0);
+        if (tb1 >= 0) stencil(tb1, yl1, yr1, o1);
+
+        // ---- DFF stores (an env reset this step starts its next episode with a zero DFF) --
+        {
+            float4* gd = reinterpret_cast<float4*>(a.dff + e0 * HW);
+            const int n4 = nenv * HW / 4;
+            const bool r0 = (rsm & 1ull) != 0, r1 = (rsm >> 32) != 0;   // wave-uniform
+            const bool z0 = zs0 == 0 ? r0 : (zs0 == 1 && r1), z1 = zs1 == 0 ? r0 : (zs1 == 1 && r1);
+            o0.x = z0 ? 0.f : o0.x; o0.y = z0 ? 0.f : o0.y; o0.z = z0 ? 0.f : o0.z; o0.w = z0 ? 0.f : o0.w;
+            o1.x = z1 ? 0.f : o1.x; o1.y = z1 ? 0.f : o1.y; o1.z = z1 ? 0.f : o1.z; o1.w = z1 ? 0.f : o1.w;
+            if (lane < n4) gd[lane] = o0;
+            if (lane + 64 < n4) gd[lane + 64] = o1;
+        }
+        wave_sync();
+        cur = nxt;
+    }
+
+    if (lane == 0) {
+        unsigned long long* ctr = a.counters + 4 * ((size_t)blockIdx.x * 4 + wv);
+        if (c_steps) atomicAdd(&ctr[0], (unsigned long long)c_steps);
+        if (c_exits) atomicAdd(&ctr[1], (unsigned long long)c_exits);
+        if (c_resets) atomicAdd(&ctr[2], (unsigned long long)c_resets);
+        if (blockIdx.x == 0 && wv == 0) atomicAdd(&ctr[3], 1ull);
+    }
+}
+
+size_t core_lane_smem_bytes(int H, int W, int F, int waves) {
+    const int PHW = (H + 2) * (W + 2);
+    return lane_shared_bytes(PHW, F) + (size_t)waves * lane_carve(PHW, lane_tile_floats(H, W), F).per_wave;
+}
+
+template <int NB, int HT, int WT>
+static hipError_t lane_op(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
+    const size_t smem = core_lane_smem_bytes(a.H, a.W, a.F, 4);
+    if (op) {
+        *occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, core_lane_kernel<NB, HT, WT>, 256, smem) != hipSuccess)
+            *occ = 0;
+        return hipSuccess;
+    }
+    core_lane_kernel<NB, HT, WT><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
+    return hipGetLastError();
+}
+
+static hipError_t lane_dispatch(const CoreStepArgs& a, int nb, int blocks, hipStream_t s, int op, int* occ) {
+    if (a.H == 12 && a.W == 12)
+        return nb == 4 ? lane_op<4, 12, 12>(a, blocks, s, op, occ) : lane_op<8, 12, 12>(a, blocks, s, op, occ);
+    return nb == 4 ? lane_op<4, 0, 0>(a, blocks, s, op, occ) : lane_op<8, 0, 0>(a, blocks, s, op, occ);
+}
+
+hipError_t launch_core_lane(const CoreStepArgs& a, int nb, int blocks, hipStream_t s) {
+    return lane_dispatch(a, nb, blocks, s, 0, nullptr);
+}
+
+int core_lane_blocks_per_cu(const CoreStepArgs& a, int nb) {
+    int n = 0;
+    (void)lane_dispatch(a, nb, 0, nullptr, 1, &n);
+    return n;
+}
+
+}  // namespace ffm

@@ -48,10 +48,10 @@ struct ffm_engine {
     ffm_engine_desc d{};
     int HW = 0, F = 0, K = 1, block = 256;
     bool f64 = false, mt = false;
-    bool pack = false;      // packed-bundle kernel (Philox, A <= 64, H*W <= 256): core_pack.hip
+    bool lane = false;      // lane kernel (Philox, A <= 32, W % 4 == 0, H*W <= 256): core_lane.hip
     bool wave = false;      // wave-per-env kernel (A <= 64) vs block-per-env kernel
     int wave_blocks = 0;    // persistent grid of the wave kernel
-    int pack_blocks = 0;    // grid of the pack kernel (every wave's env range <= 64)
+    int lane_blocks = 0;    // persistent grid of the lane kernel
     float kS32 = 0, kD32 = 0, c0 = 0, c1 = 0;
     double kS64 = 0;
     uint32_t t = 0;
@@ -153,19 +153,19 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     const int A = d.agent_capacity;
     const bool reset_lds = !e->mt && d.auto_reset;
     const int EW = A <= 32 ? 2 : 1;
-    // envs_per_block: 0 = auto (wave kernel where it fits, else block kernel),
-    // > 0 = block kernel with that many envs per workgroup, -1 = wave kernel,
-    // -2 = packed-bundle kernel (measured slower at C2: 49.9 vs 46.0 us).
-    e->pack = d.envs_per_block == -2 && !e->mt && !e->f64 && A <= 64 && W % 4 == 0 && HW <= 256 &&
-              ffm::core_pack_smem_bytes(H, W, A, e->F, 4, reset_lds, 4) <= 64 * 1024;
-    e->wave = !e->pack && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
+    // envs_per_block: 0 = auto (lane kernel, else wave kernel, where they fit; else
+    // block kernel), > 0 = block kernel with that many envs per workgroup,
+    // -1 = wave kernel, -2 = lane kernel.
+    e->lane = (d.envs_per_block == 0 || d.envs_per_block == -2) && !e->mt && !e->f64 && A <= 32 && W % 4 == 0 &&
+              HW <= 256 && ffm::core_lane_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
+    e->wave = !e->lane && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
               ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
     int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);
     if (e->mt) K = 1;
     while (K > 1 && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 64 * 1024) K--;
     e->K = K;
-    if (!e->wave && !e->pack && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 160 * 1024)
+    if (!e->wave && !e->lane && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 160 * 1024)
         return cleanup(fail(FFM_E_UNSUPPORTED, "env does not fit in LDS (tiled large-map kernel not built yet)"));
 
     const size_t E = (size_t)d.n_envs;
@@ -196,8 +196,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_cnt, E * 4);
     ALLOC(e->d_dff, E * HW * 4);
     ALLOC(e->d_eps, E * 4);
-    // Grids.  Persistent wave and pack kernels: CUs x resident blocks per CU;
-    // the pack kernel also needs every wave's env range <= 64 envs.
+    // Grids.  Persistent wave and lane kernels: CUs x resident blocks per CU.
     int cus = 0;
     he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device);
     if (he != hipSuccess) return cleanup(fail(FFM_E_HIP, "hipDeviceGetAttribute"));
@@ -213,26 +212,24 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
                 if (v > 0) e->wave_blocks = (int)std::min<long long>(v, (groups + 3) / 4);
             }
         }
-        if (e->pack) {
-            const int per_cu = std::max(1, ffm::core_pack_blocks_per_cu(a, d.neighborhood));
-            const long long need = (d.n_envs + 255) / 256;        // ranges of <= 64 envs
-            const long long most = (d.n_envs + 3) / 4;            // >= 1 env per wave
-            long long nb = std::min<long long>(most, (long long)cus * per_cu);
-            if (const char* ov = std::getenv("FFM_WAVE_BLOCKS")) {
+        if (e->lane) {
+            const int per_cu = std::max(1, ffm::core_lane_blocks_per_cu(a, d.neighborhood));
+            const long long groups = (d.n_envs + 1) / 2;
+            e->lane_blocks = (int)std::max<long long>(1, std::min<long long>((groups + 3) / 4, (long long)cus * per_cu));
+            if (const char* ov = std::getenv("FFM_WAVE_BLOCKS")) {   // diagnostic override of the grid
                 const long long v = std::atoll(ov);
-                if (v > 0) nb = std::min<long long>(v, most);
+                if (v > 0) e->lane_blocks = (int)std::min<long long>(v, (groups + 3) / 4);
             }
-            e->pack_blocks = (int)std::max<long long>(std::max<long long>(1, nb), need);
         }
     }
-    // One counter slot per wave (wave / pack kernel) or block (block kernel):
+    // One counter slot per wave (wave / lane kernel) or block (block kernel):
     // summed by ffm_engine_get_counters, never contended on the device.
     {
         const long long groups = (d.n_envs + EW - 1) / EW;
         const long long blocks = (d.n_envs + K - 1) / K;
         e->ctr_slots = (size_t)std::max<long long>(std::max<long long>(std::max<long long>(1, blocks),
                                                                        (groups + 3) / 4 * 4),
-                                                   (long long)e->pack_blocks * 4);
+                                                   (long long)e->lane_blocks * 4);
     }
     ALLOC(e->d_ctr, e->ctr_slots * 32);
     ALLOC(e->d_dbg, 16 * 8);
@@ -312,7 +309,7 @@ int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n_steps; i++) {
         ffm::CoreStepArgs a = make_args(e);
-        if (e->pack) HIP_TRY(ffm::launch_core_pack(a, e->d.neighborhood, e->pack_blocks, s));
+        if (e->lane) HIP_TRY(ffm::launch_core_lane(a, e->d.neighborhood, e->lane_blocks, s));
         else if (e->wave) HIP_TRY(ffm::launch_core_wave(a, e->d.neighborhood, e->mt, e->wave_blocks, s));
         else HIP_TRY(ffm::launch_core_block(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
         e->t++;

@@ -37,9 +37,9 @@ size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int
 size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool mt, bool reset);
 hipError_t launch_core_wave(const CoreStepArgs& a, int nb, bool mt, int blocks, hipStream_t s);
 int core_wave_blocks_per_cu(const CoreStepArgs& a, int nb, bool mt);
-size_t core_pack_smem_bytes(int H, int W, int A, int F, int nmax, bool reset, int waves);
-hipError_t launch_core_pack(const CoreStepArgs& a, int nb, int blocks, hipStream_t s);
-int core_pack_blocks_per_cu(const CoreStepArgs& a, int nb);
+size_t core_lane_smem_bytes(int H, int W, int F, int waves);
+hipError_t launch_core_lane(const CoreStepArgs& a, int nb, int blocks, hipStream_t s);
+int core_lane_blocks_per_cu(const CoreStepArgs& a, int nb);
 hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,

@@ -162,10 +162,10 @@ def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0
     return cnt, eps
 
 
-@pytest.mark.parametrize("epb", [0, -2])
+@pytest.mark.parametrize("epb", [0, -1])
 def test_philox_config2_full_size_matches_cpu(epb):
     """12x12, 32 agents, 65,536 envs (BASELINE config 2) for 150 steps (epb=0: auto,
-    the wave kernel; epb=-2: the packed-bundle kernel)."""
+    the lane kernel; epb=-1: the wave kernel)."""
     cnt, eps = _philox_compare(12, 12, 32, 65536, 150,
                                {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"},
                                envs_per_block=epb)
@@ -179,8 +179,8 @@ def test_philox_config2_full_size_matches_cpu(epb):
     {"k_S": 1.5, "k_D": 2.5, "diffuse": 0.3, "decay": 0.1, "neighborhood": "neumann"},
 ])
 def test_philox_12x12_param_points(params, N, epb):
-    """All kernels (epb=-2: packed bundles; -1: wave kernel, 2 or 1 env per wave;
-    3: block kernel, odd K)."""
+    """All kernels (epb=-2: lane kernel where A <= 32, else the block kernel; -1: wave
+    kernel, 2 or 1 env per wave; 3: block kernel, odd K)."""
     _philox_compare(12, 12, N, 2047, 120, params, seed=7, envs_per_block=epb)
 
 
@@ -192,14 +192,14 @@ def test_philox_odd_shapes():
 
 
 @pytest.mark.parametrize("E", [1, 5, 333, 5121])
-def test_philox_pack_small_and_ragged_env_counts(E):
-    """Packed kernel with fewer envs than waves, and ragged per-wave ranges."""
+def test_philox_lane_small_and_ragged_env_counts(E):
+    """Lane kernel with fewer envs than waves, an odd env count (half-empty last pair)."""
     _philox_compare(12, 12, 32, E, 90, {"neighborhood": "neumann"}, seed=11, envs_per_block=-2)
 
 
-def test_philox_pack_shapes():
-    """Packed kernel at runtime dimensions: 14x16 Moore (H*W = 224), and an 8x8 room
-    with 3 agents (bundles capped at 4 envs, most lanes idle)."""
+def test_philox_lane_shapes():
+    """Lane kernel at runtime dimensions: 14x16 Moore (H*W = 224: two DFF slots per
+    lane), and an 8x8 room with 3 agents (most lanes idle, slot-less lanes)."""
     _philox_compare(14, 16, 20, 999, 90, {"neighborhood": "moore", "k_D": 2}, seed=3, envs_per_block=-2)
     _philox_compare(8, 8, 3, 1000, 60, {"neighborhood": "neumann"}, seed=4, env_base=12345,
                     envs_per_block=-2)

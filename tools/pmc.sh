@@ -5,7 +5,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift || true
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-B="python3 bench.py --no-cpu --steps 60 --warmup 10 $*"
+B="python3 bench.py --no-cpu --steps 60 --warmup 10 --repeats 1 $*"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_INSTS_SMEM" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" \
