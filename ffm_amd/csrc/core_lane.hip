@@ -33,6 +33,24 @@
 #include "kernels.h"
 #include "wave_reset.h"
 
+#ifndef FFM_STAMPS
+#define FFM_STAMPS 0   // diagnostic builds only: per-phase s_memtime cycle sums per wave
+#endif
+#if FFM_STAMPS
+#define LSTAMP(k)                                                                          \
+    do {                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                        \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        st[k] += t_ - tlast;                                                               \
+        tlast = t_;                                                                        \
+    } while (0)
+#else
+#define LSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 namespace ffm {
 
 namespace {
@@ -48,10 +66,16 @@ __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15;
 __host__ __device__ inline int lane_tile_floats(int H, int W) { return 4 + (H + 2) * W + 4; }
 
 struct LaneCarve {
-    size_t grid, tile, words, keys, per_wave;
+    size_t grid, tile, words, keys, pend, per_wave;
 };
 
-// Per-wave LDS: two grids, two tiles, the 64 lanes' friction words, the placement keys.
+// Per-wave LDS: two grids, two tiles, the 64 lanes' friction words, the placement
+// keys, and the bitmask of envs this launch emptied (their placement is deferred to
+// the end of the launch, where none of the step's registers are live: placing in the
+// loop would set the kernel's register peak).  Bit 2 i + s = env s of the wave's
+// i-th pair; the host keeps every wave at <= kLaneMaxPairs pairs.
+constexpr int kLaneMaxPairs = 64;
+constexpr int kLanePendWords = 2 * kLaneMaxPairs / 32;
 __host__ __device__ inline LaneCarve lane_carve(int PHW, int TS, int F) {
     LaneCarve c;
     size_t o = 0;
@@ -59,6 +83,7 @@ __host__ __device__ inline LaneCarve lane_carve(int PHW, int TS, int F) {
     c.tile = o;  o += a16((size_t)(2 * TS) * 4);
     c.words = o; o += 64 * 8;
     c.keys = o;  o += a16((size_t)(F > 0 ? F : 1) * 8);
+    c.pend = o;  o += kLanePendWords * 4;
     c.per_wave = o;
     return c;
 }
@@ -67,21 +92,27 @@ __host__ __device__ inline size_t lane_shared_bytes(int PHW, int F) {
     return a16((size_t)PHW) + a16((size_t)PHW * 4) + a16((size_t)(F > 0 ? F : 1) * 2);
 }
 
-struct LaneState {
-    float4 d0, d1;   // the lane's two DFF float4 slots
-    int pos;         // agent al's cell (unpadded)
-    int cnt;         // the env's agent count
-};
+// Buffer resources over one env pair's rows of pos / cnt / DFF: a lane whose offset
+// is past the pair's bytes reads 0 and its store is dropped by the hardware, so no
+// load or store of the loop needs a lane branch, and the number of memory
+// instructions after the prefetch is fixed (the loop head then waits for the
+// prefetch only, not for the previous group's stores).
+constexpr int kOOB = 0x7FFFFFF0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pair_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
+                                           off, 0, 0);
+}
 
-// decide() of model/ffm_core.py:41-88 for one agent at padded cell pp, Philox draw
-// words (wx, wy).  Returns the slot (0..NB-1 neighbour, NB stay) or kNoReq, and
-// whether the requested cell is an exit.  The fast path compares a float32 copy of
-// u (|error| < 2^-24) inside the 1e-4 margin of fast_choice; otherwise the exact
-// NumPy pipeline runs on the float64 u53.
+
+// Candidate cells, validity and float32 scores of decide() (model/ffm_core.py:41-80)
+// for the agent at padded cell pp; shared by the fast and the exact pass.
 template <int NB>
-__device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
-                                                const float* dk, int dd0, float kS, float kD, uint32_t wx,
-                                                uint32_t wy, bool& to_exit) {
+__device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, const float* psff, const float* dk,
+                                           int dd0, float kS, float kD, bool (&v)[NB + 1], float (&xs)[NB + 1],
+                                           int& exit_slot) {
     int cell[NB + 1], dcell[NB + 1];
     uint32_t g[NB];
     float sf[NB + 1], df[NB + 1];
@@ -98,9 +129,9 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
         sf[k] = psff[cell[k]];
         df[k] = dk[dcell[k]];
     }
-    bool v[NB + 1];
     v[NB] = true;
-    int nvalid = 0, exit_slot = -1;
+    int nvalid = 0;
+    exit_slot = -1;
 #pragma unroll
     for (int s = NB - 1; s >= 0; s--) {
         v[s] = g[s] == 0u || g[s] == 3u;                                 // :52-60
@@ -117,10 +148,23 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
     float mx = -__builtin_inff();
 #pragma unroll
     for (int k = 0; k <= NB; k++) mx = (v[k] && sc[k] > mx) ? sc[k] : mx;   // :78
-    float xs[NB + 1];
 #pragma unroll
     for (int k = 0; k <= NB; k++) xs[k] = v[k] ? sc[k] - mx : -__builtin_inff();
-    // fast_choice with the float32 u, evaluated for every lane (selects only)
+    return nvalid;
+}
+
+// decide(), fast pass: returns the slot (0..NB-1 neighbour, NB stay), kNoReq, or
+// kPending when u lies within the margin of a cdf boundary.  The fast path compares
+// a float32 copy of u (|error| < 2^-24) inside fast_choice's 1e-4 margin; selects
+// only, no branch.
+template <int NB>
+__device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
+                                                const float* dk, int dd0, float kS, float kD, uint32_t wx,
+                                                bool& to_exit) {
+    bool v[NB + 1];
+    float xs[NB + 1];
+    int exit_slot;
+    const int nvalid = lane_scores<NB>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
     float cum[NB + 1];
     float acc = 0.0f;
 #pragma unroll
@@ -141,42 +185,121 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
         cs = ge ? cum[k] : cs;
     }
     to_exit = exit_slot >= 0;
-    const bool forced = nvalid == 0 || exit_slot >= 0;               // :63, :66-72: no draw decides
-    uint32_t res = nvalid == 0 ? (uint32_t)kNoReq : exit_slot >= 0 ? (uint32_t)exit_slot : (uint32_t)slot;
-    if (!forced && !(cs > t + d)) {
-        // u within the margin of a boundary: the exact NumPy arithmetic decides (rare).
-        // Two passes over the running float64 sum (cumsum, then cdf /= cdf[-1] and the
-        // search) instead of a cdf array: this path sets the kernel's register peak.
-        const double u = u53(wx, wy);
-        float e[NB + 1];
+    return nvalid == 0 ? (uint32_t)kNoReq                                // :63
+           : exit_slot >= 0 ? (uint32_t)exit_slot                        // :66-72, no draw
+           : cs > t + d ? (uint32_t)slot : (uint32_t)kPending;
+}
+
+// decide(), exact pass (rare): NumPy's float32 exp and add.reduce, float32 divide,
+// float64 cumsum, cdf /= cdf[-1], searchsorted(side="right") on the float64 u53.
+// Streams over the candidates, re-reading the scores from LDS in each of its passes
+// (max, sum, cdf total, search) with one candidate live at a time: this path sets
+// the kernel's register peak otherwise.  Neumann only (the 8-lane pairwise sum of
+// add.reduce needs every term at once: lane_decide_exact_arr).
+template <int NB>
+__device__ __forceinline__ float lane_score1(int k, int pp, int PW, const uint16_t* gk, const float* psff,
+                                             const float* dk, int dd0, float kS, float kD, bool& valid) {
+    int dx = 0, dy = 0;
 #pragma unroll
-        for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;   // :80
-        const float sum = np_sum<NB, float>(e, v, nvalid + 1);               // :81
-        double last = 0.0;
-#pragma unroll
-        for (int k = 0; k <= NB; k++)
-            if (v[k]) last += (double)(e[k] / sum);                          // :83, cumsum in choice
-        const double inv = 1.0 / last;
-        double run = 0.0;
-        uint32_t pick = NB;                                                  // cdf[-1] == 1 > u
-        bool found = false;
-#pragma unroll
-        for (int k = 0; k < NB; k++) {
-            if (v[k]) run += (double)(e[k] / sum);
-            if (v[k] && !found && cdf_gt(run, last, inv, u)) {
-                found = true;
+    for (int s = 0; s < NB; s++) {
+        dx = k == s ? nb_dx<NB>(s) : dx;
+        dy = k == s ? nb_dy<NB>(s) : dy;
+    }
+    const int cell = pp + dx * PW + dy;
+    const uint32_t g = gk[cell];
+    valid = k == NB || g == 0u || g == 3u;
+    const float sa = kS * psff[cell];
+    const float sb = kD * dk[cell + dd0 - dx * 2];
+    return sa + sb;                                                      // :77
+}
+
+template <int NB>
+__device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint16_t* gk, const float* psff,
+                                                      const float* dk, int dd0, float kS, float kD, double u) {
+    float mx = -__builtin_inff();
+#pragma unroll 1
+    for (int k = 0; k <= NB; k++) {
+        bool v;
+        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        mx = (v && sc > mx) ? sc : mx;                                   // :78
+    }
+    float sum = -0.0f;                                                   // add.reduce, < 8 terms: left fold
+#pragma unroll 1
+    for (int k = 0; k <= NB; k++) {
+        bool v;
+        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        if (v) sum += np_expf(sc - mx);                                  // :80-81
+    }
+    double last = 0.0;
+#pragma unroll 1
+    for (int k = 0; k <= NB; k++) {
+        bool v;
+        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        if (v) last += (double)(np_expf(sc - mx) / sum);                 // :83, cumsum in choice
+    }
+    const double inv = 1.0 / last;
+    double run = 0.0;
+    uint32_t pick = NB;                                                  // cdf[-1] == 1 > u
+#pragma unroll 1
+    for (int k = 0; k < NB; k++) {
+        bool v;
+        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        if (v) {
+            run += (double)(np_expf(sc - mx) / sum);
+            if (cdf_gt(run, last, inv, u)) {
                 pick = (uint32_t)k;
+                break;
             }
         }
-        res = pick;
     }
-    return res;
+    return pick;
+}
+
+// The same with every term held (Moore: add.reduce pairs 8 terms).
+template <int NB>
+__device__ __forceinline__ uint32_t lane_decide_exact_arr(int pp, int PW, const uint16_t* gk, const float* psff,
+                                                          const float* dk, int dd0, float kS, float kD, double u) {
+    bool v[NB + 1];
+    float xs[NB + 1];
+    int exit_slot;
+    const int nvalid = lane_scores<NB>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
+    float e[NB + 1];
+#pragma unroll
+    for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;   // :80
+    const float sum = np_sum<NB, float>(e, v, nvalid + 1);               // :81
+    double last = 0.0;
+#pragma unroll
+    for (int k = 0; k <= NB; k++)
+        if (v[k]) last += (double)(e[k] / sum);                          // :83, cumsum in choice
+    const double inv = 1.0 / last;
+    double run = 0.0;
+    uint32_t pick = NB;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        if (v[k]) run += (double)(e[k] / sum);
+        if (v[k] && !found && cdf_gt(run, last, inv, u)) {
+            found = true;
+            pick = (uint32_t)k;
+        }
+    }
+    return pick;
 }
 
 }  // namespace
 
+#ifndef FFM_LANE_ABLATE
+#define FFM_LANE_ABLATE 0   // diagnostic builds only: bit k replaces / skips one piece (tools/ab_core.sh)
+#endif
+// Minimum waves per SIMD asked of the register allocator.  The 12x12 Neumann build
+// (BASELINE config 2) fits 7 (72 VGPRs, SGPR spills to VGPR lanes only, no scratch);
+// forcing 7 on the others spills to scratch, so they keep the compiler's choice.
+template <int NB, int HT>
+constexpr int lane_waves() { return (NB == 4 && HT == 12) ? 7 : 1; }
+
 template <int NB, int HT, int WT>
-__global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lane_waves<NB, HT>(), 8)))
+void core_lane_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = HT ? HT : a.H, W = WT ? WT : a.W;
     const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
@@ -192,11 +315,10 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
     uint16_t* pfree = reinterpret_cast<uint16_t*>(smem + a16((size_t)PHW) + a16((size_t)PHW * 4));
     unsigned char* wbase = smem + lane_shared_bytes(PHW, a.F) + (size_t)wv * cv.per_wave;
     uint16_t* grid = reinterpret_cast<uint16_t*>(wbase + cv.grid);
-    float* tile = reinterpret_cast<float*>(wbase + cv.tile);
+    float* const tile = reinterpret_cast<float*>(wbase + cv.tile);
     uint2* words = reinterpret_cast<uint2*>(wbase + cv.words);
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
     uint16_t* gk = grid + sub * PHW;
-    float* dk = tile + sub * TS;
 
     // The lane's two float4 DFF slots: cells 4q..4q+3 of the pair (q = lane, lane + 64).
     int tb0 = -1, tb1 = -1;
@@ -218,29 +340,35 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
     // Which env each slot's cells belong to (for the reset zeroing): 0, 1 or 2 (none).
     const int zs0 = min((4 * lane) / HW, 2), zs1 = min((4 * (lane + 64)) / HW, 2);
 
-    const int ngroups = (int)((a.E + 1) / 2);
+    const int E32 = (int)a.E;                 // host-checked: E * H * W * 4 < 2^31
+    const uint32_t ebase = (uint32_t)a.env_base;
+    const int ngroups = (E32 + 1) / 2;
     const int wstride = (int)gridDim.x * 4;
     int g = (int)blockIdx.x * 4 + wv;
 
-    auto load = [&](int gg, LaneState& st) {
-        st.d0 = st.d1 = make_float4(0.f, 0.f, 0.f, 0.f);
-        st.pos = 0;
-        st.cnt = 0;
-        if (gg < 0) return;
-        const long long e0 = (long long)gg * 2;
-        const int nenv = (int)((a.E - e0) < 2 ? (a.E - e0) : 2);
-        const float4* dp = reinterpret_cast<const float4*>(a.dff + e0 * HW);
-        const int n4 = nenv * HW / 4;
-        if (sub < nenv) {
-            st.cnt = a.cnt[e0 + sub];
-            if (al < A) st.pos = a.pos[(e0 + sub) * A + al];
-        }
-        if (lane < n4) st.d0 = dp[lane];
-        if (lane + 64 < n4) st.d1 = dp[lane + 64];
-    };
+    // Per-lane byte offsets inside a pair (loop invariant); kOOB = no access.
+    const int off_cnt = sub * 4;                       // past the pair's bytes when sub >= nenv
+    const int off_d0 = 16 * lane;   // slot 1 is off_d0 + 1024 (the instruction offset)
 
+    // Next pair's state in registers: count, position, the two DFF float4 slots.
+    // Buffer loads: out-of-range lanes read 0, no lane branch.
+    struct LaneState {
+        float4 d0, d1;
+        int pos, cnt;
+    };
+    auto load = [&](int gg, LaneState& st) {
+        const int e0 = (gg < 0 ? 0 : gg) * 2;
+        const int nenv = gg < 0 ? 0 : min(E32 - e0, 2);
+        st.cnt = (int)__builtin_amdgcn_raw_buffer_load_b32(pair_rsrc(a.cnt + e0, nenv * 4), off_cnt, 0, 0);
+        st.pos = (int)__builtin_amdgcn_raw_buffer_load_b16(pair_rsrc(a.pos + (long long)e0 * A, nenv * A * 2),
+                                                           al < A ? (sub * A + al) * 2 : kOOB, 0, 0);
+        const __amdgpu_buffer_rsrc_t rd = pair_rsrc(a.dff + (long long)e0 * HW, nenv * HW * 4);
+        st.d0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, off_d0, 0, 0));
+        st.d1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, off_d0 + 1024, 0, 0));
+    };
     LaneState cur;
     load(g < ngroups ? g : -1, cur);
+
     for (int i = threadIdx.x; i < PHW; i += 256) {
         pmap[i] = a.pmap[i];
         psff[i] = reinterpret_cast<const float*>(a.psff)[i];
@@ -248,24 +376,38 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
     for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
     for (int i = lane; i < 2 * TS; i += 64) tile[i] = 0.0f;
     __syncthreads();
+    // Two dropped stores, so that on every path into the loop head the two youngest
+    // memory operations are stores (the compiler then waits for the loads with vmcnt(2),
+    // not for the previous group's DFF stores).
+    buf_st4(pair_rsrc(a.dff, 0), kOOB, make_float4(0.f, 0.f, 0.f, 0.f));
+    buf_st4(pair_rsrc(a.dff, 0), kOOB, make_float4(0.f, 0.f, 0.f, 0.f));
     for (int i = lane; i < 2 * PHW; i += 64) grid[i] = pmap[i - (i / PHW) * PHW];
     wave_sync();
 
     unsigned c_steps = 0, c_exits = 0, c_resets = 0;
     const uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W for c < 2^16
 
-    for (; g < ngroups; g += wstride) {
-        const long long e0 = (long long)g * 2;
-        const int nenv = (int)((a.E - e0) < 2 ? (a.E - e0) : 2);
-        const bool env_ok = sub < nenv;
-        const uint32_t genv = (uint32_t)(a.env_base + e0 + sub);
-
-        // ---- stage this group's DFF; agent cell and occupancy mark --------------------
+#if FFM_STAMPS
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+    float* const dk = tile + sub * TS;
+    uint32_t* const pend = reinterpret_cast<uint32_t*>(wbase + cv.pend);
+    if (lane < kLanePendWords) pend[lane] = 0u;
+    const int g_first = g;
+    for (int iter = 0; g < ngroups; g += wstride, iter++) {
+        // ---- stage this pair's DFF (loaded by the previous iteration or the prologue) -----
         if (tb0 >= 0) *reinterpret_cast<float4*>(tile + tb0) = cur.d0;
         if (tb1 >= 0) *reinterpret_cast<float4*>(tile + tb1) = cur.d1;
         const int cnt = cur.cnt;
-        const bool live = env_ok && al < cnt;
         const uint32_t cpos = (uint32_t)cur.pos;
+        const int e0 = g * 2;
+        const int nenv = min(E32 - e0, 2);
+        const bool env_ok = sub < nenv;
+        const uint32_t genv = ebase + (uint32_t)(e0 + sub);
+
+        // ---- agent cell and occupancy mark ----------------------------------------------
+        const bool live = env_ok && al < cnt;
         const int x = (int)__umulhi(cpos, mW);   // exact for cpos < 2^16
         const int y = (int)cpos - x * W;
         const int pp = live ? (x + 1) * PW + y + 1 : PW + 1;       // idle lanes: an in-bounds cell
@@ -278,19 +420,26 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
         }
         wave_sync();
 
+        LSTAMP(0);
         // ---- decide (model/ffm_core.py:40-88) -------------------------------------------
-        const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
+        const uint4 pb = (FFM_LANE_ABLATE & 1)
+                             ? make_uint4(genv * 2654435761u ^ (uint32_t)al * 40503u ^ a.t * 97u,
+                                          genv ^ (uint32_t)al * 7919u, a.t * 31u ^ genv, (uint32_t)al ^ a.t)
+                             : philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
         words[lane] = make_uint2(pb.z, pb.w);   // the friction draw, if this agent owns a contested target
         bool to_exit = false;
-        uint32_t slot = lane_decide<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, pb.y, to_exit);
+        uint32_t slot = lane_decide<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
         slot = live ? slot : kNoReq;
+        if (slot == kPending)   // u near a cdf boundary: the exact NumPy arithmetic decides
+            slot = NB == 4 ? lane_decide_exact<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, u53(pb.x, pb.y))
+                           : lane_decide_exact_arr<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, u53(pb.x, pb.y));
         // the request goes into the agent's own grid cell: direction code in the high byte
         if (live)
             *mine = (uint16_t)(DirCodes::kAgent | (uint32_t)al |
                                ((slot <= (uint32_t)NB ? slot : DirCodes::kNoDir) << 8));
         wave_sync();
 
-        // ---- next group's HBM loads, in flight across resolve / stencil / stores ---------
+        LSTAMP(1);
         // ---- resolve (model/ffm_core.py:90-98), by each requester ------------------------
         const int r = (int)slot_cell<NB>(slot, pp, PW);          // kNoReq passes through
         const bool req = slot <= (uint32_t)NB;
@@ -309,7 +458,7 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
                 o = (is && who < o) ? who : o;
             }
             if (moving) {
-                if (m == 1) {
+                if ((FFM_LANE_ABLATE & 8) || m == 1) {
                     granted = true;
                 } else {
                     const uint2 f = words[sub * 32 + o];
@@ -322,6 +471,7 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
         if (granted) __hip_atomic_fetch_add(dk + pp + dd0, 1.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         const int np = granted ? r : pp;
 
+        LSTAMP(2);
         // ---- exits: order-preserving compaction (model/ffm_core.py:100-102) ---------------
         const bool keep = live && !(granted && to_exit);
         const unsigned long long km = __ballot(keep);
@@ -339,28 +489,27 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
         c_resets += (unsigned)(((rsm & 1ull) ? 1 : 0) + ((rsm >> 32) & 1ull ? 1 : 0));
         wave_sync();
 
+        LSTAMP(3);
         // ---- positions and counts; auto-reset (rare, wave-uniform) -------
         // Before the next group's loads are issued, so that the reset's registers and the
         // prefetched state are never live together.
-        {
-            uint16_t* gp = a.pos + e0 * A;
-            if (keep) gp[sub * A + newidx] = (uint16_t)unpad(np, PW);
-            if (al == 0 && env_ok) {
-                a.cnt[e0 + sub] = rs ? a.N : newcnt;
-                if (rs && a.episodes) a.episodes[e0 + sub] += 1;
-            }
-        }
-        if (rsm) {
-            for (int s = 0; s < 2; s++)
-                if ((rsm >> (s * 32)) & 1ull)
-                    wave_reset_env(a, (uint32_t)(a.env_base + e0 + s), keys, pfree, a.pos + (e0 + s) * A, lane);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)unpad(np, PW), pair_rsrc(a.pos + (long long)e0 * A, nenv * A * 2),
+                                              keep ? (sub * A + newidx) * 2 : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)(rs ? a.N : newcnt), pair_rsrc(a.cnt + e0, nenv * 4),
+                                              al == 0 ? off_cnt : kOOB, 0, 0);
+        if (rsm) {   // wave-uniform, rare
+            if (a.episodes && al == 0 && rs) a.episodes[e0 + sub] += 1;
+            const uint32_t bits = (uint32_t)((rsm & 1ull) | (((rsm >> 32) & 1ull) << 1)) << ((2 * iter) & 31);
+            if (lane == 0) pend[(2 * iter) >> 5] |= bits;
         }
 
+        LSTAMP(4);
         // ---- next group's HBM loads, in flight across the stencil, the stores and the
         // next group's head ------------------------------------------------------------
         LaneState nxt;
         load(g + wstride < ngroups ? g + wstride : -1, nxt);
 
+        LSTAMP(5);
         // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb] -----
         auto stencil = [&](int tb, bool yl, bool yr, float4& out) {
             const float* p = tile + tb;
@@ -389,24 +538,43 @@ __global__ __launch_bounds__(256) void core_lane_kernel(CoreStepArgs a) {
         };
         float4 o0 = make_float4(0.f, 0.f, 0.f, 0.f), o1 = o0;
         if (tb0 >= 0) stencil(tb0, yl0, yr0, o0);
-        if (tb1 >= 0) stencil(tb1, yl1, yr1, o1);
+        if (!(FFM_LANE_ABLATE & 2) && tb1 >= 0) stencil(tb1, yl1, yr1, o1);
 
+        LSTAMP(6);
         // ---- DFF stores (an env reset this step starts its next episode with a zero DFF) --
         {
-            float4* gd = reinterpret_cast<float4*>(a.dff + e0 * HW);
-            const int n4 = nenv * HW / 4;
+            const __amdgpu_buffer_rsrc_t rd = pair_rsrc(a.dff + (long long)e0 * HW, nenv * HW * 4);
             const bool r0 = (rsm & 1ull) != 0, r1 = (rsm >> 32) != 0;   // wave-uniform
             const bool z0 = zs0 == 0 ? r0 : (zs0 == 1 && r1), z1 = zs1 == 0 ? r0 : (zs1 == 1 && r1);
             o0.x = z0 ? 0.f : o0.x; o0.y = z0 ? 0.f : o0.y; o0.z = z0 ? 0.f : o0.z; o0.w = z0 ? 0.f : o0.w;
             o1.x = z1 ? 0.f : o1.x; o1.y = z1 ? 0.f : o1.y; o1.z = z1 ? 0.f : o1.z; o1.w = z1 ? 0.f : o1.w;
-            if (lane < n4) gd[lane] = o0;
-            if (lane + 64 < n4) gd[lane + 64] = o1;
+            buf_st4(rd, off_d0, o0);
+            buf_st4(rd, off_d0 + 1024, o1);
         }
         wave_sync();
+        LSTAMP(7);
         cur = nxt;
     }
 
+    // ---- deferred auto-reset placements ------------------------------
+    wave_sync();
+    for (int w = 0; w < kLanePendWords; w++) {
+        uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend[w]);
+        while (m) {
+            const int bit = w * 32 + __builtin_ctz(m);
+            m &= m - 1u;
+            const int e = (g_first + (bit >> 1) * wstride) * 2 + (bit & 1);
+            wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + (long long)e * A, lane);
+        }
+    }
+
     if (lane == 0) {
+#if FFM_STAMPS
+        if (a.dbg) {
+            for (int k = 0; k < 8; k++) atomicAdd(&a.dbg[k], st[k]);
+            atomicAdd(&a.dbg[8], 1ull);
+        }
+#endif
         unsigned long long* ctr = a.counters + 4 * ((size_t)blockIdx.x * 4 + wv);
         if (c_steps) atomicAdd(&ctr[0], (unsigned long long)c_steps);
         if (c_exits) atomicAdd(&ctr[1], (unsigned long long)c_exits);
@@ -423,6 +591,8 @@ size_t core_lane_smem_bytes(int H, int W, int F, int waves) {
 template <int NB, int HT, int WT>
 static hipError_t lane_op(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
     const size_t smem = core_lane_smem_bytes(a.H, a.W, a.F, 4);
+    if (!op && ((a.E + 1) / 2 + (long long)blocks * 4 - 1) / ((long long)blocks * 4) > kLaneMaxPairs)
+        return hipErrorInvalidConfiguration;   // the grid must give every wave <= kLaneMaxPairs pairs
     if (op) {
         *occ = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, core_lane_kernel<NB, HT, WT>, 256, smem) != hipSuccess)
@@ -442,6 +612,8 @@ static hipError_t lane_dispatch(const CoreStepArgs& a, int nb, int blocks, hipSt
 hipError_t launch_core_lane(const CoreStepArgs& a, int nb, int blocks, hipStream_t s) {
     return lane_dispatch(a, nb, blocks, s, 0, nullptr);
 }
+
+int core_lane_max_pairs_per_wave() { return kLaneMaxPairs; }
 
 int core_lane_blocks_per_cu(const CoreStepArgs& a, int nb) {
     int n = 0;

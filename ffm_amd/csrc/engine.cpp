@@ -157,7 +157,8 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     // block kernel), > 0 = block kernel with that many envs per workgroup,
     // -1 = wave kernel, -2 = lane kernel.
     e->lane = (d.envs_per_block == 0 || d.envs_per_block == -2) && !e->mt && !e->f64 && A <= 32 && W % 4 == 0 &&
-              HW <= 256 && ffm::core_lane_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
+              HW <= 256 && ffm::core_lane_smem_bytes(H, W, e->F, 4) <= 64 * 1024 &&
+              (long long)d.n_envs * HW * 4 < (1ll << 31);   // 32-bit buffer offsets
     e->wave = !e->lane && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
               ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
@@ -192,7 +193,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_sff, sff_bytes);
     ALLOC(e->d_free, std::max<size_t>(1, fl.size()) * 2);
     ALLOC(e->d_free_padded, std::max<size_t>(1, fl.size()) * 2);
-    ALLOC(e->d_pos, E * A * 2);
+    ALLOC(e->d_pos, E * A * 2 + 16);   // + a dword: the lane kernel streams positions as dwords
     ALLOC(e->d_cnt, E * 4);
     ALLOC(e->d_dff, E * HW * 4);
     ALLOC(e->d_eps, E * 4);
@@ -220,6 +221,10 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
                 const long long v = std::atoll(ov);
                 if (v > 0) e->lane_blocks = (int)std::min<long long>(v, (groups + 3) / 4);
             }
+            // every wave steps at most core_lane_max_pairs_per_wave() pairs (its deferred
+            // reset mask); beyond that the grid grows past one resident wave of blocks
+            const long long per_wave = ffm::core_lane_max_pairs_per_wave();
+            e->lane_blocks = (int)std::max<long long>(e->lane_blocks, (groups + 4 * per_wave - 1) / (4 * per_wave));
         }
     }
     // One counter slot per wave (wave / lane kernel) or block (block kernel):

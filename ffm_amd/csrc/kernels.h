@@ -40,6 +40,7 @@ int core_wave_blocks_per_cu(const CoreStepArgs& a, int nb, bool mt);
 size_t core_lane_smem_bytes(int H, int W, int F, int waves);
 hipError_t launch_core_lane(const CoreStepArgs& a, int nb, int blocks, hipStream_t s);
 int core_lane_blocks_per_cu(const CoreStepArgs& a, int nb);
+int core_lane_max_pairs_per_wave();
 hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,

@@ -1,0 +1,12 @@
+#!/bin/bash
+# A/B timing of core-kernel library builds, interleaved (GPU box):
+#   bash tools/ab_core.sh "libA.so libB.so ..." [bench args...]
+set -o pipefail
+export TMPDIR=/tmp
+LIBS=$1; shift
+for r in 1 2 3; do
+  for f in $LIBS; do
+    v=$(FFM_LIB_PATH=$PWD/$f timeout -k 10 120 python3 bench.py --no-cpu --repeats 1 "$@" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d.get('kernel_ms_mean', d.get('step_ms_events', 0))*1000,2), 'us', round(d['value']/1e9,2), 'G')") || exit 1
+    echo "$(basename $f .so) $v"
+  done
+done

@@ -13,7 +13,7 @@ from ffm_amd.engine import Engine, load_library  # noqa: E402
 L = load_library()
 L.ffm_debug_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 m = make_room(12, 12)
-epb = int(sys.argv[1]) if len(sys.argv) > 1 else 0   # 0: auto (pack kernel), -1: wave kernel
+epb = int(sys.argv[1]) if len(sys.argv) > 1 else 0   # 0: auto (lane kernel), -1: wave kernel
 eng = Engine(m, l1_sff(m), n_envs=65536, n_agents=32, params={"neighborhood": "neumann"}, seed=42,
              envs_per_block=epb)
 eng.reset()
@@ -26,7 +26,8 @@ torch.cuda.synchronize()
 after = np.zeros(16, np.uint64)
 L.ffm_debug_read(eng._h, after.ctypes.data, 16)
 d = (after - base).astype(np.float64)
-names = ["head/pp", "marks", "decide", "req-write", "resolve", "exits", "stencil", "stage+store"]
+names = (["head/pp", "marks", "decide", "req-write", "resolve", "exits", "stencil", "stage+store"] if epb == -1 else
+         ["head+mark", "decide", "resolve", "exits", "pos+reset", "dma-issue", "stencil", "dff-store"])
 tot = d[:8].sum()
 waves = d[8]
 print(f"waves*launches={waves:.0f}  cycles/wave/launch={tot / waves:.0f}")
