@@ -79,8 +79,15 @@ struct ffm_learner {
     unsigned long long* d_eplog_n = nullptr;
     long long eplog_cap = 0;
     int F_all = 0;                           // free cells of the map (placement capacity)
+    ffm::TrajCapture traj{};                 // trajectory capture (n_sel = 0: off)
     DevTable V, H;
 };
+
+static void free_traj(ffm_learner* l) {
+    void* bufs[] = {(void*)l->traj.envs, (void*)l->traj.phase, l->traj.meta, l->traj.cells, l->traj.n};
+    for (void* p : bufs) (void)hipFree(p);
+    l->traj = ffm::TrajCapture{};
+}
 
 static void free_table(DevTable& T) {
     (void)hipFree(T.t.rec);
@@ -99,6 +106,7 @@ static void release(ffm_learner* l) {
                     l->d_eplog, l->d_eplog_n};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
+    free_traj(l);
     free_table(l->V);
     free_table(l->H);
     delete l;
@@ -208,7 +216,10 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (d.neighborhood != 4) return fail(FFM_E_UNSUPPORTED, "learning variants are built for neighborhood 'neumann'");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
-    if (d.agent_capacity < 1 || d.agent_capacity > 16384) return fail(FFM_E_INVALID, "agent_capacity");
+    // batched: LDS grid codes and placement sorts hold <= 16384 agents; the exact (MT) step
+    // keeps int scratch and u16 cells, so the drop-in classes can hold every free cell
+    if (d.agent_capacity < 1 || d.agent_capacity > (d.rng_mode == FFM_RNG_MT ? 65535 : 16384))
+        return fail(FFM_E_INVALID, "agent_capacity");
     if (d.n_agents < 0 || d.n_agents > d.agent_capacity) return fail(FFM_E_INVALID, "n_agents > agent_capacity");
     if (d.rng_mode != FFM_RNG_PHILOX && d.rng_mode != FFM_RNG_MT) return fail(FFM_E_INVALID, "rng_mode");
     if (learn->block_size < 1 && d.variant != FFM_VARIANT_ACTOR_ONLY) return fail(FFM_E_INVALID, "block_size");
@@ -407,6 +418,7 @@ static int phase_apply(ffm_learner* l, int32_t which, hipStream_t s) {
 }
 
 static int phase_end(ffm_learner* l, hipStream_t s) {
+    HIP_TRY(ffm::launch_learn_capture(make_args(l), l->traj, s));   // before the reset re-places
     l->cur ^= 1;
     if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
     l->t++;
@@ -754,6 +766,68 @@ int ffm_learner_drain_episodes(ffm_learner* l, int32_t* records, int64_t cap, in
     if (have > 0 && records)
         HIP_TRY(hipMemcpyAsync(records, l->d_eplog, (size_t)have * 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemsetAsync(l->d_eplog_n, 0, 8, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n = have;
+    if (dropped) *dropped = (int64_t)c - have;
+    return FFM_OK;
+}
+
+int ffm_learner_set_trajectory_capture(ffm_learner* l, const int32_t* envs, const int32_t* phases, int32_t n_sel,
+                                       int32_t period, int64_t capacity_rows, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->mt) return fail(FFM_E_INVALID, "trajectory capture is the batched step's (MT drop-in: run(return_trajectory=True))");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    if (n_sel < 0 || (n_sel > 0 && (!envs || period < 1 || capacity_rows < 1)))
+        return fail(FFM_E_INVALID, "trajectory capture: envs, period >= 1 and capacity_rows >= 1 are required");
+    for (int32_t i = 0; i < n_sel; i++) {
+        if (envs[i] < 0 || envs[i] >= l->d.n_envs) return fail(FFM_E_INVALID, "trajectory capture: env out of range");
+        if (phases && phases[i] < 0) return fail(FFM_E_INVALID, "trajectory capture: phase must be >= 0");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipStreamSynchronize(s));        // the previous buffers may still be read by queued steps
+    free_traj(l);
+    if (n_sel == 0) return FFM_OK;
+    ffm::TrajCapture& c = l->traj;
+    const size_t A = (size_t)l->d.agent_capacity;
+    hipError_t e = hipSuccess;
+    int* de = nullptr; int* dp = nullptr;
+    if (e == hipSuccess) e = hipMalloc((void**)&de, (size_t)n_sel * 4);
+    if (e == hipSuccess && phases) e = hipMalloc((void**)&dp, (size_t)n_sel * 4);
+    c.envs = de; c.phase = dp;
+    if (e == hipSuccess) e = hipMalloc((void**)&c.meta, (size_t)capacity_rows * 16);
+    if (e == hipSuccess) e = hipMalloc((void**)&c.cells, (size_t)capacity_rows * A * 2);
+    if (e == hipSuccess) e = hipMalloc((void**)&c.n, 8);
+    if (e != hipSuccess) {
+        free_traj(l);
+        return fail(FFM_E_NOMEM, std::string("trajectory capture: ") + hipGetErrorString(e));
+    }
+    c.n_sel = n_sel; c.period = period; c.cap = capacity_rows;
+    HIP_TRY(hipMemcpyAsync(de, envs, (size_t)n_sel * 4, hipMemcpyHostToDevice, s));
+    if (dp) HIP_TRY(hipMemcpyAsync(dp, phases, (size_t)n_sel * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c.n, 0, 8, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_learner_drain_trajectory(ffm_learner* l, int32_t* meta, uint16_t* cells, int64_t cap, int64_t* n,
+                                 int64_t* dropped, void* stream) {
+    if (!l || !n) return fail(FFM_E_INVALID, "null argument");
+    *n = 0;
+    if (dropped) *dropped = 0;
+    if (l->traj.n_sel == 0) return FFM_OK;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, l->traj.n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const long long have = std::min<long long>((long long)c, l->traj.cap);
+    if (have > cap) {
+        *n = have;
+        return fail(FFM_E_INVALID, "drain_trajectory: buffer too small (*n holds the count)");
+    }
+    const size_t A = (size_t)l->d.agent_capacity;
+    if (have > 0 && meta) HIP_TRY(hipMemcpyAsync(meta, l->traj.meta, (size_t)have * 16, hipMemcpyDeviceToHost, s));
+    if (have > 0 && cells) HIP_TRY(hipMemcpyAsync(cells, l->traj.cells, (size_t)have * A * 2, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemsetAsync(l->traj.n, 0, 8, s));
     HIP_TRY(hipStreamSynchronize(s));
     *n = have;
     if (dropped) *dropped = (int64_t)c - have;

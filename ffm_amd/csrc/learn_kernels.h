@@ -86,6 +86,18 @@ struct LearnArgs {
 
 constexpr int kHstatBlocks = 2048;
 
+// Trajectory capture of the batched step (ffm_learner_set_trajectory_capture): the
+// selected envs' positions after every step of a captured episode, appended as rows.
+struct TrajCapture {
+    const int* envs;            // [n_sel] local env indices
+    const int* phase;           // [n_sel] episode k is captured iff (k + phase) % period == 0
+    int n_sel, period;
+    int* meta;                  // [cap][4] global env, episode k, step in the episode (1-based), count
+    uint16_t* cells;            // [cap][A] x*W+y, live agents first, 0xFFFF after
+    unsigned long long* n;      // rows claimed (past cap: dropped)
+    long long cap;
+};
+
 size_t learn_exact_scratch_bytes(int HW, int A);
 int learn_batch_block_size(int A);
 size_t learn_batch_smem_bytes(int HW, int A, int D);
@@ -97,6 +109,7 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_capture(const LearnArgs& a, const TrajCapture& c, hipStream_t s);
 hipError_t launch_learn_clear(const LearnTable& T, int width, double dflt, hipStream_t s);
 hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
                                     long long cap, unsigned long long* count, hipStream_t s);

@@ -1554,6 +1554,32 @@ __global__ __launch_bounds__(256) void learn_clear_kernel(LearnTable T, int widt
 // Philox placement: the N free cells with the smallest
 // (key_j, j), in that order.  Candidates (all F, or those under a threshold
 // chosen so that N <= expected count << capacity) are bitonic-sorted in LDS.
+// Trajectory capture (model/ffm_unified.py:902-931 run(return_trajectory=True): the
+// positions after every step; run_actor_only_training.py:199-218 keeps one every 100th
+// episode).  One workgroup per selected env, after the step and before the auto-reset
+// re-places an env that ended, so an episode's last row holds its final positions.
+__global__ __launch_bounds__(256) void learn_capture_kernel(LearnArgs a, TrajCapture c) {
+    __shared__ long long row;
+    const int b = blockIdx.x;
+    const long long e = c.envs[b];
+    const int k = a.episodes[e];
+    const int ph = c.phase ? c.phase[b] : 0;
+    if ((k + ph) % c.period != 0) return;                 // workgroup-uniform
+    if (threadIdx.x == 0) row = (long long)atomicAdd(c.n, 1ull);
+    __syncthreads();
+    if (row >= c.cap) return;                             // counted as dropped by the drain
+    const int n = a.cnt[e];
+    if (threadIdx.x == 0) {
+        int* m = c.meta + 4 * row;
+        m[0] = (int)(a.env_base + e);
+        m[1] = k;
+        m[2] = a.ep_steps[e];
+        m[3] = n;
+    }
+    for (int i = threadIdx.x; i < a.A; i += 256)
+        c.cells[row * a.A + i] = i < n ? a.pos[e * a.A + i] : kNone16;
+}
+
 constexpr int kResetBS = 256;
 constexpr int kResetCap = 16384;
 
@@ -1925,6 +1951,12 @@ hipError_t launch_learn_import(const LearnTable& T, int width, const unsigned lo
 
 hipError_t launch_learn_clear(const LearnTable& T, int width, double dflt, hipStream_t s) {
     learn_clear_kernel<<<dim3(2048), dim3(256), 0, s>>>(T, width, dflt);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_capture(const LearnArgs& a, const TrajCapture& c, hipStream_t s) {
+    if (c.n_sel <= 0) return hipSuccess;
+    learn_capture_kernel<<<dim3((unsigned)c.n_sel), dim3(256), 0, s>>>(a, c);
     return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ EXPORTED = [
     "ffm_learner_set_step_index", "ffm_learner_step_local", "ffm_learner_step_apply", "ffm_learner_step_end",
     "ffm_learner_delta_export", "ffm_learner_delta_merge", "ffm_learner_set_placement",
     "ffm_learner_set_epsilon_schedule", "ffm_learner_drain_episodes",
+    "ffm_learner_set_trajectory_capture", "ffm_learner_drain_trajectory",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -131,6 +132,8 @@ def load_library():
     L.ffm_learner_set_placement.argtypes = [P, P, i32, i32]
     L.ffm_learner_set_epsilon_schedule.argtypes = [P, C.c_double, C.c_double, C.c_double, C.c_double]
     L.ffm_learner_drain_episodes.argtypes = [P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
+    L.ffm_learner_set_trajectory_capture.argtypes = [P, P, P, i32, i32, i64, P]
+    L.ffm_learner_drain_trajectory.argtypes = [P, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     for name in EXPORTED:
         if name != "ffm_last_error":
             getattr(L, name).restype = C.c_int
@@ -498,6 +501,47 @@ class Learner:
             raise RuntimeError(f"episode log overflowed: {dropped.value} records lost (drain more often)")
         out = buf[: n.value]
         return out[np.lexsort((out[:, 1], out[:, 0]))]
+
+    def set_trajectory_capture(self, envs, period: int = 100, phases=None, capacity_rows: int | None = None,
+                               stream=None):
+        """Capture the positions after every step of episode k of env envs[i] (local index)
+        whenever (k + phases[i]) % period == 0 (k counted from the last reset, 0-based);
+        drain_trajectories() returns them.  envs=[] turns capture off.  Default capacity:
+        1,024 steps of every selected env between drains."""
+        envs = np.ascontiguousarray(envs, np.int32).reshape(-1)
+        ph = None if phases is None else np.ascontiguousarray(phases, np.int32).reshape(-1)
+        if ph is not None and len(ph) != len(envs):
+            raise ValueError("phases must have one entry per selected env")
+        cap = int(capacity_rows) if capacity_rows else max(1, 1024 * len(envs))
+        self._traj_cap = cap if len(envs) else 0
+        _check(self._L.ffm_learner_set_trajectory_capture(
+            self._h, _ptr(envs) if len(envs) else None, _ptr(ph) if ph is not None and len(ph) else None,
+            len(envs), int(period), cap, _stream_handle(stream)))
+
+    def drain_trajectories(self, stream=None) -> dict:
+        """Rows captured since the last drain, grouped: {(global env, episode k): (steps [T],
+        positions list of T int32 [n_t, 2] arrays)} in step order -- the reference's
+        run(return_trajectory=True) list of `positions` copies (model/ffm_unified.py:902-931)."""
+        cap = getattr(self, "_traj_cap", 0)
+        if not cap:
+            return {}
+        meta = np.empty((cap, 4), np.int32)
+        cells = np.empty((cap, self.A), np.uint16)
+        n, dropped = C.c_int64(), C.c_int64()
+        _check(self._L.ffm_learner_drain_trajectory(self._h, _ptr(meta), _ptr(cells), cap, C.byref(n),
+                                                    C.byref(dropped), _stream_handle(stream)))
+        if dropped.value:
+            raise RuntimeError(f"trajectory buffer overflowed: {dropped.value} rows lost (drain more often)")
+        meta, cells = meta[: n.value], cells[: n.value]
+        order = np.lexsort((meta[:, 2], meta[:, 1], meta[:, 0]))
+        out = {}
+        for r in order.tolist():
+            env, k, st, c = meta[r].tolist()
+            cc = cells[r, :c].astype(np.int32)
+            steps, pos = out.setdefault((env, k), ([], []))
+            steps.append(st)
+            pos.append(np.stack([cc // self.W, cc % self.W], axis=1))
+        return out
 
     def set_v_default(self, v: float, stream=None):
         _check(self._L.ffm_learner_set_v_default(self._h, float(v), _stream_handle(stream)))

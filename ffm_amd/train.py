@@ -44,18 +44,50 @@ def _key_obj(variant, k):
     return K.to_rank_tuple(k) if variant in ("unified", "trained") else K.to_cells_bytes(k)
 
 
+def trajectory_selection(E: int, per_env: int, every: int):
+    """Envs and capture phases for the trajectories of every `every`-th episode.
+
+    Within a configuration the reported episodes are numbered env-major, episode
+    n = e * per_env + k + 1 for env e's k-th episode (k < per_env); the reference keeps
+    the trajectory of every episode with n % every == 0 (run_actor_only_training.py:199-218),
+    i.e. (k + phase_e) % every == 0 with phase_e = (e * per_env + 1) % every."""
+    envs, phases = [], []
+    for e in range(E):
+        ph = (e * per_env + 1) % every
+        if (-ph) % every < per_env:
+            envs.append(e)
+            phases.append(ph)
+    return np.asarray(envs, np.int32), np.asarray(phases, np.int32)
+
+
+def save_trajectory(out_dir: str, N: int, episode: int, total: int, positions: list, steps: int):
+    """One trajectory file as run_actor_only_training.py:206-218 writes it."""
+    os.makedirs(out_dir, exist_ok=True)
+    traj = np.empty(len(positions), dtype=object)      # np.array(trajectory, dtype=object)
+    for i, p in enumerate(positions):
+        traj[i] = p
+    np.savez_compressed(os.path.join(out_dir, f"trajectory_N{N}_ep{episode:05d}_total{total:05d}.npz"),
+                        positions=traj, episode=episode, N=N, total_episode=total, steps=steps)
+
+
 def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per_config: int,
                    eps_start: float | None = None, eps_end: float | None = None, out_dir: str | None = None,
-                   log_every: int = 16, verbose: bool = True) -> dict:
+                   log_every: int = 16, verbose: bool = True, trajectory_every: int = 0) -> dict:
     """Run every (radius, N) configuration; return per-configuration statistics and
-    (when `out_dir` is given) write the reference's output files there."""
+    (when `out_dir` is given) write the reference's output files there, with the
+    trajectory of every `trajectory_every`-th episode under out_dir/trajectories."""
     L = learner
     E = L.n_envs
     per_env = max(1, math.ceil(episodes_per_config / E))
     chunk = max(1, min(int(log_every), 16))      # the episode log holds 16 steps of episode ends
     rows, configs = [], []
     episode_num = 0
+    n_traj = 0
     t_start = time.time()
+    tsel, tph = (trajectory_selection(E, per_env, trajectory_every) if trajectory_every > 0
+                 else (np.zeros(0, np.int32), None))
+    if len(tsel):
+        L.set_trajectory_capture(tsel, period=trajectory_every, phases=tph, capacity_rows=len(tsel) * chunk * 2)
     for radius in radius_list:
         avail = available_cells(L.map, exit_pos, radius)
         for N in n_list:
@@ -67,23 +99,36 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
                 L.set_epsilon_schedule(eps_start, eps_end, 1, per_env)
             v0 = L.table_size("V")
             L.reset()
-            done = []
+            done, trajs = [], {}
             while True:
                 L.step(chunk)
                 d = L.drain_episodes()
                 if len(d):
                     done.append(d)
+                if len(tsel):
+                    for key, val in L.drain_trajectories().items():
+                        st, ps = trajs.setdefault(key, ([], []))
+                        st.extend(val[0])
+                        ps.extend(val[1])
                 if L.episodes()[0].min() >= per_env:
                     break
             ended = np.concatenate(done)
             ended = ended[ended[:, 1] < per_env]
+            ended = ended[np.lexsort((ended[:, 1], ended[:, 0]))]   # env-major: episode e * per_env + k + 1
             v1 = L.table_size("V")
             h1 = L.table_size("H") if L.actor else 0
-            for env, k, steps, emptied in ended.tolist():
+            base = episode_num
+            for idx, (env, k, steps, emptied) in enumerate(ended.tolist()):
                 episode_num += 1
                 eps = (min(max(eps_start + (eps_end - eps_start) * ((k + 1) / per_env), 0.0), 1.0)
                        if eps_start is not None and L.actor else 0.0)
                 rows.append([episode_num, len(configs) + 1, radius, N, steps, v1, h1, f"{eps:.6f}"])
+                tr = trajs.get((env, k))
+                if tr is not None and out_dir and (idx + 1) % trajectory_every == 0:
+                    assert len(tr[0]) == steps and tr[0] == list(range(1, steps + 1)), "trajectory rows"
+                    save_trajectory(os.path.join(out_dir, "trajectories"), N, idx + 1, base + idx + 1, tr[1],
+                                    steps)
+                    n_traj += 1
             mean = float(ended[:, 2].mean())
             configs.append({"radius": radius, "N": N, "episodes": len(ended), "mean_steps": mean,
                             "std_steps": float(ended[:, 2].std()), "emptied": int(ended[:, 3].sum()),
@@ -91,7 +136,9 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
             if verbose:
                 print(f"radius={radius:2d}, N={N:3d}: mean steps={mean:7.2f} over {len(ended)} episodes, "
                       f"V {v0} -> {v1}", flush=True)
-    result = {"configs": configs, "rows": rows, "seconds": time.time() - t_start}
+    if len(tsel):
+        L.set_trajectory_capture([])
+    result = {"configs": configs, "rows": rows, "seconds": time.time() - t_start, "trajectories": n_traj}
     if out_dir:
         write_outputs(L, result, out_dir, exit_pos, radius_list, n_list, episodes_per_config)
     return result
@@ -141,6 +188,9 @@ def main():
     ap.add_argument("--eps", default="0.2,0.01", help="epsilon start,end (actor modes)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--trajectory-every", type=int, default=None,
+                    help="save every n-th episode's trajectory (default 100 for actor modes, as "
+                         "run_actor_only_training.py; 0 = none)")
     a = ap.parse_args()
     m = make_room(a.size, a.size)
     # run_unified_*_training.py MODEL_PARAMS
@@ -151,7 +201,9 @@ def main():
     L = Learner(m, l1_sff(m), a.variant, n_envs=a.envs, n_agents=max(n_list), mode=a.mode, params=params,
                 seed=a.seed, max_steps=a.max_steps)
     es, ee = (float(x) for x in a.eps.split(","))
-    run_curriculum(L, (0, a.size // 2), [int(x) for x in a.radius.split(",")], n_list, a.episodes, es, ee, a.out)
+    every = a.trajectory_every if a.trajectory_every is not None else (100 if L.actor else 0)
+    run_curriculum(L, (0, a.size // 2), [int(x) for x in a.radius.split(",")], n_list, a.episodes, es, ee, a.out,
+                   trajectory_every=every)
 
 
 if __name__ == "__main__":

@@ -77,7 +77,7 @@ typedef struct {
     int32_t neighborhood;     /* 4 = "neumann", 8 = "moore" (model/ffm_core.py:28-34) */
     double k_S, k_D, diffuse, decay;   /* params, model/ffm_core.py:8-15 */
     int64_t n_envs;           /* E: independent environments on this device */
-    int32_t agent_capacity;   /* A: slots per env (>= n_agents) */
+    int32_t agent_capacity;   /* A: slots per env (>= n_agents; learners: <= 16384 batched, <= 65535 MT) */
     int32_t n_agents;         /* N placed by reset / auto-reset */
     int32_t rng_mode;         /* FFM_RNG_* */
     int32_t auto_reset;       /* 1: an env emptied by a step is re-placed (Philox, keyed by that
@@ -257,6 +257,21 @@ int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double ep
  * episode per step, so draining every 16 steps never loses one). */
 int ffm_learner_drain_episodes(ffm_learner* l, int32_t* records, int64_t cap, int64_t* n, int64_t* dropped,
                                void* stream);
+/* Trajectory capture of the batched step (replaces run(max_steps, return_trajectory=True),
+ * model/ffm_unified.py:902-931 / model/ffm_actor_only.py, and the driver's every-100th-episode
+ * trajectory files, run_actor_only_training.py:199-218).  For each selected env (local index)
+ * its episode k (0-based, counted from the last ffm_learner_reset) is captured iff
+ * (k + phases[i]) % period == 0 (phases NULL: 0).  After every step of a captured episode one
+ * row is appended: meta {global env, k, step in the episode (1-based), count} and the
+ * agent_capacity cells (x*W+y, live agents first in the reference's order, 0xFFFF after),
+ * i.e. the reference's `positions` after that step.  Rows past capacity_rows are dropped and
+ * counted.  n_sel = 0 turns capture off.  Batched (Philox) learners only. */
+int ffm_learner_set_trajectory_capture(ffm_learner* l, const int32_t* envs, const int32_t* phases, int32_t n_sel,
+                                       int32_t period, int64_t capacity_rows, void* stream);
+/* Rows captured since the last drain, in no particular order within a step (sort by
+ * env, k, step); meta [cap][4] int32, cells [cap][agent_capacity] u16, host pointers. */
+int ffm_learner_drain_trajectory(ffm_learner* l, int32_t* meta, uint16_t* cells, int64_t cap, int64_t* n,
+                                 int64_t* dropped, void* stream);
 int ffm_learner_get_step_index(ffm_learner* l, uint32_t* t);
 int ffm_learner_set_step_index(ffm_learner* l, uint32_t t);
 

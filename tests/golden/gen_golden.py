@@ -95,9 +95,18 @@ def run_case(name, FloorFieldModel, map_array, sff, params, N, seeds, max_steps,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated case names to (re)generate")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
     sys.path.insert(0, args.ref)
     from model.ffm_core import FloorFieldModel  # the reference itself
+
+    global run_case
+    _run = run_case
+
+    def run_case(name, *a, **kw):        # noqa: F811 -- filter by --only
+        if not only or name in only:
+            _run(name, *a, **kw)
 
     yaml_params = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"}
     m12, s12 = reference_12x12(args.ref, HERE)
@@ -118,6 +127,9 @@ def main():
     from ffm_amd.data import make_room, l1_sff
     m64 = make_room(64, 64)
     run_case("neumann_64x64_N512", FloorFieldModel, m64, l1_sff(m64), yaml_params, 512, [7], 40, 0)
+    # BASELINE config-3 geometry at depth: 4 seeds x 200 steps (episodes last ~300 steps)
+    run_case("neumann_64x64_N512_s4", FloorFieldModel, m64, l1_sff(m64), yaml_params, 512, [31, 32, 33, 34],
+             200, 1)
     # main.py configuration: 50x50 room, float64 L1 SFF, N=100, seed 42, until empty
     m50 = np.load(os.path.join(args.ref, "data/maps/simple_room.npy"))
     s50 = np.load(os.path.join(args.ref, "data/sff/distance_L1.npy"))

@@ -82,14 +82,14 @@ def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_ste
                     model.set_epsilon(e)
                 eps_list.append(e)
                 p0 = model.positions
-                init.append((p0[:, 0] * W + p0[:, 1]).astype(np.int16))
+                init.append((p0[:, 0] * W + p0[:, 1]).astype(np.int64))
                 steps = 0
                 while model.positions.shape[0] > 0 and steps < max_steps:
                     model.step()
                     steps += 1
                     p = model.positions
                     counts.append(p.shape[0])
-                    cells.extend((p[:, 0] * W + p[:, 1]).astype(np.int16).tolist())
+                    cells.extend((p[:, 0] * W + p[:, 1]).astype(np.int64).tolist())
                     hashes.append(dff_hash(model.dff))
                 nsteps.append(steps)
             V = model.get_v_table()
@@ -106,13 +106,14 @@ def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_ste
             bg = np.random.mtrand._rand._bit_generator
             np_tail.append(np.asarray(bg.random_raw(4), dtype=np.uint32))
             py_tail.append(np.asarray([random.getrandbits(32) for _ in range(4)], dtype=np.uint32))
+    cdt = np.int16 if H * W <= 32767 and N <= 32767 else np.int32   # cells of a 256x256 map need 17 bits
     out = dict(
         map=map_array.astype(np.uint8), sff=sff, params=json.dumps(params), variant=variant,
         mode=mode or "", N=np.int32(N), seeds=np.asarray(seeds, np.int64), n_ep=np.int32(n_ep),
         max_steps=np.int32(max_steps), reload_v=np.int32(reload_v), eps=np.asarray(eps_list),
-        init=np.concatenate(init).astype(np.int16), init_n=np.asarray([len(i) for i in init], np.int32),
-        nsteps=np.asarray(nsteps, np.int32), counts=np.asarray(counts, np.int16),
-        cells=np.asarray(cells, np.int16), dff_hash=np.asarray(hashes, np.uint64),
+        init=np.concatenate(init).astype(cdt), init_n=np.asarray([len(i) for i in init], np.int32),
+        nsteps=np.asarray(nsteps, np.int32), counts=np.asarray(counts, cdt),
+        cells=np.asarray(cells, cdt), dff_hash=np.asarray(hashes, np.uint64),
         v_keys=np.asarray(vk, np.uint64), v_vals=np.asarray(vv, np.float64), v_n=np.asarray(vn, np.int64),
         h_keys=np.asarray(hk, np.uint64), h_vals=np.asarray(hv, np.float64).reshape(-1, 5),
         h_n=np.asarray(hn, np.int64), np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
@@ -227,6 +228,18 @@ def main():
     run_case("actoronly_12x12_N16", "actor_only", AO, m12, s12, ao_p, 16, [12, 13], 4, 300,
              eps_sched=eps)
     run_case("actoronly_12x12_N32_eps0", "actor_only", AO, m12, s12, ao_p, 32, [14], 2, 300)
+
+    # BASELINE config-5 geometry (256x256 room, 8,192 agents, block 1, the
+    # run_unified_actor_training.py parameters), truncated: every reference step
+    # rebuilds an O(N) occupied set per agent (model/ffm_unified.py:297-299) and
+    # the actor scans the whole H table per agent (:413-422).
+    from ffm_amd.data import make_room, l1_sff
+    m256 = make_room(256, 256)
+    s256 = l1_sff(m256)
+    run_case("unified_critic_256x256_N8192", "unified", UNI, m256, s256, uni_p, 8192, [21], 1, 20,
+             mode="critic_only")
+    run_case("unified_actor_256x256_N8192", "unified", UNI, m256, s256, uni_p, 8192, [22], 1, 3,
+             mode="actor_only", eps_sched=[0.2])
 
     # pretrained critics (the drivers' pretrained_v_path): a critic recorded by the
     # reference itself, pickled with bytes keys like the critic-training scripts

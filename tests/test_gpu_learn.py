@@ -131,7 +131,7 @@ def _random_rank_table(H, W, bs, seed=0, frac=0.6):
 
 
 def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
-                    nthreads=16, sff_dtype=np.float32):
+                    nthreads=16, sff_dtype=np.float32, log2_cap=22, chunks=1):
     from ffm_amd.data import make_room, l1_sff
     from oracle import learn as LO
     from oracle import oracle as O
@@ -140,7 +140,7 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     A = A or N
     L = _learner(m, s, variant, n_envs=E, n_agents=N, agent_capacity=A, mode=mode, params=params,
                  rng="philox", seed=seed, auto_reset=True, max_steps=max_steps, env_base=env_base)
-    cpu = LO.Learn(m, s, variant, mode, params, log2_cap=22)
+    cpu = LO.Learn(m, s, variant, mode, params, log2_cap=log2_cap)
     if variant == "trained":
         hk, hv = _random_rank_table(H, W, int(params.get("block_size", 5)), seed=seed)
         L.import_table("H", hk, hv)
@@ -161,6 +161,8 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     for t in range(1, T + 1):
         tot += cpu.step_philox_batch(pos, counts, dff, eps, ep_steps, seed, t, True, N, max_steps, env_base,
                                      nthreads)
+        if chunks > 1 and t % (T // chunks) == 0:
+            print(f"  cpu step {t}/{T}", flush=True)   # progress of a long comparison
     L.step(T)
     gp, gc, gd = L.get_state()
     geps, gst = L.episodes()
@@ -225,6 +227,19 @@ def test_learner_philox_config5_geometry():
     """256x256 room, 8,192 agents (BASELINE config 5, ffm_unified actor_only): thresholded
     on-device placement (> 16,384 free cells) and the 8-agents-per-lane kernel."""
     _philox_compare("unified", "actor_only", {"block_size": 5}, 256, 256, 8192, 4, 6, max_steps=300, seed=5)
+
+
+@pytest.mark.timeout(900)
+def test_learner_philox_config5_through_truncation():
+    """The bench's config-5 workload itself (run_unified_actor_training.py parameters,
+    block 1, epsilon 0.2, max_steps 300) on 8 envs for 310 steps: every env is
+    truncated at step 300 and auto-reset, the H statistics are populated for 300
+    steps, and positions, DFF bits, V and H must equal the CPU restatement."""
+    import bench
+    cfg = bench.LEARN_CONFIGS[5]
+    counts, eps = _philox_compare(cfg["variant"], cfg["mode"], cfg["params"], 256, 256, 8192, 8, 310,
+                                  max_steps=cfg["max_steps"], seed=42, log2_cap=24, chunks=10)
+    assert (eps == 1).all(), "every env truncates once at max_steps = 300"
 
 
 def test_learner_table_import_export_roundtrip():
@@ -407,6 +422,94 @@ def test_learner_curriculum_schedule_and_episode_log(variant, mode):
     assert np.array_equal(np.sort(k0), np.sort(k1))
     assert np.array_equal(v0[np.argsort(k0)].view(np.uint64), v1[np.argsort(k1)].view(np.uint64))
     L.close()
+
+
+@pytest.mark.parametrize("variant,mode", [("actor_only", None), ("unified", "actor_only"), ("unified", "critic_only")])
+def test_learner_trajectory_capture_matches_cpu(variant, mode):
+    """Batched trajectory capture (run(return_trajectory=True) rows, model/ffm_unified.py:902-931;
+    the drivers keep every 100th episode's, run_actor_only_training.py:199-218) against the CPU
+    restatement stepped in phases: the positions after every step of every captured episode,
+    including the final rows of emptied and of truncated (max_steps) episodes."""
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import learn as LO
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"epsilon": 0.1, "block_size": 1}
+    E, N, T, seed, maxs = 96, 12, 120, 11, 30
+    sel = np.array([0, 5, 17, 42, 95], np.int32)
+    ph = np.array([0, 1, 2, 1, 0], np.int32)
+    period = 2
+    L = _learner(m, s, variant, n_envs=E, n_agents=N, mode=mode, params=p, seed=seed, max_steps=maxs)
+    L.set_trajectory_capture(sel, period=period, phases=ph, capacity_rows=len(sel) * 40)
+    L.reset()
+    got = {}
+    for _ in range(T // 30):
+        L.step(30)
+        for key, (st, ps) in L.drain_trajectories().items():
+            g = got.setdefault(key, ([], []))
+            g[0].extend(st)
+            g[1].extend(ps)
+    cpu = LO.Learn(m, s, variant, mode, p, log2_cap=20)
+    sh = LO.Shard(cpu, E, N, N, seed, 0, maxs, nthreads=8)
+    want = {}
+    for _ in range(T):
+        sh.step_local()
+        sh.step_apply("V")
+        if sh.actor:
+            sh.step_apply("H")
+        for e, q in zip(sel.tolist(), ph.tolist()):
+            k = int(sh.episodes[e])
+            if (k + q) % period == 0:
+                c = int(sh.counts[e])
+                cells = sh.pos[e, :c].astype(np.int32)
+                w = want.setdefault((e, k), ([], []))
+                w[0].append(int(sh.ep_steps[e]) + 1)
+                w[1].append(np.stack([cells // 12, cells % 12], axis=1))
+        sh.step_end()
+    assert sorted(got) == sorted(want)
+    for key, (st, ps) in want.items():
+        assert got[key][0] == st, f"{key}: steps"
+        assert len(got[key][1]) == len(ps)
+        for a, b in zip(got[key][1], ps):
+            assert np.array_equal(a, b), f"{key}: positions"
+    assert len(want) >= 2 * len(sel)
+    if mode == "critic_only":      # SFF-led agents: emptied episodes end with an empty row
+        assert any(len(v[1][-1]) == 0 for v in want.values())
+    else:                          # near-random walkers: truncated at max_steps
+        assert any(len(v[0]) == maxs for v in want.values())
+    L.set_trajectory_capture([])
+    L.step(1)
+    assert L.drain_trajectories() == {}
+    L.close()
+
+
+def test_train_writes_reference_trajectory_files(tmp_path):
+    """ffm_amd.train.run_curriculum keeps every n-th episode's trajectory in the file format of
+    run_actor_only_training.py:206-218 (positions as an object array of per-step [n_t, 2]
+    arrays, episode, N, total_episode, steps), consistent with steps_per_episode.csv."""
+    import csv
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.train import run_curriculum
+    m = make_room(12, 12)
+    p = {"k_D": 1, "k_A": 10, "alpha_v": 0.1, "alpha_h": 0.1, "gamma": 0.95, "exit_reward": 100.0,
+         "step_penalty": 0.0, "collision_penalty": -1.0, "neighborhood": "neumann"}
+    L = _learner(m, l1_sff(m), "actor_only", n_envs=16, n_agents=8, params=p, seed=3, max_steps=60)
+    res = run_curriculum(L, (0, 6), [3, 5], [1, 8], 40, 0.2, 0.01, str(tmp_path), verbose=False,
+                         trajectory_every=10)
+    L.close()
+    with open(tmp_path / "steps_per_episode.csv") as f:
+        rows = list(csv.DictReader(f))
+    files = sorted((tmp_path / "trajectories").glob("trajectory_N*_ep*_total*.npz"))
+    assert res["trajectories"] == len(files) == 4 * len(res["configs"])   # 48 episodes per config: 10..40
+    by_total = {int(r["episode_num"]): r for r in rows}
+    for fp in files:
+        z = np.load(fp, allow_pickle=True)    # written by this test, an object array as the reference's
+        steps, ep, total, N = int(z["steps"]), int(z["episode"]), int(z["total_episode"]), int(z["N"])
+        assert ep % 10 == 0 and len(z["positions"]) == steps
+        r = by_total[total]
+        assert int(r["steps"]) == steps and int(r["N"]) == N
+        assert all(q.shape[1] == 2 and len(q) <= N for q in z["positions"])
+        assert len(z["positions"][-1]) == 0 or steps == 60
 
 
 # model/ffm_unified.py critic_only on the 12x12 room with run_unified_critic_training.py's
