@@ -97,16 +97,28 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+// Dense tables: the slot is the key and an absent slot already holds the default,
+// so a caller may load the values together with the presence word (not after it)
+// and insert afterwards.  Presence is one bit of a 2 MB-scale bitmap that stays in
+// L2; the key is stored for export only.
+__device__ __forceinline__ void dense_ensure(const LearnTable& T, uint32_t h, unsigned long long key) {
+    const uint32_t bit = 1u << (h & 31);
+    uint32_t* w = T.present + (h >> 5);
+    if (*w & bit) return;                                 // stale 0 only costs the atomic
+    if (atomicOr(w, bit) & bit) return;
+    tkey(T, h) = key;
+    T.order[wave_claim(T.n)] = h;
+}
+
+// The slot whose values a lookup reads: dense tables need no load for it.
+__device__ __forceinline__ uint32_t first_slot(const LearnTable& T, unsigned long long key) {
+    return T.dense_by ? dense_slot(key, T) : (uint32_t)mix64(key) & T.mask;
+}
+
 __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflow) {
     if (T.dense_by) {
-        // The slot is the key: presence is one bit of a 2 MB-scale bitmap that stays
-        // in L2, so a lookup touches no key line (the key is stored for export only).
-        const uint32_t h = dense_slot(key, T), bit = 1u << (h & 31);
-        uint32_t* w = T.present + (h >> 5);
-        if (*w & bit) return (int)h;                    // stale 0 only costs the atomic
-        if (atomicOr(w, bit) & bit) return (int)h;
-        tkey(T, h) = key;
-        T.order[wave_claim(T.n)] = h;
+        const uint32_t h = dense_slot(key, T);
+        dense_ensure(T, h, key);
         return (int)h;
     }
     uint32_t h = (uint32_t)mix64(key) & T.mask;
@@ -1005,6 +1017,12 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 #ifndef FFM_SMALL_EPB
 #define FFM_SMALL_EPB 8
 #endif
+#ifndef FFM_RASTER
+#define FFM_RASTER 1   // large-map learner: lanes walk the agents in cell-raster order (A/B switch)
+#endif
+#ifndef FFM_PREF
+#define FFM_PREF 0     // large-map learner: touch pass over every agent's lines first (A/B switch)
+#endif
 #ifndef FFM_LABLATE
 #define FFM_LABLATE 0
 #endif
@@ -1128,12 +1146,55 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
     for (int c = tid; c < A * D; c += LPE) req[c] = kNone16;
     __syncthreads();
-    int p[APT];
+    // Lane slot j of this thread is rank r = tid + j * LPE.  By default rank = agent
+    // index; RASTER (global-memory DFF, >= one wave per env) instead hands rank r to
+    // the r-th occupied cell in raster order, so the 64 agents of a wave stand on a
+    // few neighbouring rows: their DFF lines, and the records of equal rank patterns
+    // (rank-major dense slots), are shared instead of ~10 distinct lines per agent.
+    // The agent index (owner priority, Philox keys, order-preserving compaction)
+    // is then read back from the grid.
+    constexpr bool RASTER = FFM_RASTER && !DL && LPE >= 64 && EPB == 1;
+    int p[APT], ia[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;
         p[j] = i < n ? a.pos[e * A + i] : 0;
+        ia[j] = i;
         if (i < n) grid[p[j]] = (uint16_t)i;
+    }
+    if (RASTER) {
+        __syncthreads();
+        // wave w of the env lists cells [w * cpw, (w + 1) * cpw) in two passes
+        // (count, then place) of 64 consecutive cells per round; the list lives in req
+        // (A * D >= n entries) until decide overwrites it.
+        constexpr int NW = LPE / 64;
+        const int w = tid >> 6, lane = tid & 63;
+        const int cpw = ((HW + NW * 64 - 1) / (NW * 64)) * 64;
+        const int c0 = w * cpw, c1 = min(c0 + cpw, HW);
+        int cnt = 0;
+        for (int c = c0 + lane; c - lane < c1; c += 64)
+            cnt += __popcll(__ballot(c < c1 && grid[c] != kNone16));
+        if (lane == 0) ws[w] = cnt;
+        __syncthreads();
+        int base = 0;
+#pragma unroll
+        for (int q = 0; q < NW; q++) base += q < w ? ws[q] : 0;
+        for (int c = c0 + lane; c - lane < c1; c += 64) {
+            const bool f = c < c1 && grid[c] != kNone16;
+            const unsigned long long m = __ballot(f);
+            if (f) req[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)c;
+            base += __popcll(m);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < APT; j++) {
+            const int r = tid + j * LPE;
+            p[j] = r < n ? req[r] : 0;
+            ia[j] = r < n ? grid[p[j]] : r;
+        }
+        __syncthreads();   // the list is read: decide may write req
+        for (int c = tid; c < n; c += LPE) req[c] = kNone16;
+        __syncthreads();
     }
     const bool trained = a.variant == kVarTrained;
     const double eps = live && actor ? env_epsilon(a, a.episodes[e]) : 0.0;
@@ -1152,13 +1213,30 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     // ---- decide --------------------------------------------------------------
     unsigned long long skey[APT];
     int act[APT], avalid[APT], wexit[APT], hsl[APT];
+    // Several agents per lane with the DFF in global memory: first every agent's
+    // state key, and one load into each line its decide will read (the H record,
+    // the DFF rows x-1..x+1), so that the lines of all APT agents are in flight
+    // together; the decide loop below then finds them in L2 instead of paying one
+    // dependent HBM round trip per agent.
+    constexpr bool PREF = FFM_PREF && !DL && APT > 1;
+    uint32_t sink = 0;
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * LPE;
-        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
-        if (i >= n) continue;
+        skey[j] = 0;
+        if (!PREF || tid + j * LPE >= n) continue;
         const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
         skey[j] = encode(a, smc, x, y);
+        if (actor || trained) sink ^= (uint32_t)tkey(a.Ht, first_slot(a.Ht, skey[j]));
+        const float* d = dff + p[j];
+        sink ^= __float_as_uint(d[0]) ^ (x > 0 ? __float_as_uint(d[-W]) : 0u) ^ (x + 1 < H ? __float_as_uint(d[W]) : 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = ia[j];
+        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1;
+        if (tid + j * LPE >= n) continue;
+        const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
+        if (!PREF) skey[j] = encode(a, smc, x, y);
         int coord[5], valid[5], inb[5];
         moves5(a, x, y, occ, coord, valid, inb);
         int ex = -1;                               // first exit among the neighbours
@@ -1197,6 +1275,10 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                     trained_policy(a, tab_find(a.Ht, skey[j]), coord, valid, dff, hs, P);
                 } else if (!actor) {
                     critic_policy(a, coord, valid, dff, P);
+                } else if (a.Ht.dense_by) {
+                    hsl[j] = (int)dense_slot(skey[j], a.Ht);
+                    actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, false, P);
+                    dense_ensure(a.Ht, (uint32_t)hsl[j], skey[j]);
                 } else {
                     hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
                     if (hsl[j] < 0) continue;
@@ -1240,9 +1322,9 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     int nxt[APT], coll[APT], wins[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * LPE;
+        const int i = ia[j];
         nxt[j] = p[j]; coll[j] = -1; wins[j] = 0;
-        if (i >= n) continue;
+        if (tid + j * LPE >= n) continue;
         int best_owner = -1, best_won_owner = -1;
 #pragma unroll
         for (int d = 0; d < D; d++) {
@@ -1282,8 +1364,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     // agent's next cell joins the next state map unless it is an exit
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * LPE;
-        if (i >= n) continue;
+        if (tid + j * LPE >= n) continue;
         if (wins[j]) {
             float* c = dff + p[j];
             float v = *c;
@@ -1297,9 +1378,20 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
 
     // ---- learning (TD(0) critic, actor) --------------------------------------------------
     const SmBits smn{a.map2, bits};
+    // as in decide: the next-state keys first and one load into each V record line
+    // (s' and s) of every agent, then the TD updates
+    unsigned long long nkey[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = tid + j * LPE;
+        nkey[j] = 0;
+        if (!PREF || tid + j * LPE >= n || trained || wexit[j]) continue;
+        const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
+        nkey[j] = encode(a, smn, nx, ny);
+        sink ^= (uint32_t)tkey(a.V, first_slot(a.V, nkey[j])) ^ (uint32_t)tkey(a.V, first_slot(a.V, skey[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < APT; j++) {
+        const int i = tid + j * LPE;   // recs in lane-rank order: the post kernel inherits the locality
         if (i >= n || trained || (FFM_LABLATE & 2)) continue;
         double r = a.step_penalty;
         if (wexit[j]) r = r + a.exit_reward;
@@ -1307,17 +1399,32 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         int sn = -1;
         double vn = 0.0;
         if (!wexit[j]) {
-            const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
-            sn = tab_get(a.V, encode(a, smn, nx, ny), a.overflow);
-            vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
+            if (!PREF) {
+                const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
+                nkey[j] = encode(a, smn, nx, ny);
+            }
+            if (a.V.dense_by) {
+                sn = (int)dense_slot(nkey[j], a.V);
+                vn = tval(a.V, sn)[0];
+                dense_ensure(a.V, (uint32_t)sn, nkey[j]);
+            } else {
+                sn = tab_get(a.V, nkey[j], a.overflow);
+                vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
+            }
         }
-        const int sv = tab_get(a.V, skey[j], a.overflow);
+        int sv;
+        if (a.V.dense_by) {
+            sv = (int)dense_slot(skey[j], a.V);
+            dense_ensure(a.V, (uint32_t)sv, skey[j]);
+        } else {
+            sv = tab_get(a.V, skey[j], a.overflow);
+        }
         if (sv < 0) continue;
         const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
         if (!(FFM_LABLATE & 1)) acc_add(a.V.acc + sv, fx(a.alpha_v * td));
         if (!actor) continue;
         if (act[j] < 0) continue;
-        if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+        if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
         if (hsl[j] < 0) continue;
         if (post_update) {
             LearnRec rc;
@@ -1331,14 +1438,33 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     LSTAMP(4);
     // ---- exit removal (order preserving), counters ---------------------------------------
     int base_ = 0;
+    if (RASTER) {
+        // back to agent order for the order-preserving compaction: next cells by agent
+        // index through req (resolve's last read of it is behind the barrier above)
 #pragma unroll
-    for (int j = 0; j < APT; j++) {
-        const int i = tid + j * LPE;
-        const bool keep = i < n && map2_at(a.map2, nxt[j]) != 3;
-        int tot;
-        const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
-        if (keep) a.pos[e * A + base_ + off] = (uint16_t)nxt[j];
-        base_ += tot;
+        for (int j = 0; j < APT; j++)
+            if (tid + j * LPE < n) req[ia[j]] = map2_at(a.map2, nxt[j]) != 3 ? (uint16_t)nxt[j] : kNone16;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < APT; j++) {
+            const int i = tid + j * LPE;
+            const int c = i < n ? req[i] : kNone16;
+            const bool keep = c != kNone16;
+            int tot;
+            const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
+            if (keep) a.pos[e * A + base_ + off] = (uint16_t)c;
+            base_ += tot;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < APT; j++) {
+            const int i = tid + j * LPE;
+            const bool keep = i < n && map2_at(a.map2, nxt[j]) != 3;
+            int tot;
+            const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
+            if (keep) a.pos[e * A + base_ + off] = (uint16_t)nxt[j];
+            base_ += tot;
+        }
     }
     __syncthreads();     // deposits visible to the whole workgroup before the stencil
     LSTAMP(5);
@@ -1366,6 +1492,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                ts_[1] - ts_[0], ts_[2] - ts_[1], ts_[3] - ts_[2], ts_[4] - ts_[3], ts_[5] - ts_[4], ts_[6] - ts_[5]);
 
 #endif
+    if (PREF && sink == 0x9E3779B9u && a.t == 0xFFFFFFFFu) atomicOr(a.overflow, 4);   // keeps the touch loads (bit 2: unused)
     if (live && tid == 0) {
         a.cnt[e] = base_;
         a.nstart[e] = n;
@@ -1551,9 +1678,6 @@ __global__ __launch_bounds__(256) void learn_clear_kernel(LearnTable T, int widt
     }
 }
 
-// Philox placement (DESIGN.md 3.2): the N free cells with the smallest
-// (key_j, j), in that order.  Candidates (all F, or those under a threshold
-// chosen so that N <= expected count << capacity) are bitonic-sorted in LDS.
 // Trajectory capture (model/ffm_unified.py:902-931 run(return_trajectory=True): the
 // positions after every step; run_actor_only_training.py:199-218 keeps one every 100th
 // episode).  One workgroup per selected env, after the step and before the auto-reset
@@ -1580,6 +1704,9 @@ __global__ __launch_bounds__(256) void learn_capture_kernel(LearnArgs a, TrajCap
         c.cells[row * a.A + i] = i < n ? a.pos[e * a.A + i] : kNone16;
 }
 
+// Philox placement (DESIGN.md 3.2): the N free cells with the smallest
+// (key_j, j), in that order.  Candidates (all F, or those under a threshold
+// chosen so that N <= expected count << capacity) are bitonic-sorted in LDS.
 constexpr int kResetBS = 256;
 constexpr int kResetCap = 16384;
 
