@@ -64,6 +64,8 @@ def parse():
                     help="timed regions of K steps each, back to back; value = their median (BASELINE.md 3)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--log2-table", type=int, default=0, help="learner V/H hash capacity (0 = engine default)")
+    ap.add_argument("--sync-period", type=int, default=1,
+                    help="learner configs: apply / exchange the tables every K steps (1 = the reference's per-step)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (default: profiles/traffic_<H>x<W>_A<A>_E<E>.json)")
     a = ap.parse_args()
@@ -285,9 +287,10 @@ def bench_learner(args, world, rank, torch, dist):
     if world > 1:
         # the ranks share V / H: every step exchanges the table deltas over RCCL
         from ffm_amd.dist import TableSync
-        sync = TableSync(L, device="cuda", capacity=1 << 18)
+        sync = TableSync(L, device="cuda", capacity=1 << 17, sync_period=args.sync_period)
         run = sync.step
     else:
+        L.set_sync_period(args.sync_period)
         run = lambda k: L.step(k, stream)  # noqa: E731
     run(args.warmup)
     torch.cuda.synchronize()
@@ -325,7 +328,8 @@ def bench_learner(args, world, rank, torch, dist):
                 "workload": (f"config {args.config}: {cfg['variant']}"
                              f"{'/' + cfg['mode'] if cfg['mode'] else ''} learning step, {H}x{W} room, "
                              f"{A} agents/env, {E} envs/GPU, epsilon {cfg['params']['epsilon']}, "
-                             f"max_steps {cfg['max_steps']}, Philox seed {args.seed}, on-device auto-reset"),
+                             f"max_steps {cfg['max_steps']}, Philox seed {args.seed}, on-device auto-reset"
+                             + (f", tables applied every {args.sync_period} steps" if args.sync_period > 1 else "")),
                 "map": f"{H}x{W}", "agents_per_env": A, "envs_per_gpu": E, "global_envs": E * world,
                 "parallelism": f"env-sharded x{world}",
             },
@@ -334,6 +338,10 @@ def bench_learner(args, world, rank, torch, dist):
             "repeats": reps["summary"],
             "step_ms_events": step_ms,
             "tables": {"V": v_size, "H": h_size},
+            "table_sync": ({"period": args.sync_period, "mode": "dense all-reduce" if sync.dense else "records",
+                            "bytes_per_rank_per_step": sync.bytes_sent / max(1, args.warmup + reps["summary"]["n"]
+                                                                           * args.steps + nk)}
+                           if world > 1 else {"period": args.sync_period}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "traffic_kernel": "learn_batch_kernel (PMC FETCH_SIZE x2 + WRITE_SIZE)",

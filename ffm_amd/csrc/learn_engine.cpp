@@ -80,6 +80,8 @@ struct ffm_learner {
     long long eplog_cap = 0;
     int F_all = 0;                           // free cells of the map (placement capacity)
     ffm::TrajCapture traj{};                 // trajectory capture (n_sel = 0: off)
+    int sync_period = 1;                     // tables applied every sync_period-th step
+    int since_apply = 0;                     // steps since the last apply
     DevTable V, H;
 };
 
@@ -181,6 +183,7 @@ static int check_overflow(ffm_learner* l, hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
     if (ov & 1) return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
     if (ov & 2) return fail(FFM_E_HIP, "placement candidate list out of range (reset)");
+    if (ov & 4) return fail(FFM_E_INVALID, "asynchronous delta export: record buffer too small (raise its capacity)");
     return FFM_OK;
 }
 
@@ -404,20 +407,29 @@ static int phase_local(ffm_learner* l, hipStream_t s) {
     return FFM_OK;
 }
 
+// With a sync period K > 1 the increments of K steps accumulate and the tables
+// (and the H statistics) change only at every K-th step's apply; the post-update
+// actor increments of the other steps use the V of the last apply.
+static bool apply_due(const ffm_learner* l) { return l->since_apply + 1 >= l->sync_period; }
+
 static int phase_apply(ffm_learner* l, int32_t which, hipStream_t s) {
+    const bool due = apply_due(l);
     if (which == FFM_TABLE_V) {
-        if (!l->trained) HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
+        if (!l->trained && due) HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
         if (l->post_update) HIP_TRY(ffm::launch_learn_post(make_args(l), s));
         l->phase = 2;
         return FFM_OK;
     }
-    HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
-    l->hstat_valid = true;
+    if (due) {
+        HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
+        l->hstat_valid = true;
+    }
     l->phase = 3;
     return FFM_OK;
 }
 
 static int phase_end(ffm_learner* l, hipStream_t s) {
+    l->since_apply = apply_due(l) ? 0 : l->since_apply + 1;
     HIP_TRY(ffm::launch_learn_capture(make_args(l), l->traj, s));   // before the reset re-places
     l->cur ^= 1;
     if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
@@ -435,6 +447,8 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
     // here (every sync point -- counters, export, get_state -- reports it exactly).
     if (l->h_overflow && (__atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) & 1))
         return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
+    if (l->h_overflow && (__atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) & 4))
+        return fail(FFM_E_INVALID, "asynchronous delta export: record buffer too small (raise its capacity)");
     for (int i = 0; i < n_steps; i++) {
         if (l->mt) {
             HIP_TRY(ffm::launch_learn_exact(make_args(l), s));
@@ -769,6 +783,72 @@ int ffm_learner_drain_episodes(ffm_learner* l, int32_t* records, int64_t cap, in
     HIP_TRY(hipStreamSynchronize(s));
     *n = have;
     if (dropped) *dropped = (int64_t)c - have;
+    return FFM_OK;
+}
+
+int ffm_learner_delta_export_async(ffm_learner* l, int32_t which, uint64_t* d_keys, int64_t* d_acc, int64_t cap,
+                                   int64_t* d_count, void* stream) {
+    if (!l || !d_count) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if (l->phase == 0) return fail(FFM_E_INVALID, "delta_export outside a phased step");
+    if (cap > 0 && (!d_keys || !d_acc)) return fail(FFM_E_INVALID, "null record buffers");
+    hipStream_t s = (hipStream_t)stream;
+    auto* cnt = reinterpret_cast<unsigned long long*>(d_count);
+    HIP_TRY(hipMemsetAsync(cnt, 0, 8, s));
+    HIP_TRY(ffm::launch_learn_delta_export(T->t, T->width, reinterpret_cast<unsigned long long*>(d_keys),
+                                           reinterpret_cast<long long*>(d_acc), cap, cnt, s));
+    HIP_TRY(ffm::launch_learn_delta_check(cnt, cap, l->d_overflow, s));
+    return FFM_OK;
+}
+
+int ffm_learner_delta_merge_async(ffm_learner* l, int32_t which, const uint64_t* d_keys, const int64_t* d_acc,
+                                  const int64_t* d_count, int64_t cap, void* stream) {
+    if (!l || !d_count || cap < 0) return fail(FFM_E_INVALID, "bad argument");
+    DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if (l->phase == 0) return fail(FFM_E_INVALID, "delta_merge outside a phased step");
+    HIP_TRY(ffm::launch_learn_delta_merge(T->t, T->width, reinterpret_cast<const unsigned long long*>(d_keys),
+                                          reinterpret_cast<const long long*>(d_acc), cap, l->d_overflow,
+                                          (hipStream_t)stream, reinterpret_cast<const long long*>(d_count)));
+    return FFM_OK;
+}
+
+int ffm_learner_set_sync_period(ffm_learner* l, int32_t period) {
+    if (!l || period < 1) return fail(FFM_E_INVALID, "sync period must be >= 1");
+    if (l->mt && period != 1) return fail(FFM_E_INVALID, "the exact (MT) step applies every step");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    l->sync_period = period;
+    l->since_apply = 0;
+    return FFM_OK;
+}
+
+int ffm_learner_apply_due(ffm_learner* l, int32_t* due) {
+    if (!l || !due) return fail(FFM_E_INVALID, "null argument");
+    *due = apply_due(l) ? 1 : 0;
+    return FFM_OK;
+}
+
+int ffm_learner_dense_buffers(ffm_learner* l, int32_t which, int64_t** d_acc, int64_t* acc_count,
+                              uint32_t** d_present, int64_t* present_words) {
+    if (!l || !d_acc || !acc_count || !d_present || !present_words) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && (l->actor || l->trained) ? &l->H : nullptr);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if (!T->t.dense_by) return fail(FFM_E_UNSUPPORTED, "not a dense (rank-key) table");
+    *d_acc = reinterpret_cast<int64_t*>(T->t.acc);
+    *acc_count = (int64_t)(T->cap * (size_t)T->width);
+    *d_present = T->t.present;
+    *present_words = (int64_t)(T->cap / 32);
+    return FFM_OK;
+}
+
+int ffm_learner_dense_adopt(ffm_learner* l, int32_t which, const uint32_t* d_union, void* stream) {
+    if (!l || !d_union) return fail(FFM_E_INVALID, "null argument");
+    DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
+    if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
+    if (!T->t.dense_by) return fail(FFM_E_UNSUPPORTED, "not a dense (rank-key) table");
+    if (l->phase == 0) return fail(FFM_E_INVALID, "dense_adopt outside a phased step");
+    HIP_TRY(ffm::launch_learn_dense_adopt(T->t, d_union, (hipStream_t)stream));
     return FFM_OK;
 }
 

@@ -114,7 +114,10 @@ hipError_t launch_learn_clear(const LearnTable& T, int width, double dflt, hipSt
 hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
                                     long long cap, unsigned long long* count, hipStream_t s);
 hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsigned long long* keys,
-                                   const long long* acc, long long n, int* overflow, hipStream_t s);
+                                   const long long* acc, long long n, int* overflow, hipStream_t s,
+                                   const long long* dn = nullptr);
+hipError_t launch_learn_delta_check(const unsigned long long* count, long long cap, int* overflow, hipStream_t s);
+hipError_t launch_learn_dense_adopt(const LearnTable& T, const uint32_t* uni, hipStream_t s);
 hipError_t launch_learn_import(const LearnTable& T, int width, const unsigned long long* keys, const double* vals,
                               long long n, int* overflow, hipStream_t s);
 

@@ -110,10 +110,6 @@ __device__ __forceinline__ void dense_ensure(const LearnTable& T, uint32_t h, un
     T.order[wave_claim(T.n)] = h;
 }
 
-// The slot whose values a lookup reads: dense tables need no load for it.
-__device__ __forceinline__ uint32_t first_slot(const LearnTable& T, unsigned long long key) {
-    return T.dense_by ? dense_slot(key, T) : (uint32_t)mix64(key) & T.mask;
-}
 
 __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflow) {
     if (T.dense_by) {
@@ -1020,9 +1016,6 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 #ifndef FFM_RASTER
 #define FFM_RASTER 1   // large-map learner: lanes walk the agents in cell-raster order (A/B switch)
 #endif
-#ifndef FFM_PREF
-#define FFM_PREF 0     // large-map learner: touch pass over every agent's lines first (A/B switch)
-#endif
 #ifndef FFM_LABLATE
 #define FFM_LABLATE 0
 #endif
@@ -1213,30 +1206,13 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
     // ---- decide --------------------------------------------------------------
     unsigned long long skey[APT];
     int act[APT], avalid[APT], wexit[APT], hsl[APT];
-    // Several agents per lane with the DFF in global memory: first every agent's
-    // state key, and one load into each line its decide will read (the H record,
-    // the DFF rows x-1..x+1), so that the lines of all APT agents are in flight
-    // together; the decide loop below then finds them in L2 instead of paying one
-    // dependent HBM round trip per agent.
-    constexpr bool PREF = FFM_PREF && !DL && APT > 1;
-    uint32_t sink = 0;
-#pragma unroll
-    for (int j = 0; j < APT; j++) {
-        skey[j] = 0;
-        if (!PREF || tid + j * LPE >= n) continue;
-        const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
-        skey[j] = encode(a, smc, x, y);
-        if (actor || trained) sink ^= (uint32_t)tkey(a.Ht, first_slot(a.Ht, skey[j]));
-        const float* d = dff + p[j];
-        sink ^= __float_as_uint(d[0]) ^ (x > 0 ? __float_as_uint(d[-W]) : 0u) ^ (x + 1 < H ? __float_as_uint(d[W]) : 0u);
-    }
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = ia[j];
-        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1;
+        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
         if (tid + j * LPE >= n) continue;
         const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
-        if (!PREF) skey[j] = encode(a, smc, x, y);
+        skey[j] = encode(a, smc, x, y);
         int coord[5], valid[5], inb[5];
         moves5(a, x, y, occ, coord, valid, inb);
         int ex = -1;                               // first exit among the neighbours
@@ -1378,17 +1354,6 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
 
     // ---- learning (TD(0) critic, actor) --------------------------------------------------
     const SmBits smn{a.map2, bits};
-    // as in decide: the next-state keys first and one load into each V record line
-    // (s' and s) of every agent, then the TD updates
-    unsigned long long nkey[APT];
-#pragma unroll
-    for (int j = 0; j < APT; j++) {
-        nkey[j] = 0;
-        if (!PREF || tid + j * LPE >= n || trained || wexit[j]) continue;
-        const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
-        nkey[j] = encode(a, smn, nx, ny);
-        sink ^= (uint32_t)tkey(a.V, first_slot(a.V, nkey[j])) ^ (uint32_t)tkey(a.V, first_slot(a.V, skey[j]));
-    }
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;   // recs in lane-rank order: the post kernel inherits the locality
@@ -1399,16 +1364,14 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         int sn = -1;
         double vn = 0.0;
         if (!wexit[j]) {
-            if (!PREF) {
-                const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
-                nkey[j] = encode(a, smn, nx, ny);
-            }
+            const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
+            const unsigned long long nk = encode(a, smn, nx, ny);
             if (a.V.dense_by) {
-                sn = (int)dense_slot(nkey[j], a.V);
+                sn = (int)dense_slot(nk, a.V);
                 vn = tval(a.V, sn)[0];
-                dense_ensure(a.V, (uint32_t)sn, nkey[j]);
+                dense_ensure(a.V, (uint32_t)sn, nk);
             } else {
-                sn = tab_get(a.V, nkey[j], a.overflow);
+                sn = tab_get(a.V, nk, a.overflow);
                 vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
             }
         }
@@ -1492,7 +1455,6 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
                ts_[1] - ts_[0], ts_[2] - ts_[1], ts_[3] - ts_[2], ts_[4] - ts_[3], ts_[5] - ts_[4], ts_[6] - ts_[5]);
 
 #endif
-    if (PREF && sink == 0x9E3779B9u && a.t == 0xFFFFFFFFu) atomicOr(a.overflow, 4);   // keeps the touch loads (bit 2: unused)
     if (live && tid == 0) {
         a.cnt[e] = base_;
         a.nstart[e] = n;
@@ -1791,7 +1753,7 @@ __global__ __launch_bounds__(256) void learn_delta_export_kernel(LearnTable T, u
         }
         if (!touched) continue;
         const unsigned long long r = atomicAdd(count, 1ull);
-        if ((long long)r >= cap) continue;
+        if ((long long)r >= cap) continue;     // the caller checks *count against cap
         keys[r] = tkey(T, s);
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) acc[r * WIDTH + k] = q[k];
@@ -1799,9 +1761,12 @@ __global__ __launch_bounds__(256) void learn_delta_export_kernel(LearnTable T, u
 }
 
 // Another rank's records: insert missing keys (default values), add increments.
+// dn: the record count on the device (asynchronous exchange, capped at n); else n.
 template <int WIDTH>
 __global__ __launch_bounds__(256) void learn_delta_merge_kernel(LearnTable T, const unsigned long long* keys,
-                                                                const long long* acc, long long n, int* overflow) {
+                                                                const long long* acc, long long n, int* overflow,
+                                                                const long long* dn) {
+    if (dn) n = min(n, *dn);
     for (long long r = (long long)blockIdx.x * 256 + threadIdx.x; r < n; r += (long long)gridDim.x * 256) {
         const int s = tab_get(T, keys[r], overflow);
         if (s < 0) continue;
@@ -1809,6 +1774,30 @@ __global__ __launch_bounds__(256) void learn_delta_merge_kernel(LearnTable T, co
         for (int k = 0; k < WIDTH; k++) {
             const long long q = acc[r * WIDTH + k];
             if (q != 0) acc_add(T.acc + (size_t)s * WIDTH + k, q);
+        }
+    }
+}
+
+// Asynchronous export: record buffer overflow is flagged for the next sync point.
+__global__ void learn_delta_check_kernel(const unsigned long long* count, long long cap, int* overflow) {
+    if (threadIdx.x == 0 && (long long)*count > cap) atomicOr(overflow, 4);
+}
+
+// Dense tables after an all-reduce of the increments: adopt the presence union of
+// every rank (slots another rank inserted get their key and an insertion index).
+__global__ __launch_bounds__(256) void learn_dense_adopt_kernel(LearnTable T, const uint32_t* uni) {
+    const size_t words = ((size_t)T.mask + 1) / 32;
+    for (size_t w = (size_t)blockIdx.x * 256 + threadIdx.x; w < words; w += (size_t)gridDim.x * 256) {
+        uint32_t nw = uni[w] & ~T.present[w];
+        if (!nw) continue;
+        T.present[w] |= nw;
+        while (nw) {
+            const uint32_t h = (uint32_t)(w * 32) + (uint32_t)__builtin_ctz(nw);
+            nw &= nw - 1u;
+            const uint32_t sh = (uint32_t)__builtin_ctz((T.mask + 1) >> 8);
+            const uint32_t rem = h & ((1u << sh) - 1u), bx = rem / T.dense_by, by = rem - bx * T.dense_by;
+            tkey(T, h) = (unsigned long long)(h >> sh) | ((unsigned long long)bx << 26) | ((unsigned long long)by << 45);
+            T.order[atomicAdd(T.n, 1u)] = h;
         }
     }
 }
@@ -2062,11 +2051,24 @@ hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned lo
 }
 
 hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsigned long long* keys,
-                                   const long long* acc, long long n, int* overflow, hipStream_t s) {
+                                   const long long* acc, long long n, int* overflow, hipStream_t s,
+                                   const long long* dn) {
     if (n <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)std::min<long long>(4096, (n + 255) / 256);
-    if (width == 1) learn_delta_merge_kernel<1><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow);
-    else learn_delta_merge_kernel<5><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow);
+    if (width == 1) learn_delta_merge_kernel<1><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
+    else learn_delta_merge_kernel<5><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_delta_check(const unsigned long long* count, long long cap, int* overflow, hipStream_t s) {
+    learn_delta_check_kernel<<<dim3(1), dim3(64), 0, s>>>(count, cap, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_dense_adopt(const LearnTable& T, const uint32_t* uni, hipStream_t s) {
+    const size_t words = ((size_t)T.mask + 1) / 32;
+    const unsigned blocks = (unsigned)std::min<size_t>(2048, (words + 255) / 256);
+    learn_dense_adopt_kernel<<<dim3(blocks), dim3(256), 0, s>>>(T, uni);
     return hipGetLastError();
 }
 

@@ -61,100 +61,117 @@ def reduce_max(x: float, device=None, group=None) -> float:
 # ---------------------------------------------------------------------------
 # Learning variants: the tables are shared by every env of every rank
 # ---------------------------------------------------------------------------
-def all_gather_varlen(keys: torch.Tensor, acc: torch.Tensor, n: int, group=None):
-    """All-gather each rank's first ``n`` records (keys [cap], acc [cap, width]).
-
-    Counts first, then the records padded to the longest list (one collective
-    per array; RCCL on device tensors, gloo on host tensors).  Returns
-    (counts, keys [world, m], acc [world, m, width]) with m = max(counts)."""
-    world = dist.get_world_size(group)
-    cnt = torch.tensor([int(n)], dtype=torch.int64, device=keys.device)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
-    m = max(counts)
-    if m == 0:
-        return counts, None, None
-    if m > keys.shape[0]:
-        raise ValueError(f"record buffers hold {keys.shape[0]} < {m}")
-    ks = [torch.empty_like(keys[:m]) for _ in range(world)]
-    acs = [torch.empty_like(acc[:m]) for _ in range(world)]
-    dist.all_gather(ks, keys[:m].contiguous(), group=group)
-    dist.all_gather(acs, acc[:m].contiguous(), group=group)
-    return counts, torch.stack(ks), torch.stack(acs)
-
-
 class TableSync:
     """The batched learning step of one rank's shard, with the V / H table deltas
-    exchanged so every rank ends each step with the tables a single device
+    exchanged so every rank ends each sync step with the tables a single device
     holding all envs would have.
 
-    ``shard`` is an ``ffm_amd.engine.Learner`` (records on its device, RCCL) or
-    anything with the same phase interface (tests drive the CPU restatement
-    through gloo).  Increments are integers (2^-32 fixed point), so the merged sum
-    does not depend on rank or arrival order: sharded == single device, bit for bit.
+    ``shard`` is an ``ffm_amd.engine.Learner`` (buffers on its device, RCCL) or
+    anything with the same phase interface (tests drive the CPU restatement through
+    gloo).  Increments are integers (2^-32 fixed point), so the merged sum does not
+    depend on rank or arrival order: sharded == single device, bit for bit, in table
+    values (hashed tables' insertion order -- the dict order of get_v_table /
+    get_h_table -- differs between ranks).
+
+    No host synchronisation inside the step loop: the record counts stay on the
+    device (fixed-capacity record buffers, ``capacity`` records per rank and table;
+    a step that touches more is reported as an error at the next sync point).
+
+    * ``dense`` (default: the shard's tables are dense, i.e. ffm_unified): the whole
+      fixed-point accumulator array is all-reduced (SUM; RCCL runs it as
+      reduce-scatter + all-gather) and the presence bitmaps are OR-ed, instead of
+      exporting touched records;
+    * ``sync_period`` K: the tables are applied (and exchanged) every K-th step only,
+      the increments of K steps accumulating in between
+      (``Learner.set_sync_period``); K = 1 is the reference's per-step update.
     """
 
-    def __init__(self, shard, group=None, device=None, capacity: int = 1 << 16):
+    def __init__(self, shard, group=None, device=None, capacity: int = 1 << 16, sync_period: int = 1,
+                 dense: bool | None = None):
         self.shard = shard
         self.group = group
         self.device = device
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.bufs = {}
         self.capacity = int(capacity)
-        self.records_sent = 0
+        self.sync_period = int(sync_period)
+        shard.set_sync_period(self.sync_period)
+        self.dense = bool(getattr(shard, "dense_tables", False)) if dense is None else bool(dense)
+        self.bufs = {}
+        self.bytes_sent = 0          # per rank, summed over exchanges (what this rank contributes)
+        self.exchanges = 0
 
-    def _buffers(self, which: str, cap: int):
-        width = 1 if which == "V" else 5
+    def _record_buffers(self, which: str):
         b = self.bufs.get(which)
-        if b is None or b[0].shape[0] < cap:
-            b = (torch.empty(cap, dtype=torch.int64, device=self.device),
-                 torch.empty((cap, width), dtype=torch.int64, device=self.device))
+        if b is None:
+            width, cap, w, dev = (1 if which == "V" else 5), self.capacity, self.world, self.device
+            b = (torch.zeros(cap, dtype=torch.int64, device=dev),
+                 torch.zeros((cap, width), dtype=torch.int64, device=dev),
+                 torch.zeros(1, dtype=torch.int64, device=dev),
+                 torch.zeros((w, cap), dtype=torch.int64, device=dev),
+                 torch.zeros((w, cap, width), dtype=torch.int64, device=dev),
+                 torch.zeros(w, dtype=torch.int64, device=dev))
             self.bufs[which] = b
         return b
 
-    def _exchange(self, which: str):
-        keys, acc = self._buffers(which, self.capacity)
-        n = self.shard.delta_export(which, keys.data_ptr(), acc.data_ptr(), keys.shape[0])
-        m = torch.tensor([n], dtype=torch.int64, device=self.device)
-        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)      # every rank holds the longest list
-        m = int(m.item())
-        if m > keys.shape[0]:
-            self.capacity = max(m, 2 * self.capacity)
-            keys, acc = self._buffers(which, self.capacity)
-            n = self.shard.delta_export(which, keys.data_ptr(), acc.data_ptr(), keys.shape[0])
-        counts, gk, ga = all_gather_varlen(keys, acc, n, self.group)
-        self.records_sent += n
+    def _exchange_records(self, which: str):
+        keys, acc, cnt, gk, ga, gc = self._record_buffers(which)
+        cap = keys.shape[0]
+        self.shard.delta_export_async(which, keys.data_ptr(), acc.data_ptr(), cap, cnt.data_ptr())
+        dist.all_gather([gc[r:r + 1] for r in range(self.world)], cnt, group=self.group)
+        dist.all_gather([gk[r] for r in range(self.world)], keys, group=self.group)
+        dist.all_gather([ga[r] for r in range(self.world)], acc, group=self.group)
         for r in range(self.world):
-            if r == self.rank or counts[r] == 0:
-                continue
-            kr, ar = gk[r].contiguous(), ga[r].contiguous()
-            self.shard.delta_merge(which, kr.data_ptr(), ar.data_ptr(), counts[r])
-            self._keep = (kr, ar)      # alive until the merge has consumed them
+            if r != self.rank:
+                self.shard.delta_merge_async(which, gk[r].data_ptr(), ga[r].data_ptr(), gc[r:r + 1].data_ptr(), cap)
+        self.bytes_sent += 8 + keys.numel() * 8 + acc.numel() * 8
+
+    def _exchange_dense(self, which: str):
+        acc, present = self.shard.dense_buffers(which)
+        dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
+        g = self.bufs.get(("present", which))
+        if g is None:
+            g = torch.empty((self.world, present.numel()), dtype=present.dtype, device=present.device)
+            self.bufs[("present", which)] = g
+        dist.all_gather([g[r] for r in range(self.world)], present, group=self.group)
+        uni = g[0].clone()
+        for r in range(1, self.world):
+            uni.bitwise_or_(g[r])
+        self.shard.dense_adopt(which, uni.data_ptr())
+        self._keep = uni                 # until the adopt kernel (same stream) has read it
+        self.bytes_sent += acc.numel() * 8 + present.numel() * 4
+
+    def _exchange(self, which: str):
+        self.exchanges += 1
+        (self._exchange_dense if self.dense else self._exchange_records)(which)
 
     def step(self, n_steps: int = 1):
         s = self.shard
         for _ in range(int(n_steps)):
+            due = s.apply_due()      # host-side state, no device sync
             s.step_local()
-            self._exchange("V")
-            if s.actor and not s.post_update:
-                self._exchange("H")
+            if due:
+                self._exchange("V")
+                if s.actor and not s.post_update:
+                    self._exchange("H")
             s.step_apply("V")
             if s.actor:
-                if s.post_update:
+                if s.post_update and due:
                     self._exchange("H")
                 s.step_apply("H")
             s.step_end()
 
 
-def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16):
+def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16, sync_period: int = 1,
+                 dense: bool = False):
     """TableSync's protocol for several shards driven by one process (e.g. one
     Learner per device, or shards of one device): the same phases, with the
-    all-gather replaced by handing every shard the others' records."""
-    bufs = {}
+    collectives replaced by handing every shard the others' records (or, dense,
+    the summed accumulators and the presence union)."""
+    for s in shards:
+        s.set_sync_period(sync_period)
 
-    def export(i, s, which):
+    def export(s, which):
         width = 1 if which == "V" else 5
         cap = capacity
         while True:
@@ -162,31 +179,42 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16)
             a = torch.empty((cap, width), dtype=torch.int64, device=device)
             n = s.delta_export(which, k.data_ptr(), a.data_ptr(), cap)
             if n <= cap:
-                bufs[(i, which)] = (k, a)
-                return n
+                return k, a, n
             cap = n
 
     def exchange(which):
-        ns = [export(i, s, which) for i, s in enumerate(shards)]
+        if dense:
+            bufs = [s.dense_buffers(which) for s in shards]
+            tot = torch.stack([b[0] for b in bufs]).sum(0)
+            uni = bufs[0][1].clone()
+            for b in bufs[1:]:
+                uni.bitwise_or_(b[1])
+            for s, b in zip(shards, bufs):
+                b[0].copy_(tot)
+                s.dense_adopt(which, uni.data_ptr())
+            torch.cuda.synchronize()
+            return
+        recs = [export(s, which) for s in shards]
         for i, s in enumerate(shards):
-            for j in range(len(shards)):
-                if j != i and ns[j]:
-                    k, a = bufs[(j, which)]
-                    s.delta_merge(which, k.data_ptr(), a.data_ptr(), ns[j])
+            for j, (k, a, n) in enumerate(recs):
+                if j != i and n:
+                    s.delta_merge(which, k.data_ptr(), a.data_ptr(), n)
             if device is not None and str(device).startswith("cuda"):
                 torch.cuda.synchronize()
 
     for _ in range(int(n_steps)):
+        due = shards[0].apply_due()
         for s in shards:
             s.step_local()
         actor, post = shards[0].actor, shards[0].post_update
-        exchange("V")
-        if actor and not post:
-            exchange("H")
+        if due:
+            exchange("V")
+            if actor and not post:
+                exchange("H")
         for s in shards:
             s.step_apply("V")
         if actor:
-            if post:
+            if post and due:
                 exchange("H")
             for s in shards:
                 s.step_apply("H")

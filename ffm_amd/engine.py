@@ -37,6 +37,8 @@ EXPORTED = [
     "ffm_learner_delta_export", "ffm_learner_delta_merge", "ffm_learner_set_placement",
     "ffm_learner_set_epsilon_schedule", "ffm_learner_drain_episodes",
     "ffm_learner_set_trajectory_capture", "ffm_learner_drain_trajectory",
+    "ffm_learner_delta_export_async", "ffm_learner_delta_merge_async", "ffm_learner_set_sync_period",
+    "ffm_learner_apply_due", "ffm_learner_dense_buffers", "ffm_learner_dense_adopt",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -133,6 +135,12 @@ def load_library():
     L.ffm_learner_set_epsilon_schedule.argtypes = [P, C.c_double, C.c_double, C.c_double, C.c_double]
     L.ffm_learner_drain_episodes.argtypes = [P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     L.ffm_learner_set_trajectory_capture.argtypes = [P, P, P, i32, i32, i64, P]
+    L.ffm_learner_delta_export_async.argtypes = [P, i32, P, P, i64, P, P]
+    L.ffm_learner_delta_merge_async.argtypes = [P, i32, P, P, P, i64, P]
+    L.ffm_learner_set_sync_period.argtypes = [P, i32]
+    L.ffm_learner_apply_due.argtypes = [P, C.POINTER(i32)]
+    L.ffm_learner_dense_buffers.argtypes = [P, i32, C.POINTER(P), C.POINTER(i64), C.POINTER(P), C.POINTER(i64)]
+    L.ffm_learner_dense_adopt.argtypes = [P, i32, P, P]
     L.ffm_learner_drain_trajectory.argtypes = [P, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     for name in EXPORTED:
         if name != "ffm_last_error":
@@ -166,6 +174,14 @@ def _stream_handle(stream):
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class _DevArray:
+    """A device buffer of the library, exposed to torch.as_tensor (zero copy)."""
+
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
 
 
 DEFAULT_PARAMS = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "moore"}
@@ -424,6 +440,7 @@ class Learner:
         d.auto_reset = int(bool(auto_reset))
         d.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         d.env_base, d.device = int(env_base), int(device)
+        self.device = int(device)
         ld = LearnDesc()
         ld.mode = LEARN_MODES.get(self.mode, 1) if variant == "unified" else (1 if variant == "actor_only" else 0)
         ld.k_A = float(p.get("k_A", 0.0))
@@ -678,6 +695,49 @@ class Learner:
     def delta_merge(self, which: str, keys_ptr: int, acc_ptr: int, n: int, stream=None):
         _check(self._L.ffm_learner_delta_merge(self._h, TABLE_V if which == "V" else TABLE_H, keys_ptr, acc_ptr,
                                                int(n), _stream_handle(stream)))
+
+    def delta_export_async(self, which: str, keys_ptr: int, acc_ptr: int, cap: int, count_ptr: int, stream=None):
+        """delta_export without a host sync: the record count goes to the device int64 at
+        count_ptr; a count above cap is reported at the next sync point."""
+        _check(self._L.ffm_learner_delta_export_async(self._h, TABLE_V if which == "V" else TABLE_H, keys_ptr,
+                                                      acc_ptr, int(cap), count_ptr, _stream_handle(stream)))
+
+    def delta_merge_async(self, which: str, keys_ptr: int, acc_ptr: int, count_ptr: int, cap: int, stream=None):
+        _check(self._L.ffm_learner_delta_merge_async(self._h, TABLE_V if which == "V" else TABLE_H, keys_ptr,
+                                                     acc_ptr, count_ptr, int(cap), _stream_handle(stream)))
+
+    def set_sync_period(self, k: int):
+        """Apply the tables every k-th step (increments of k steps accumulate; default 1)."""
+        _check(self._L.ffm_learner_set_sync_period(self._h, int(k)))
+
+    def apply_due(self) -> bool:
+        d = C.c_int32()
+        _check(self._L.ffm_learner_apply_due(self._h, C.byref(d)))
+        return bool(d.value)
+
+    @property
+    def dense_tables(self) -> bool:
+        """ffm_unified / ffm_trained_core rank-key tables are dense (slot = key)."""
+        if not hasattr(self, "_dense"):
+            a, p, na, npw = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int64()
+            self._dense = self._L.ffm_learner_dense_buffers(self._h, TABLE_V, C.byref(a), C.byref(na), C.byref(p),
+                                                            C.byref(npw)) == OK
+        return self._dense
+
+    def dense_buffers(self, which: str):
+        """(acc int64 [cap * width], presence int32 [cap / 32]) torch views of the device
+        buffers of a dense table (zero copy)."""
+        import torch
+        a, p, na, npw = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int64()
+        _check(self._L.ffm_learner_dense_buffers(self._h, TABLE_V if which == "V" else TABLE_H, C.byref(a),
+                                                 C.byref(na), C.byref(p), C.byref(npw)))
+        dev = torch.device("cuda", self.device)
+        return (torch.as_tensor(_DevArray(a.value, na.value, "<i8"), device=dev),
+                torch.as_tensor(_DevArray(p.value, npw.value, "<i4"), device=dev))
+
+    def dense_adopt(self, which: str, union_ptr: int, stream=None):
+        _check(self._L.ffm_learner_dense_adopt(self._h, TABLE_V if which == "V" else TABLE_H, union_ptr,
+                                               _stream_handle(stream)))
 
     # -- telemetry -----------------------------------------------------------------------
     def counters(self, stream=None) -> dict:

@@ -244,6 +244,28 @@ int ffm_learner_delta_export(ffm_learner* l, int32_t which, uint64_t* d_keys, in
                              int64_t* n, void* stream);
 int ffm_learner_delta_merge(ffm_learner* l, int32_t which, const uint64_t* d_keys, const int64_t* d_acc,
                             int64_t n, void* stream);
+/* The same exchange without host synchronisation (multi-rank steps issue no host
+ * sync inside the loop): export writes the record count to the DEVICE int64 d_count
+ * (records past cap are dropped; count > cap is reported as FFM_E_INVALID at the next
+ * sync point or ffm_learner_step); merge reads min(*d_count, cap) records. */
+int ffm_learner_delta_export_async(ffm_learner* l, int32_t which, uint64_t* d_keys, int64_t* d_acc, int64_t cap,
+                                   int64_t* d_count, void* stream);
+int ffm_learner_delta_merge_async(ffm_learner* l, int32_t which, const uint64_t* d_keys, const int64_t* d_acc,
+                                  const int64_t* d_count, int64_t cap, void* stream);
+/* Table sync period K >= 1 (default 1 = the reference's per-step updates): the fixed-point
+ * increments of K steps accumulate and V / H (and the actor's H statistics) are applied
+ * at every K-th step only; a multi-rank run exchanges deltas at those steps only, so
+ * sharded == one device at the same K, bit for bit.  apply_due: 1 if the current (or
+ * next) step's step_apply applies. */
+int ffm_learner_set_sync_period(ffm_learner* l, int32_t period);
+int ffm_learner_apply_due(ffm_learner* l, int32_t* due);
+/* Dense (ffm_unified rank-key) tables: the device fixed-point accumulators (acc_count
+ * int64) and presence bitmap (present_words u32), for an all-reduce of the increments;
+ * dense_adopt then takes the presence union of all ranks (a DEVICE bitmap): slots other
+ * ranks inserted get their keys.  Between step_local and step_apply. */
+int ffm_learner_dense_buffers(ffm_learner* l, int32_t which, int64_t** d_acc, int64_t* acc_count,
+                              uint32_t** d_present, int64_t* present_words);
+int ffm_learner_dense_adopt(ffm_learner* l, int32_t which, const uint32_t* d_union, void* stream);
 /* Philox placement candidates of later resets: `count` distinct free cells (x*W+y) and the
  * agents to place, <= count (the radius curriculum, model/ffm_unified.py:150-171:
  * actual_N = min(N, cells within the radius)).  count = 0 restores every free cell. */

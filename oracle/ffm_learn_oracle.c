@@ -135,9 +135,12 @@ int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, in
     return 0;
 }
 
+/* Applies the pending increments; the next delta export starts from here (the
+ * device's apply kernels set their mark the same way). */
 void ffo_tab_apply(ffo_tab* t) {
     for (int64_t s = 0; s < t->cap * t->width; s++)
         if (t->acc[s]) { t->vals[s] = t->vals[s] + (double)t->acc[s] * (1.0 / FX_ONE); t->acc[s] = 0; }
+    t->mark = t->n;
 }
 
 int ffo_tab_import(ffo_tab* t, const uint64_t* keys, const double* vals, int64_t n) {
@@ -146,6 +149,7 @@ int ffo_tab_import(ffo_tab* t, const uint64_t* keys, const double* vals, int64_t
         if (s < 0) return -1;
         memcpy(t->vals + s * t->width, vals + i * t->width, sizeof(double) * (size_t)t->width);
     }
+    t->mark = t->n;
     return 0;
 }
 
@@ -893,8 +897,6 @@ int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, 
     if (actor || c->variant == FFO_VAR_TRAINED) h_stats(b->Ht, &hs);
     float smin, smax;
     sff_minmax(c, &smin, &smax);
-    ffo_tab_mark(b->V);
-    ffo_tab_mark(b->Ht);
     memset(b->recs, 0, sizeof(lrec) * (size_t)(E * A_cap));
     uint64_t total = 0;
     int err = 0;
@@ -937,10 +939,9 @@ int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, 
 
 /* which 0: apply V, then (ffm_unified actor_only) the actor's increments from the
  * TD errors of the updated V (model/ffm_unified.py:559-598); which 1: apply H. */
-void ffo_lbatch_apply(ffo_lbatch* b, int which) {
+/* ffm_unified actor_only: the actor increments from the TD errors of the (applied) V. */
+void ffo_lbatch_post(ffo_lbatch* b) {
     const ffo_learn_cfg* c = b->c;
-    if (which == 1) { ffo_tab_apply(b->Ht); return; }
-    ffo_tab_apply(b->V);
     if (!(c->variant == FFO_VAR_UNIFIED && c->mode == FFO_MODE_ACTOR)) return;
     for (int64_t e = 0; e < b->E; e++)
         for (int i = 0; i < b->nstart[e]; i++) {
@@ -950,6 +951,12 @@ void ffo_lbatch_apply(ffo_lbatch* b, int which) {
             const double td = (q->r + c->gamma * vn) - b->V->vals[q->sv];
             b->Ht->acc[(int64_t)q->hslot * 5 + q->k] += fx(c->alpha_h * td);
         }
+}
+
+void ffo_lbatch_apply(ffo_lbatch* b, int which) {
+    if (which == 1) { ffo_tab_apply(b->Ht); return; }
+    ffo_tab_apply(b->V);
+    ffo_lbatch_post(b);
 }
 
 /* Episode ends: emptied, or truncated at max_steps (run_*_training.py MAX_STEPS). */

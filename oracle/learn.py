@@ -79,6 +79,7 @@ def _lib():
         L.ffo_lbatch_set_placement.argtypes = [P, P, C.c_int32]
         L.ffo_lbatch_local.restype = C.c_int
         L.ffo_lbatch_apply.argtypes = [P, C.c_int]
+        L.ffo_lbatch_post.argtypes = [P]
         L.ffo_lbatch_end.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_int64, P]
         L.ffo_lbatch_end.restype = C.c_int64
@@ -207,6 +208,8 @@ class Shard:
         self.t = 1
         self.agent_steps = 0
         self.log = []
+        self.sync_period, self.since_apply = 1, 0
+        self.dense_tables = False
         self.b = _lib().ffo_lbatch_new(C.byref(learn.cfg), learn.V.h, learn.Ht.h, E, A)
 
     def __del__(self):
@@ -233,8 +236,18 @@ class Shard:
             raise RuntimeError("oracle table full")
         self.agent_steps += int(tot.value)
 
+    def set_sync_period(self, k: int):
+        """The engine's table sync period (ffm_learner_set_sync_period)."""
+        self.sync_period, self.since_apply = int(k), 0
+
+    def apply_due(self) -> bool:
+        return self.since_apply + 1 >= self.sync_period
+
     def step_apply(self, which):
-        _lib().ffo_lbatch_apply(self.b, 0 if which == "V" else 1)
+        if self.apply_due():
+            _lib().ffo_lbatch_apply(self.b, 0 if which == "V" else 1)
+        elif which == "V":
+            _lib().ffo_lbatch_post(self.b)
 
     def set_placement(self, cells, n_agents: int):
         c = np.ascontiguousarray(cells, np.uint16)
@@ -248,6 +261,7 @@ class Shard:
                                   self.max_steps, self.env_base, O._ptr(log))
         self.log.extend(map(tuple, log[:n].tolist()))
         self.t += 1
+        self.since_apply = 0 if self.apply_due() else self.since_apply + 1
 
     def delta_export(self, which, keys_ptr, acc_ptr, cap):
         T = self._tab(which)
@@ -255,6 +269,22 @@ class Shard:
         if n > cap:
             return n
         return int(_lib().ffo_tab_delta_export(T.h, keys_ptr, acc_ptr))
+
+    def delta_export_async(self, which, keys_ptr, acc_ptr, cap, count_ptr):
+        """The engine's asynchronous export: the count goes to memory (here host memory)."""
+        T = self._tab(which)
+        tmp_k = np.empty(max(len(T), 1), np.uint64)
+        tmp_a = np.empty((max(len(T), 1), T.width), np.int64)
+        n = int(_lib().ffo_tab_delta_export(T.h, O._ptr(tmp_k), O._ptr(tmp_a)))
+        m = min(n, int(cap))
+        C.memmove(keys_ptr, tmp_k.ctypes.data, m * 8)
+        C.memmove(acc_ptr, tmp_a.ctypes.data, m * 8 * T.width)
+        C.c_int64.from_address(count_ptr).value = n
+        if n > cap:
+            raise RuntimeError("asynchronous delta export: record buffer too small")
+
+    def delta_merge_async(self, which, keys_ptr, acc_ptr, count_ptr, cap):
+        self.delta_merge(which, keys_ptr, acc_ptr, min(C.c_int64.from_address(count_ptr).value, int(cap)))
 
     def delta_merge(self, which, keys_ptr, acc_ptr, n):
         T = self._tab(which)

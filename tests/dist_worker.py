@@ -107,9 +107,9 @@ def sorted_tables(learn):
     return out
 
 
-def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1):
+def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1, sync_period=1, steps=LEARN_STEPS):
     """Single shard (or `coupled_shards` shards coupled in-process) of the batched
-    learning step on the CPU restatement."""
+    learning step on the CPU restatement, tables applied every `sync_period` steps."""
     from oracle import learn as LO
     from ffm_amd.dist import shard_range, step_coupled
     m, s = room()
@@ -119,13 +119,13 @@ def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1):
         L = LO.Learn(m, s, variant, mode, learn_params(variant), log2_cap=20)
         learns.append(L)
         shards.append(LO.Shard(L, c, LEARN_N, LEARN_N, SEED, env_base + b, LEARN_MAX))
-    step_coupled(shards, LEARN_STEPS, device="cpu")
+    step_coupled(shards, steps, device="cpu", sync_period=sync_period)
     cat = lambda f: np.concatenate([f(x) for x in shards])
     return (cat(lambda x: x.pos), cat(lambda x: x.counts), cat(lambda x: x.dff), cat(lambda x: x.episodes),
             cat(lambda x: x.ep_steps), sorted_tables(learns[0])), [sorted_tables(L) for L in learns]
 
 
-def learn_worker(rank, world, port, n_global, variant, mode, out_path):
+def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_period=1, steps=LEARN_STEPS):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -135,8 +135,9 @@ def learn_worker(rank, world, port, n_global, variant, mode, out_path):
         base, n = shard_range(n_global, rank, world)
         L = LO.Learn(m, s, variant, mode, learn_params(variant), log2_cap=20)
         shard = LO.Shard(L, n, LEARN_N, LEARN_N, SEED, base, LEARN_MAX)
-        sync = TableSync(shard, device="cpu", capacity=64)      # small: exercises the regrow path
-        sync.step(LEARN_STEPS)
+        sync = TableSync(shard, device="cpu", capacity=8192, sync_period=sync_period)
+        sync.step(steps)
+        assert sync.exchanges > 0
         parts = {}
         for name, a in (("pos", shard.pos), ("cnt", shard.counts), ("dff", shard.dff), ("eps", shard.episodes),
                         ("est", shard.ep_steps)):

@@ -95,15 +95,32 @@ def test_coupled_learning_shards_equal_single_run(variant, mode):
     assert a["eps"].sum() > 0 and len(a["V_keys"]) > 50
 
 
+@pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("unified", "both"), ("actor_only", None)])
+def test_sync_period_coupled_equals_single_and_changes_dynamics(variant, mode):
+    """A table sync period K = 4 (increments of 4 steps applied together): 3 coupled
+    shards == one batch of all envs at the same K, and K = 4 differs from K = 1."""
+    n = 41
+    one4, _ = W.run_learn_oracle(variant, mode, 0, n, sync_period=4, steps=52)
+    three4, _ = W.run_learn_oracle(variant, mode, 0, n, coupled_shards=3, sync_period=4, steps=52)
+    one1, _ = W.run_learn_oracle(variant, mode, 0, n, steps=52)
+    a, b, c = W.learn_summary(one4), W.learn_summary(three4), W.learn_summary(one1)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert not np.array_equal(a["V_vals"], c["V_vals"]) or len(a["V_keys"]) != len(c["V_keys"])
+
+
+@pytest.mark.parametrize("sync_period", [1, 4])
 @pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None), ("ac", None)])
-def test_gloo_world2_table_sync_equals_single_run(variant, mode, tmp_path):
-    """TableSync over a real world-2 gloo group (all_gather of variable-length
-    delta records) == a single-process batch of all envs."""
+def test_gloo_world2_table_sync_equals_single_run(variant, mode, sync_period, tmp_path):
+    """TableSync over a real world-2 gloo group (fixed-capacity delta records, counts
+    on the device side, no host sync in the loop) == a single-process batch of all
+    envs with the same table sync period."""
     n = 37
     out = str(tmp_path / "learn.npz")
-    mp.spawn(W.learn_worker, args=(2, _port(), n, variant, mode, out), nprocs=2, join=True)
+    steps = 52          # a whole number of sync windows: every rank holds every key
+    mp.spawn(W.learn_worker, args=(2, _port(), n, variant, mode, out, sync_period, steps), nprocs=2, join=True)
     got = dict(np.load(out))
-    single, _ = W.run_learn_oracle(variant, mode, 0, n)
+    single, _ = W.run_learn_oracle(variant, mode, 0, n, sync_period=sync_period, steps=steps)
     want = W.learn_summary(single)
     for k in want:
         assert np.array_equal(got[k], want[k]), k

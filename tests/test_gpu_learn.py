@@ -323,12 +323,15 @@ def test_learner_unified_dense_table_rejects_foreign_keys():
     L.close()
 
 
-@pytest.mark.parametrize("variant,mode", VARIANTS)
-def test_learner_coupled_shards_equal_one_learner(variant, mode):
+@pytest.mark.parametrize("variant,mode,sync,dense", [v + (1, False) for v in VARIANTS] + [
+    (("unified", "actor_only") + (1, True)), (("unified", "both") + (4, True)),
+    (("unified", "critic_only") + (4, True)), (("actor_only", None) + (4, False))])
+def test_learner_coupled_shards_equal_one_learner(variant, mode, sync, dense):
     """Multi-GPU contract on one device: three Learner shards (env_base offsets) stepped
     through ffm_amd.dist.step_coupled (delta export -> merge of the others' records ->
-    apply) end every step with the tables of ONE learner holding all envs, bit for bit,
-    and the same env states."""
+    apply; dense: summed fixed-point accumulators + presence union) end every sync step
+    with the tables of ONE learner holding all envs at the same table sync period, bit
+    for bit, and the same env states."""
     from ffm_amd.data import make_room, l1_sff
     from ffm_amd.dist import shard_range, step_coupled
     m = make_room(12, 12)
@@ -337,6 +340,7 @@ def test_learner_coupled_shards_equal_one_learner(variant, mode):
     n, N, T = 3001, 32, 60
     kw = dict(mode=mode, params=p, rng="philox", seed=21, auto_reset=True, max_steps=40)
     one = _learner(m, s, variant, n_envs=n, n_agents=N, **kw)
+    one.set_sync_period(sync)
     one.reset()
     one.step(T)
     shards = []
@@ -345,7 +349,7 @@ def test_learner_coupled_shards_equal_one_learner(variant, mode):
         L = _learner(m, s, variant, n_envs=c, n_agents=N, env_base=b, **kw)
         L.reset()
         shards.append(L)
-    step_coupled(shards, T, device="cuda", capacity=1024)
+    step_coupled(shards, T, device="cuda", capacity=1024, sync_period=sync, dense=dense)
     op, oc, od = one.get_state()
     sp = [L.get_state() for L in shards]
     assert np.array_equal(oc, np.concatenate([x[1] for x in sp]))
