@@ -242,13 +242,13 @@ __device__ __forceinline__ uint32_t slot_cell(uint32_t slot, int pp, int PW) {
 
 // The requesters of target r (padded): agents adjacent to r whose request is r.
 // who[s] = agent index at r - off(s) (or 0xFFFF), is[s] = it requests r.
-template <int NB, class GT>
-__device__ __forceinline__ int requesters(int r, int PW, const GT* grid, const uint16_t* sreq,
+template <int NB, class GT, class RT = uint16_t>
+__device__ __forceinline__ int requesters(int r, int PW, const GT* grid, const RT* sreq,
                                           uint16_t (&who)[NB], bool (&is)[NB]) {
     uint32_t g[NB];
 #pragma unroll
     for (int s = 0; s < NB; s++) g[s] = grid[r - nb_dx<NB>(s) * PW - nb_dy<NB>(s)];
-    uint16_t q[NB];
+    RT q[NB];
 #pragma unroll
     for (int s = 0; s < NB; s++) {
         const bool ag = (g[s] & GridCodes<GT>::kAgent) != 0u;
@@ -258,7 +258,7 @@ __device__ __forceinline__ int requesters(int r, int PW, const GT* grid, const u
     int m = 0;
 #pragma unroll
     for (int s = 0; s < NB; s++) {
-        is[s] = who[s] != 0xFFFF && q[s] == (uint16_t)r;
+        is[s] = who[s] != 0xFFFF && q[s] == (RT)r;
         m += is[s] ? 1 : 0;
     }
     return m;

@@ -34,6 +34,7 @@
 //     so order does not matter; MT mode (reference replay) serialises the
 //     draws of each env on one lane in exactly the reference's order.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "core_common.h"
@@ -519,6 +520,7 @@ void core_wave_kernel(CoreStepArgs a) {
 // ~40 KB at config 3 (64x64, 512 agents), 3 blocks per CU instead of 1.
 struct BlockCarve {
     size_t grid, dff, pos, req, nxt, misc, u, flag, keys, total;
+    size_t lds;     // LDS bytes per block (big: the misc words only; the rest is global scratch)
 };
 
 // Placement candidates kept in LDS: the threshold of reset_threshold() passes
@@ -532,25 +534,37 @@ __host__ __device__ inline int block_keys_cap(int A, int F) {
     return cap < F ? cap : F;
 }
 
-__host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, bool f64, bool mt, bool reset) {
+// big: maps whose state exceeds the LDS (up to 256 x 256): one env per block, the
+// grid, DFF tile, cell lists and placement keys in a global scratch region of the
+// block (L2-resident while the block runs), padded cells as u32 (> 65,535 of them).
+__host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, bool f64, bool mt, bool reset,
+                                                  bool big = false) {
     BlockCarve c;
     size_t o = 0;
     (void)f64;
+    const size_t ix = big ? 4 : 2;
+    const size_t misc = align16((size_t)(8 * K + 64) * 4);
     c.grid = o; o += align16((size_t)K * PHW * 2);
     c.dff = o;  o += align16((size_t)K * PHW * 4);
-    c.pos = o;  o += align16((size_t)K * A * 2);
-    c.req = o;  o += align16((size_t)K * A * 2);
-    c.nxt = o;  o += align16((size_t)K * A * 2);
-    c.misc = o; o += align16((size_t)(8 * K + 64) * 4);
+    c.pos = o;  o += align16((size_t)K * A * ix);
+    c.req = o;  o += align16((size_t)K * A * ix);
+    c.nxt = o;  o += align16((size_t)K * A * ix);
+    c.misc = big ? 0 : o;
+    o += big ? 0 : misc;
     c.u = o;    o += mt ? align16((size_t)K * A * 8) : 0;
     c.flag = o; o += mt ? align16((size_t)K * A * 2) : 0;
     c.keys = o; o += reset ? align16((size_t)block_keys_cap(A, F) * 8) : 0;
     c.total = o;
+    c.lds = big ? misc : o;
     return c;
 }
 
 size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool mt, bool reset) {
     return block_carve((H + 2) * (W + 2), A, K, F, f64, mt, reset).total;
+}
+
+size_t core_big_scratch_bytes(int H, int W, int A, int F, bool mt) {
+    return block_carve((H + 2) * (W + 2), A, 1, F, false, mt, true, true).total;
 }
 
 // (env, row, column) of a flat index i = (k * rows + r) * cols + c, advanced by a
@@ -614,31 +628,102 @@ __device__ __forceinline__ int block_excl_scan(bool flag, int* swsum, int& total
     return wp + lp;
 }
 
-template <int NB, bool F64, bool MT, int BS>
+// Philox placement of env e by the whole workgroup: the N free cells
+// with the smallest (key_j, j).  Candidates under a threshold (~2N + 16 of them) are
+// kept in `keys` (KC of them) and ranked; more than KC take an exact recomputing path.
+template <int BS>
+__device__ void block_place_env(const CoreStepArgs& a, long long e, unsigned long long* keys, int KC, int* swsum) {
+    const int tid = threadIdx.x;
+    const uint32_t genv = (uint32_t)(a.env_base + e);
+    uint32_t T = reset_threshold(a.N, a.F);
+    int C = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        C = 0;
+        for (int j0 = 0; j0 < a.F; j0 += BS) {
+            const int j = j0 + tid;
+            uint32_t key = 0;
+            bool cand = false;
+            if (j < a.F) {
+                key = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
+                cand = key <= T;
+            }
+            int tot;
+            const int ex = block_excl_scan<BS>(cand, swsum, tot);
+            if (cand && C + ex < KC) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
+            C += tot;
+        }
+        if ((C >= a.N && C <= KC) || T == 0xFFFFFFFFu) break;
+        if (C > KC) break;       // too many to keep: the recomputing path below
+        T = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    if (C <= KC) {
+        for (int i = tid; i < C; i += BS) {
+            const unsigned long long ki = keys[i];
+            int rank = 0;
+#pragma unroll 4
+            for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
+            if (rank < a.N) a.pos[e * a.A + rank] = a.free_list[(int)(ki & 0xFFFFFFFFu)];
+        }
+    } else {
+        // Exact but slow (keys recomputed per comparison): the candidates exceed KC.
+        for (int j = tid; j < a.F; j += BS) {
+            const uint32_t kj = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
+            if (kj > T) continue;
+            const unsigned long long ki = ((unsigned long long)kj << 32) | (unsigned)j;
+            int rank = 0;
+            for (int q = 0; q < a.F && rank < a.N; q++) {
+                const unsigned long long kq =
+                    ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)q) << 32) | (unsigned)q;
+                rank += kq < ki ? 1 : 0;
+            }
+            if (rank < a.N) a.pos[e * a.A + rank] = a.free_list[j];
+        }
+    }
+    __syncthreads();
+}
+
+// Request / target cell of a decide slot: padded cells are u16 (CT) in LDS-sized envs
+// and u32 for big maps, whose cell indices reach the u16 sentinels.
+template <class CT>
+struct ReqCodes {
+    static constexpr CT kNone = (CT)~(CT)0, kWait = (CT)(~(CT)0 - 1);
+};
+template <int NB, class CT>
+__device__ __forceinline__ CT req_cell(uint32_t slot, int pp, int PW) {
+    return slot <= (uint32_t)NB ? (CT)slot_cell<NB>(slot, pp, PW)
+           : slot == kPending ? ReqCodes<CT>::kWait : ReqCodes<CT>::kNone;
+}
+
+template <int NB, bool F64, bool MT, int BS, bool BIG>
 __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     using GT = uint16_t;
+    using CT = typename std::conditional<BIG, uint32_t, uint16_t>::type;
+    constexpr CT kNoReqC = ReqCodes<CT>::kNone, kPendingC = ReqCodes<CT>::kWait;
     const int tid = threadIdx.x;
     const int H = a.H, W = a.W, HW = H * W, PW = W + 2, PHW = (H + 2) * PW, A = a.A;
     const long long e0 = (long long)blockIdx.x * a.K;
     const int K = (int)((a.E - e0) < a.K ? (a.E - e0) : a.K);
     const bool do_reset = !MT && a.auto_reset;
-    const BlockCarve cv = block_carve(PHW, A, a.K, a.F, F64, MT, do_reset);
+    const BlockCarve cv = block_carve(PHW, A, a.K, a.F, F64, MT, do_reset || BIG, BIG);
+    // big maps: everything but the misc words in this block's global scratch region
+    unsigned char* gbase = BIG ? a.scratch + (size_t)blockIdx.x * a.scratch_stride : smem;
     const uint8_t* pmap = a.pmap;
     const float* psff32 = reinterpret_cast<const float*>(a.psff);
     const double* psff64 = reinterpret_cast<const double*>(a.psff);
     const int KC = block_keys_cap(A, a.F);
-    GT* grid = reinterpret_cast<GT*>(smem + cv.grid);
-    float* tile = reinterpret_cast<float*>(smem + cv.dff);
-    uint16_t* spos = reinterpret_cast<uint16_t*>(smem + cv.pos);
-    uint16_t* sreq = reinterpret_cast<uint16_t*>(smem + cv.req);
-    uint16_t* snxt = reinterpret_cast<uint16_t*>(smem + cv.nxt);
+    GT* grid = reinterpret_cast<GT*>(gbase + cv.grid);
+    float* tile = reinterpret_cast<float*>(gbase + cv.dff);
+    CT* spos = reinterpret_cast<CT*>(gbase + cv.pos);
+    CT* sreq = reinterpret_cast<CT*>(gbase + cv.req);
+    CT* snxt = reinterpret_cast<CT*>(gbase + cv.nxt);
     int* scnt = reinterpret_cast<int*>(smem + cv.misc);   // [K] count at step start
     int* snew = scnt + a.K;                                // [K] count after exits
     int* sreset = snew + a.K;                              // [K] reset flag
     int* sseg = sreset + a.K;                              // [K] scan segment base
     int* swsum = sseg + a.K;                               // [BS/64]
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem + cv.keys);
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(gbase + cv.keys);
 
     const int nA = K * A;
     const int nP = K * PHW;
@@ -662,13 +747,13 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
         const int it = ag.it;
         const int k = ag.k, i = ag.i;
-        int pp = 0xFFFF;
+        int pp = 0;
         if (i < scnt[k]) {
             const int c = a.pos[(e0 + k) * A + i];
             const int x = c / W, y = c - (c / W) * W;
             pp = (x + 1) * PW + y + 1;
         }
-        spos[it] = (uint16_t)pp;
+        spos[it] = (CT)pp;
     }
     __syncthreads();
 
@@ -678,7 +763,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         const int k = ag.k, i = ag.i;
         if (i < scnt[k]) grid[k * PHW + spos[it]] = (GT)(GridCodes<GT>::kAgent | (uint32_t)i);
         snxt[it] = spos[it];
-        sreq[it] = kNoReq;
+        sreq[it] = kNoReqC;
     }
     __syncthreads();
 
@@ -688,48 +773,49 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         const int k = ag.k, i = ag.i;
         if (i >= scnt[k]) continue;
         const int pp = spos[it];
-        uint32_t r;
+        CT r;
         if (MT) {
-            r = slot_cell<NB>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64,
-                                    DrawPending{}), pp, PW);
+            r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32,
+                                                     a.kS64, DrawPending{}), pp, PW);
         } else {
             const DrawPhilox d{a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i};
-            r = slot_cell<NB>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32, a.kS64, d), pp, PW);
+            r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32,
+                                                     a.kS64, d), pp, PW);
         }
-        sreq[it] = (uint16_t)r;
+        sreq[it] = r;
     }
     __syncthreads();
 
     if (MT) {
         // NumPy stream: one draw per pending agent, in agent order; then redo the choice.
-        double* su = reinterpret_cast<double*>(smem + cv.u);
+        double* su = reinterpret_cast<double*>(gbase + cv.u);
         if (tid < K) {
             uint32_t* mt_np = a.mt_np + (e0 + tid) * 625;
             for (int i = 0; i < scnt[tid]; i++)
-                if (sreq[tid * A + i] == kPending) su[tid * A + i] = mt_u53(mt_np);
+                if (sreq[tid * A + i] == kPendingC) su[tid * A + i] = mt_u53(mt_np);
         }
         __syncthreads();
         for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
         const int it = ag.it;
             const int k = ag.k, i = ag.i;
-            if (i >= scnt[k] || sreq[it] != kPending) continue;
-            sreq[it] = (uint16_t)slot_cell<NB>(decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
-                                                     a.kS32, a.kD32, a.kS64, DrawFixed{su[it]}), spos[it], PW);
+            if (i >= scnt[k] || sreq[it] != kPendingC) continue;
+            sreq[it] = req_cell<NB, CT>(decide<NB, F64, GT>(spos[it], PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
+                                                            a.kS32, a.kD32, a.kS64, DrawFixed{su[it]}), spos[it], PW);
         }
         __syncthreads();
 
         // Owners of contested targets, then their draws in owner (= dict) order.
-        uint16_t* sflag = reinterpret_cast<uint16_t*>(smem + cv.flag);
+        uint16_t* sflag = reinterpret_cast<uint16_t*>(gbase + cv.flag);
         for (AgentIdx ag = ag0; ag.it < nA; ag.advance()) {
         const int it = ag.it;
             const int k = ag.k, i = ag.i;
             sflag[it] = 0;
             if (i >= scnt[k]) continue;
-            const int r = sreq[it];
-            if (r == kNoReq || r == spos[it]) continue;
+            const CT r = sreq[it];
+            if (r == kNoReqC || r == spos[it]) continue;
             uint16_t who[NB];
             bool is[NB];
-            const int m = requesters<NB, GT>(r, PW, grid + k * PHW, sreq + k * A, who, is);
+            const int m = requesters<NB, GT, CT>((int)r, PW, grid + k * PHW, sreq + k * A, who, is);
             const int s0 = kth_slot<NB>(who, is, 0);
             if (m >= 2 && s0 >= 0 && who[s0] == i) sflag[it] = (uint16_t)m;
         }
@@ -754,8 +840,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         const int it = ag.it;
         const int k = ag.k, i = ag.i;
         if (i >= scnt[k]) continue;
-        const int r = sreq[it];
-        if (r == kNoReq) continue;
+        const CT rc = sreq[it];
+        if (rc == kNoReqC) continue;
+        const int r = (int)rc;
         float* dk = tile + k * PHW;
         const int pp = spos[it];
         if (r == pp) {
@@ -764,14 +851,14 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         }
         uint16_t who[NB];
         bool is[NB];
-        const int m = requesters<NB, GT>(r, PW, grid + k * PHW, sreq + k * A, who, is);
+        const int m = requesters<NB, GT, CT>(r, PW, grid + k * PHW, sreq + k * A, who, is);
         const int s0 = kth_slot<NB>(who, is, 0);
         if (s0 < 0 || who[s0] != i) continue;  // not the owner
         int ws = -1;
         if (m == 1) {
             ws = s0;
         } else if (MT) {
-            const int f = reinterpret_cast<uint16_t*>(smem + cv.flag)[it];
+            const int f = reinterpret_cast<uint16_t*>(gbase + cv.flag)[it];
             if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
         } else {
             const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
@@ -788,7 +875,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
                     wcell = r - nb_dx<NB>(s) * PW - nb_dy<NB>(s);
                     wi = who[s];
                 }
-            snxt[k * A + wi] = (uint16_t)r;
+            snxt[k * A + wi] = (CT)r;
             dk[wcell] += 1.0f;                                                        // :97-98
         }
     }
@@ -823,53 +910,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         __syncthreads();
         for (int k = 0; k < K; k++) {
             if (!sreset[k]) continue;   // block-uniform
-            const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
-            uint32_t T = reset_threshold(a.N, a.F);
-            int C = 0;
-            for (int attempt = 0; attempt < 2; attempt++) {
-                C = 0;
-                for (int j0 = 0; j0 < a.F; j0 += BS) {
-                    const int j = j0 + tid;
-                    uint32_t key = 0;
-                    bool cand = false;
-                    if (j < a.F) {
-                        key = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
-                        cand = key <= T;
-                    }
-                    int tot;
-                    const int ex = block_excl_scan<BS>(cand, swsum, tot);
-                    if (cand && C + ex < KC) keys[C + ex] = ((unsigned long long)key << 32) | (unsigned)j;
-                    C += tot;
-                }
-                if ((C >= a.N && C <= KC) || T == 0xFFFFFFFFu) break;
-                if (C > KC) break;       // too many to keep: the recomputing path below
-                T = 0xFFFFFFFFu;
-            }
-            __syncthreads();
-            if (C <= KC) {
-                for (int i = tid; i < C; i += BS) {
-                    const unsigned long long ki = keys[i];
-                    int rank = 0;
-#pragma unroll 4
-                    for (int q = 0; q < C; q++) rank += keys[q] < ki ? 1 : 0;
-                    if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[(int)(ki & 0xFFFFu)], PW);
-                }
-            } else {
-                // Exact but slow (keys recomputed per comparison): the candidates exceed KC.
-                for (int j = tid; j < a.F; j += BS) {
-                    const uint32_t kj = reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j);
-                    if (kj > T) continue;
-                    const unsigned long long ki = ((unsigned long long)kj << 32) | (unsigned)j;
-                    int rank = 0;
-                    for (int q = 0; q < a.F && rank < a.N; q++) {
-                        const unsigned long long kq =
-                            ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)q) << 32) | (unsigned)q;
-                        rank += kq < ki ? 1 : 0;
-                    }
-                    if (rank < a.N) a.pos[(e0 + k) * A + rank] = (uint16_t)unpad(a.free_padded[j], PW);
-                }
-            }
-            __syncthreads();
+            block_place_env<BS>(a, e0 + k, keys, KC, swsum);
         }
     }
 
@@ -921,6 +962,17 @@ __global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
     for (int i = threadIdx.x; i < a.F; i += 64) fl[i] = a.free_padded[i];
     wave_sync();
     wave_reset_env(a, (uint32_t)(a.env_base + e), keys, fl, a.pos + e * a.A, threadIdx.x);
+    if (threadIdx.x == 0) a.cnt[e] = a.N;
+}
+
+// Reset every env of a map whose free list does not fit the wave reset's LDS
+// (big maps): one workgroup per env, keys in the env block's global scratch.
+__global__ __launch_bounds__(1024) void core_block_reset_kernel(CoreStepArgs a) {
+    __shared__ int swsum[16];
+    const long long e = blockIdx.x;
+    const BlockCarve cv = block_carve((a.H + 2) * (a.W + 2), a.A, 1, a.F, false, false, true, true);
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(a.scratch + (size_t)e * a.scratch_stride + cv.keys);
+    block_place_env<1024>(a, e, keys, block_keys_cap(a.A, a.F), swsum);
     if (threadIdx.x == 0) a.cnt[e] = a.N;
 }
 
@@ -1007,11 +1059,16 @@ int core_wave_blocks_per_cu(const CoreStepArgs& a, int nb, bool mt) {
 template <int NB, bool F64, bool MT>
 static hipError_t launch_block_t(const CoreStepArgs& a, int block, hipStream_t s) {
     const long long nblk = (a.E + a.K - 1) / a.K;
+    if (a.scratch) {   // big maps: K = 1, state in global scratch
+        const size_t smem = block_carve((a.H + 2) * (a.W + 2), a.A, 1, a.F, F64, MT, true, true).lds;
+        core_block_kernel<NB, F64, MT, 1024, true><<<dim3((unsigned)nblk), dim3(1024), smem, s>>>(a);
+        return hipGetLastError();
+    }
     const size_t smem = core_block_smem_bytes(a.H, a.W, a.A, a.K, a.F, F64, MT, !MT && a.auto_reset);
     if (block == 512) {
-        core_block_kernel<NB, F64, MT, 512><<<dim3((unsigned)nblk), dim3(512), smem, s>>>(a);
+        core_block_kernel<NB, F64, MT, 512, false><<<dim3((unsigned)nblk), dim3(512), smem, s>>>(a);
     } else {
-        core_block_kernel<NB, F64, MT, 256><<<dim3((unsigned)nblk), dim3(256), smem, s>>>(a);
+        core_block_kernel<NB, F64, MT, 256, false><<<dim3((unsigned)nblk), dim3(256), smem, s>>>(a);
     }
     return hipGetLastError();
 }
@@ -1023,6 +1080,11 @@ hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, i
     }
     if (f64) return mt ? launch_block_t<8, true, true>(a, block, s) : launch_block_t<8, true, false>(a, block, s);
     return mt ? launch_block_t<8, false, true>(a, block, s) : launch_block_t<8, false, false>(a, block, s);
+}
+
+hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s) {
+    core_block_reset_kernel<<<dim3((unsigned)a.E), dim3(1024), 0, s>>>(a);
+    return hipGetLastError();
 }
 
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s) {

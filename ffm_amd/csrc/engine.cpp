@@ -69,6 +69,10 @@ struct ffm_engine {
     uint32_t* d_mt_np = nullptr;
     uint32_t* d_mt_py = nullptr;
     unsigned long long* d_dbg = nullptr;   // diagnostic counters (FFM_STAMPS builds)
+    bool big = false;            // block kernel with its state in global scratch (maps beyond LDS)
+    bool block_reset = false;    // placement by core_block_reset_kernel (free list beyond the wave reset's LDS)
+    unsigned char* d_scratch = nullptr;    // [E][scratch_stride]
+    size_t scratch_stride = 0;
 };
 
 extern "C" {
@@ -91,6 +95,7 @@ static void release(ffm_engine* e) {
     (void)hipFree(e->d_mt_np);
     (void)hipFree(e->d_mt_py);
     (void)hipFree(e->d_dbg);
+    (void)hipFree(e->d_scratch);
     delete e;
 }
 
@@ -100,13 +105,16 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     const ffm_engine_desc& d = *desc;
     if (d.abi_version != FFM_ABI_VERSION) return fail(FFM_E_INVALID, "abi_version mismatch");
     if (d.variant != FFM_VARIANT_CORE) return fail(FFM_E_UNSUPPORTED, "only FFM_VARIANT_CORE is built");
-    if (d.H < 3 || d.W < 3 || (long long)d.H * d.W > 65534)
-        return fail(FFM_E_INVALID, "map must be at least 3x3 and at most 65534 cells");
+    // Positions are u16 cell indices with 0xFFFF = none; a free cell is never on the
+    // border, so up to 65,536 cells (256 x 256) every stored cell is < 0xFFFF.
+    if (d.H < 3 || d.W < 3 || (long long)d.H * d.W > 65536)
+        return fail(FFM_E_INVALID, "map must be at least 3x3 and at most 65536 cells");
     if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
     if (d.neighborhood != 4 && d.neighborhood != 8) return fail(FFM_E_INVALID, "neighborhood must be 4 or 8");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
-    if (d.agent_capacity < 1 || d.agent_capacity > 65534) return fail(FFM_E_INVALID, "agent_capacity");
+    // the block kernel's grid codes hold a 15-bit agent index
+    if (d.agent_capacity < 1 || d.agent_capacity > 32767) return fail(FFM_E_INVALID, "agent_capacity");
     if (d.n_agents < 0 || d.n_agents > d.agent_capacity) return fail(FFM_E_INVALID, "n_agents > agent_capacity");
     if (d.rng_mode != FFM_RNG_PHILOX && d.rng_mode != FFM_RNG_MT) return fail(FFM_E_INVALID, "rng_mode");
     const int H = d.H, W = d.W, HW = H * W;
@@ -166,8 +174,18 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     if (e->mt) K = 1;
     while (K > 1 && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 64 * 1024) K--;
     e->K = K;
-    if (!e->wave && !e->lane && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 160 * 1024)
-        return cleanup(fail(FFM_E_UNSUPPORTED, "env does not fit in LDS (tiled large-map kernel not built yet)"));
+    // Maps whose env state exceeds the LDS, or whose padded cell indices exceed u16:
+    // the block kernel keeps grid, DFF tile, cell lists and placement keys in a
+    // global scratch region per block (one env per block).
+    e->big = !e->wave && !e->lane &&
+             ((size_t)(H + 2) * (W + 2) > 65535 ||
+              ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 64 * 1024);
+    if (e->big) e->K = 1;
+    // Philox placement of the whole free list in the wave reset's LDS, else by blocks
+    auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t wave_reset_lds = al16(8 * (size_t)std::max(1, e->F)) + al16(2 * (size_t)std::max(1, d.n_agents)) +
+                                  al16(2 * (size_t)std::max(1, e->F));   // launch_core_reset's carve
+    e->block_reset = !e->mt && wave_reset_lds > 64 * 1024;
 
     const size_t E = (size_t)d.n_envs;
     const int PW = W + 2, PHW = (H + 2) * PW;
@@ -197,6 +215,10 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_cnt, E * 4);
     ALLOC(e->d_dff, E * HW * 4);
     ALLOC(e->d_eps, E * 4);
+    if (e->big || e->block_reset) {
+        e->scratch_stride = (ffm::core_big_scratch_bytes(H, W, A, e->F, e->mt) + 255) & ~(size_t)255;
+        ALLOC(e->d_scratch, E * e->scratch_stride);
+    }
     // Grids.  Persistent wave and lane kernels: CUs x resident blocks per CU.
     int cus = 0;
     he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d.device);
@@ -306,6 +328,8 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
     a.mt_np = e->d_mt_np;
     a.mt_py = e->d_mt_py;
     a.dbg = e->d_dbg;
+    a.scratch = e->big ? e->d_scratch : nullptr;
+    a.scratch_stride = e->scratch_stride;
     return a;
 }
 
@@ -331,7 +355,13 @@ int ffm_engine_reset(ffm_engine* e, void* stream) {
     HIP_TRY(hipMemsetAsync(e->d_pos, 0xFF, E * e->d.agent_capacity * 2, s));
     if (e->mt) return FFM_OK;  // the caller uploads positions drawn from its own MT stream
     // Philox placement, same stream as the in-kernel auto-reset (key: current t).
-    HIP_TRY(ffm::launch_core_reset(make_args(e), s));
+    if (e->block_reset) {
+        ffm::CoreStepArgs a = make_args(e);
+        a.scratch = e->d_scratch;
+        HIP_TRY(ffm::launch_core_block_reset(a, s));
+    } else {
+        HIP_TRY(ffm::launch_core_reset(make_args(e), s));
+    }
     e->t++;
     return FFM_OK;
 }

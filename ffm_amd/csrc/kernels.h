@@ -31,6 +31,8 @@ struct CoreStepArgs {
     uint32_t* mt_np;       // [E][625] MT mode
     uint32_t* mt_py;       // [E][625]
     unsigned long long* dbg;  // diagnostic builds: [16] per-phase cycle sums (else unused)
+    unsigned char* scratch;   // big maps: [blocks][scratch_stride] block state (else nullptr)
+    size_t scratch_stride;
 };
 
 size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves);
@@ -43,6 +45,8 @@ int core_lane_blocks_per_cu(const CoreStepArgs& a, int nb);
 int core_lane_max_pairs_per_wave();
 hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
+size_t core_big_scratch_bytes(int H, int W, int A, int F, bool mt);
+hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,
                              float c1, hipStream_t s);
 hipError_t launch_np_expf(const float* x, float* y, long long n, hipStream_t s);
