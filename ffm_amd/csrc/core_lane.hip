@@ -31,6 +31,7 @@
 
 #include "core_common.h"
 #include "kernels.h"
+#include "lane_common.h"
 #include "wave_reset.h"
 
 #ifndef FFM_STAMPS
@@ -54,16 +55,6 @@
 namespace ffm {
 
 namespace {
-
-__host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
-
-// DFF tile of one env: 4 leading zero floats, H + 2 rows of W floats (a zero row
-// above and below the map; no halo columns, so the float4 slots of consecutive lanes
-// are consecutive and the 16-B accesses are bank-conflict free), 4 trailing zeros.
-// Cell (x, y) at 4 + (x + 1) * W + y.  Left / right neighbours across the map edge
-// are read from a zero word instead (the stencil) or belong to blocked cells whose
-// score is masked (decide).
-__host__ __device__ inline int lane_tile_floats(int H, int W) { return 4 + (H + 2) * W + 4; }
 
 struct LaneCarve {
     size_t grid, tile, words, keys, pend, per_wave;
@@ -92,210 +83,22 @@ __host__ __device__ inline size_t lane_shared_bytes(int PHW, int F) {
     return a16((size_t)PHW) + a16((size_t)PHW * 4) + a16((size_t)(F > 0 ? F : 1) * 2);
 }
 
-// Buffer resources over one env pair's rows of pos / cnt / DFF: a lane whose offset
-// is past the pair's bytes reads 0 and its store is dropped by the hardware, so no
-// load or store of the loop needs a lane branch, and the number of memory
-// instructions after the prefetch is fixed (the loop head then waits for the
-// prefetch only, not for the previous group's stores).
-constexpr int kOOB = 0x7FFFFFF0;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t pair_rsrc(const void* base, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
-}
-__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
-                                           off, 0, 0);
-}
-
-
-// Candidate cells, validity and float32 scores of decide() (model/ffm_core.py:41-80)
-// for the agent at padded cell pp; shared by the fast and the exact pass.
-template <int NB>
-__device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, const float* psff, const float* dk,
-                                           int dd0, float kS, float kD, bool (&v)[NB + 1], float (&xs)[NB + 1],
-                                           int& exit_slot) {
-    int cell[NB + 1], dcell[NB + 1];
-    uint32_t g[NB];
-    float sf[NB + 1], df[NB + 1];
-#pragma unroll
-    for (int s = 0; s < NB; s++) {
-        cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
-        dcell[s] = cell[s] + dd0 - nb_dx<NB>(s) * 2;   // the tile row is 2 shorter than the grid row
-        g[s] = gk[cell[s]];
-    }
-    cell[NB] = pp;
-    dcell[NB] = pp + dd0;
-#pragma unroll
-    for (int k = 0; k <= NB; k++) {
-        sf[k] = psff[cell[k]];
-        df[k] = dk[dcell[k]];
-    }
-    v[NB] = true;
-    int nvalid = 0;
-    exit_slot = -1;
-#pragma unroll
-    for (int s = NB - 1; s >= 0; s--) {
-        v[s] = g[s] == 0u || g[s] == 3u;                                 // :52-60
-        nvalid += v[s] ? 1 : 0;
-        exit_slot = g[s] == 3u ? s : exit_slot;                          // :66-72
-    }
-    float sc[NB + 1];
-#pragma unroll
-    for (int k = 0; k <= NB; k++) {
-        const float a = kS * sf[k];
-        const float b = kD * df[k];
-        sc[k] = a + b;                                                   // :77
-    }
-    float mx = -__builtin_inff();
-#pragma unroll
-    for (int k = 0; k <= NB; k++) mx = (v[k] && sc[k] > mx) ? sc[k] : mx;   // :78
-#pragma unroll
-    for (int k = 0; k <= NB; k++) xs[k] = v[k] ? sc[k] - mx : -__builtin_inff();
-    return nvalid;
-}
-
-// decide(), fast pass: returns the slot (0..NB-1 neighbour, NB stay), kNoReq, or
-// kPending when u lies within the margin of a cdf boundary.  The fast path compares
-// a float32 copy of u (|error| < 2^-24) inside fast_choice's 1e-4 margin; selects
-// only, no branch.
-template <int NB>
-__device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
-                                                const float* dk, int dd0, float kS, float kD, uint32_t wx,
-                                                bool& to_exit) {
-    bool v[NB + 1];
-    float xs[NB + 1];
-    int exit_slot;
-    const int nvalid = lane_scores<NB>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
-    float cum[NB + 1];
-    float acc = 0.0f;
-#pragma unroll
-    for (int k = 0; k <= NB; k++) {
-        const float e = __builtin_amdgcn_exp2f(xs[k] * 1.44269504088896341f);
-        acc += v[k] ? e : 0.0f;
-        cum[k] = v[k] ? acc : -1.0f;
-    }
-    const float uf = (float)(wx >> 8) * 0x1p-24f;
-    const float t = uf * acc;
-    const float d = kFastMargin * acc;
-    int slot = NB;
-    float cs = cum[NB];
-#pragma unroll
-    for (int k = NB - 1; k >= 0; k--) {
-        const bool ge = cum[k] >= t - d;
-        slot = ge ? k : slot;
-        cs = ge ? cum[k] : cs;
-    }
-    to_exit = exit_slot >= 0;
-    return nvalid == 0 ? (uint32_t)kNoReq                                // :63
-           : exit_slot >= 0 ? (uint32_t)exit_slot                        // :66-72, no draw
-           : cs > t + d ? (uint32_t)slot : (uint32_t)kPending;
-}
-
-// decide(), exact pass (rare): NumPy's float32 exp and add.reduce, float32 divide,
-// float64 cumsum, cdf /= cdf[-1], searchsorted(side="right") on the float64 u53.
-// Streams over the candidates, re-reading the scores from LDS in each of its passes
-// (max, sum, cdf total, search) with one candidate live at a time: this path sets
-// the kernel's register peak otherwise.  Neumann only (the 8-lane pairwise sum of
-// add.reduce needs every term at once: lane_decide_exact_arr).
-template <int NB>
-__device__ __forceinline__ float lane_score1(int k, int pp, int PW, const uint16_t* gk, const float* psff,
-                                             const float* dk, int dd0, float kS, float kD, bool& valid) {
-    int dx = 0, dy = 0;
-#pragma unroll
-    for (int s = 0; s < NB; s++) {
-        dx = k == s ? nb_dx<NB>(s) : dx;
-        dy = k == s ? nb_dy<NB>(s) : dy;
-    }
-    const int cell = pp + dx * PW + dy;
-    const uint32_t g = gk[cell];
-    valid = k == NB || g == 0u || g == 3u;
-    const float sa = kS * psff[cell];
-    const float sb = kD * dk[cell + dd0 - dx * 2];
-    return sa + sb;                                                      // :77
-}
-
-template <int NB>
-__device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint16_t* gk, const float* psff,
-                                                      const float* dk, int dd0, float kS, float kD, double u) {
-    float mx = -__builtin_inff();
-#pragma unroll 1
-    for (int k = 0; k <= NB; k++) {
-        bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
-        mx = (v && sc > mx) ? sc : mx;                                   // :78
-    }
-    float sum = -0.0f;                                                   // add.reduce, < 8 terms: left fold
-#pragma unroll 1
-    for (int k = 0; k <= NB; k++) {
-        bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
-        if (v) sum += np_expf(sc - mx);                                  // :80-81
-    }
-    double last = 0.0;
-#pragma unroll 1
-    for (int k = 0; k <= NB; k++) {
-        bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
-        if (v) last += (double)(np_expf(sc - mx) / sum);                 // :83, cumsum in choice
-    }
-    const double inv = 1.0 / last;
-    double run = 0.0;
-    uint32_t pick = NB;                                                  // cdf[-1] == 1 > u
-#pragma unroll 1
-    for (int k = 0; k < NB; k++) {
-        bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
-        if (v) {
-            run += (double)(np_expf(sc - mx) / sum);
-            if (cdf_gt(run, last, inv, u)) {
-                pick = (uint32_t)k;
-                break;
-            }
-        }
-    }
-    return pick;
-}
-
-// The same with every term held (Moore: add.reduce pairs 8 terms).
-template <int NB>
-__device__ __forceinline__ uint32_t lane_decide_exact_arr(int pp, int PW, const uint16_t* gk, const float* psff,
-                                                          const float* dk, int dd0, float kS, float kD, double u) {
-    bool v[NB + 1];
-    float xs[NB + 1];
-    int exit_slot;
-    const int nvalid = lane_scores<NB>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
-    float e[NB + 1];
-#pragma unroll
-    for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;   // :80
-    const float sum = np_sum<NB, float>(e, v, nvalid + 1);               // :81
-    double last = 0.0;
-#pragma unroll
-    for (int k = 0; k <= NB; k++)
-        if (v[k]) last += (double)(e[k] / sum);                          // :83, cumsum in choice
-    const double inv = 1.0 / last;
-    double run = 0.0;
-    uint32_t pick = NB;
-    bool found = false;
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-        if (v[k]) run += (double)(e[k] / sum);
-        if (v[k] && !found && cdf_gt(run, last, inv, u)) {
-            found = true;
-            pick = (uint32_t)k;
-        }
-    }
-    return pick;
-}
-
 }  // namespace
 
+#ifndef FFM_LANE_PIPE
+#define FFM_LANE_PIPE 0   // 1: the decide draws of the next pair are computed a pair ahead
+#endif
 #ifndef FFM_LANE_ABLATE
 #define FFM_LANE_ABLATE 0   // diagnostic builds only: bit k replaces / skips one piece (tools/ab_core.sh)
 #endif
 // Minimum waves per SIMD asked of the register allocator.  The 12x12 Neumann build
 // (BASELINE config 2) fits 7 (72 VGPRs, SGPR spills to VGPR lanes only, no scratch);
 // forcing 7 on the others spills to scratch, so they keep the compiler's choice.
+#ifndef FFM_LANE_WAVES
+#define FFM_LANE_WAVES 7   // diagnostic builds may lower / raise the 12x12 Neumann occupancy ask
+#endif
 template <int NB, int HT>
-constexpr int lane_waves() { return (NB == 4 && HT == 12) ? 7 : 1; }
+constexpr int lane_waves() { return (NB == 4 && HT == 12) ? FFM_LANE_WAVES : 1; }
 
 template <int NB, int HT, int WT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lane_waves<NB, HT>(), 8)))
@@ -395,6 +198,9 @@ void core_lane_kernel(CoreStepArgs a) {
     uint32_t* const pend = reinterpret_cast<uint32_t*>(wbase + cv.pend);
     if (lane < kLanePendWords) pend[lane] = 0u;
     const int g_first = g;
+#if FFM_LANE_PIPE
+    uint4 pbn = philox(make_uint4(a.t, ebase + (uint32_t)(g * 2 + sub), (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
+#endif
     for (int iter = 0; g < ngroups; g += wstride, iter++) {
         // ---- stage this pair's DFF (loaded by the previous iteration or the prologue) -----
         if (tb0 >= 0) *reinterpret_cast<float4*>(tile + tb0) = cur.d0;
@@ -422,13 +228,18 @@ void core_lane_kernel(CoreStepArgs a) {
 
         LSTAMP(0);
         // ---- decide (model/ffm_core.py:40-88) -------------------------------------------
+#if FFM_LANE_PIPE
+        const uint4 pb = pbn;
+#else
         const uint4 pb = (FFM_LANE_ABLATE & 1)
                              ? make_uint4(genv * 2654435761u ^ (uint32_t)al * 40503u ^ a.t * 97u,
                                           genv ^ (uint32_t)al * 7919u, a.t * 31u ^ genv, (uint32_t)al ^ a.t)
                              : philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
+#endif
         words[lane] = make_uint2(pb.z, pb.w);   // the friction draw, if this agent owns a contested target
         bool to_exit = false;
-        uint32_t slot = lane_decide<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
+        uint32_t slot = (FFM_LANE_ABLATE & 16) ? (uint32_t)NB
+                                               : lane_decide<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
         slot = live ? slot : kNoReq;
         if (slot == kPending)   // u near a cdf boundary: the exact NumPy arithmetic decides
             slot = NB == 4 ? lane_decide_exact<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, u53(pb.x, pb.y))
@@ -508,6 +319,11 @@ void core_lane_kernel(CoreStepArgs a) {
         // next group's head ------------------------------------------------------------
         LaneState nxt;
         load(g + wstride < ngroups ? g + wstride : -1, nxt);
+#if FFM_LANE_PIPE
+        // the next pair's decide draws: counter-based, so they need no state of this step
+        pbn = philox(make_uint4(a.t, ebase + (uint32_t)((g + wstride) * 2 + sub), (uint32_t)al, kPurDecide << 28),
+                     a.key0, a.key1);
+#endif
 
         LSTAMP(5);
         // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb] -----
@@ -564,7 +380,7 @@ void core_lane_kernel(CoreStepArgs a) {
             const int bit = w * 32 + __builtin_ctz(m);
             m &= m - 1u;
             const int e = (g_first + (bit >> 1) * wstride) * 2 + (bit & 1);
-            wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + (long long)e * A, lane);
+            if (!(FFM_LANE_ABLATE & 64)) wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + (long long)e * A, lane);
         }
     }
 

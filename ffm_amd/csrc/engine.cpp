@@ -52,6 +52,8 @@ struct ffm_engine {
     bool wave = false;      // wave-per-env kernel (A <= 64) vs block-per-env kernel
     int wave_blocks = 0;    // persistent grid of the wave kernel
     int lane_blocks = 0;    // persistent grid of the lane kernel
+    bool group = false;     // group kernel (lane conditions at 12x12): core_group.hip
+    int group_blocks = 0;   // persistent grid of the group kernel
     float kS32 = 0, kD32 = 0, c0 = 0, c1 = 0;
     double kS64 = 0;
     uint32_t t = 0;
@@ -163,11 +165,14 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     const int EW = A <= 32 ? 2 : 1;
     // envs_per_block: 0 = auto (lane kernel, else wave kernel, where they fit; else
     // block kernel), > 0 = block kernel with that many envs per workgroup,
-    // -1 = wave kernel, -2 = lane kernel.
-    e->lane = (d.envs_per_block == 0 || d.envs_per_block == -2) && !e->mt && !e->f64 && A <= 32 && W % 4 == 0 &&
-              HW <= 256 && ffm::core_lane_smem_bytes(H, W, e->F, 4) <= 64 * 1024 &&
-              (long long)d.n_envs * HW * 4 < (1ll << 31);   // 32-bit buffer offsets
-    e->wave = !e->lane && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
+    // -1 = wave kernel, -2 = lane kernel, -3 = group kernel.
+    const bool lane_ok = !e->mt && !e->f64 && A <= 32 && W % 4 == 0 && HW <= 256 &&
+                         (long long)d.n_envs * HW * 4 < (1ll << 31);   // 32-bit buffer offsets
+    e->group = (d.envs_per_block == 0 || d.envs_per_block == -3) && lane_ok && ffm::core_group_supported(H, W) &&
+               ffm::core_group_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
+    e->lane = !e->group && (d.envs_per_block == 0 || d.envs_per_block == -2) && lane_ok &&
+              ffm::core_lane_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
+    e->wave = !e->lane && !e->group && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
               ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
     int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);
@@ -177,7 +182,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     // Maps whose env state exceeds the LDS, or whose padded cell indices exceed u16:
     // the block kernel keeps grid, DFF tile, cell lists and placement keys in a
     // global scratch region per block (one env per block).
-    e->big = !e->wave && !e->lane &&
+    e->big = !e->wave && !e->lane && !e->group &&
              ((size_t)(H + 2) * (W + 2) > 65535 ||
               ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 64 * 1024);
     if (e->big) e->K = 1;
@@ -248,6 +253,19 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
             const long long per_wave = ffm::core_lane_max_pairs_per_wave();
             e->lane_blocks = (int)std::max<long long>(e->lane_blocks, (groups + 4 * per_wave - 1) / (4 * per_wave));
         }
+        if (e->group) {
+            const int per_cu = std::max(1, ffm::core_group_blocks_per_cu(a, d.neighborhood));
+            const long long G = ffm::core_group_envs();
+            const long long groups = (d.n_envs + G - 1) / G;
+            e->group_blocks = (int)std::max<long long>(1, std::min<long long>((groups + 3) / 4, (long long)cus * per_cu));
+            if (const char* ov = std::getenv("FFM_WAVE_BLOCKS")) {   // diagnostic override of the grid
+                const long long v = std::atoll(ov);
+                if (v > 0) e->group_blocks = (int)std::min<long long>(v, (groups + 3) / 4);
+            }
+            // every wave steps at most core_group_max_iters() groups (its deferred-reset mask)
+            const long long per_wave = ffm::core_group_max_iters();
+            e->group_blocks = (int)std::max<long long>(e->group_blocks, (groups + 4 * per_wave - 1) / (4 * per_wave));
+        }
     }
     // One counter slot per wave (wave / lane kernel) or block (block kernel):
     // summed by ffm_engine_get_counters, never contended on the device.
@@ -256,7 +274,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
         const long long blocks = (d.n_envs + K - 1) / K;
         e->ctr_slots = (size_t)std::max<long long>(std::max<long long>(std::max<long long>(1, blocks),
                                                                        (groups + 3) / 4 * 4),
-                                                   (long long)e->lane_blocks * 4);
+                                                   (long long)std::max(e->lane_blocks, e->group_blocks) * 4);
     }
     ALLOC(e->d_ctr, e->ctr_slots * 32);
     ALLOC(e->d_dbg, 16 * 8);
@@ -338,7 +356,8 @@ int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     for (int i = 0; i < n_steps; i++) {
         ffm::CoreStepArgs a = make_args(e);
-        if (e->lane) HIP_TRY(ffm::launch_core_lane(a, e->d.neighborhood, e->lane_blocks, s));
+        if (e->group) HIP_TRY(ffm::launch_core_group(a, e->d.neighborhood, e->group_blocks, s));
+        else if (e->lane) HIP_TRY(ffm::launch_core_lane(a, e->d.neighborhood, e->lane_blocks, s));
         else if (e->wave) HIP_TRY(ffm::launch_core_wave(a, e->d.neighborhood, e->mt, e->wave_blocks, s));
         else HIP_TRY(ffm::launch_core_block(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
         e->t++;

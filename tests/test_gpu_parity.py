@@ -162,25 +162,25 @@ def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0
     return cnt, eps
 
 
-@pytest.mark.parametrize("epb", [0, -1])
+@pytest.mark.parametrize("epb", [0, -2, -1])
 def test_philox_config2_full_size_matches_cpu(epb):
     """12x12, 32 agents, 65,536 envs (BASELINE config 2) for 150 steps (epb=0: auto,
-    the lane kernel; epb=-1: the wave kernel)."""
+    the group kernel; -2: the lane kernel; -1: the wave kernel)."""
     cnt, eps = _philox_compare(12, 12, 32, 65536, 150,
                                {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"},
                                envs_per_block=epb)
     assert eps.sum() > 0  # auto-reset exercised
 
 
-@pytest.mark.parametrize("epb", [-2, -1, 3])
+@pytest.mark.parametrize("epb", [-3, -2, -1, 3])
 @pytest.mark.parametrize("N", [32, 60])
 @pytest.mark.parametrize("params", [
     {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "moore"},
     {"k_S": 1.5, "k_D": 2.5, "diffuse": 0.3, "decay": 0.1, "neighborhood": "neumann"},
 ])
 def test_philox_12x12_param_points(params, N, epb):
-    """All kernels (epb=-2: lane kernel where A <= 32, else the block kernel; -1: wave
-    kernel, 2 or 1 env per wave; 3: block kernel, odd K)."""
+    """All kernels (epb=-3 / -2: group / lane kernel where A <= 32, else the block
+    kernel; -1: wave kernel, 2 or 1 env per wave; 3: block kernel, odd K)."""
     _philox_compare(12, 12, N, 2047, 120, params, seed=7, envs_per_block=epb)
 
 
@@ -191,10 +191,20 @@ def test_philox_odd_shapes():
     _philox_compare(20, 11, 40, 301, 80, {"neighborhood": "moore"}, seed=5, env_base=1 << 20)
 
 
+@pytest.mark.parametrize("epb", [-3, -2])
 @pytest.mark.parametrize("E", [1, 5, 333, 5121])
-def test_philox_lane_small_and_ragged_env_counts(E):
-    """Lane kernel with fewer envs than waves, an odd env count (half-empty last pair)."""
-    _philox_compare(12, 12, 32, E, 90, {"neighborhood": "neumann"}, seed=11, envs_per_block=-2)
+def test_philox_lane_small_and_ragged_env_counts(E, epb):
+    """Group / lane kernel with fewer envs than waves, env counts that leave the last
+    group or pair part empty."""
+    _philox_compare(12, 12, 32, E, 90, {"neighborhood": "neumann"}, seed=11, envs_per_block=epb)
+
+
+@pytest.mark.parametrize("N", [1, 7, 19])
+def test_philox_group_few_agents(N):
+    """Group kernel with few agents per env (many envs per chunk, odd position
+    strides), Moore and Neumann."""
+    _philox_compare(12, 12, N, 3001, 70, {"neighborhood": "neumann"}, seed=21, envs_per_block=-3)
+    _philox_compare(12, 12, N, 1003, 70, {"neighborhood": "moore", "k_D": 2}, seed=22, envs_per_block=-3)
 
 
 def test_philox_lane_shapes():
