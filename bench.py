@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed regions of K steps each, back to back; value = their median (BASELINE.md 3)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--multi-step", type=int, default=10,
+                    help="configs 2/3: also time step(K) with this many steps fused per launch "
+                         "(ffm_engine_set_fused_steps; a secondary field, 0 = skip)")
     ap.add_argument("--log2-table", type=int, default=0, help="learner V/H hash capacity (0 = engine default)")
     ap.add_argument("--sync-period", type=int, default=1,
                     help="learner configs: apply / exchange the tables every K steps (1 = the reference's per-step)")
@@ -140,6 +143,23 @@ def main():
     # number of bytes one launch moves (read + write), for context beside `peak`.
     copy_gbs = copy_bandwidth(torch, stream, E * (2 * A + 4 * H * W + 4))
 
+    # Secondary line: the same steps with K fused per launch (state on chip between
+    # the K steps of an env pair; bit-identical results, tests/test_gpu_parity.py).
+    multi = None
+    if args.multi_step > 1:
+        eng.set_fused_steps(args.multi_step)
+        eng.step(args.multi_step, stream)
+        torch.cuda.synchronize()
+        mr = timed_repeats(args, world, dist, torch, lambda: eng.step(args.steps, stream),
+                           lambda: eng.counters(stream))
+        eng.set_fused_steps(1)
+        multi = {"fused_steps": args.multi_step, "value": mr["agent_steps"] / mr["elapsed"],
+                 "unit": "agent-steps/s", "ms_per_step": mr["elapsed"] / args.steps * 1e3,
+                 "env_steps_per_s": E * world * args.steps / mr["elapsed"],
+                 "repeats": mr["summary"],
+                 "note": "ffm_engine_step(K) with K steps per launch (core_multi_kernel where the shape "
+                         "allows it, else one launch per step); the headline value is one launch per step"}
+
     if rank == 0:
         bytes_per_env_step = 2 * (2 * A + 4 * H * W + 4)
         mean_kernel_s = float(np.mean(kern_ms)) / 1e3
@@ -183,6 +203,7 @@ def main():
                 "frac_of_copy": achieved / copy_gbs if copy_gbs else None,
             },
             "cpu_baseline": None,
+            "multi_step": multi,
         }
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args, m, s, params, torch)

@@ -15,8 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "libffm_amd.so")
-SOURCES = ["core_step.hip", "core_lane.hip", "core_group.hip", "learn_step.hip", "engine.cpp", "learn_engine.cpp"]
-HEADERS = ["device_common.h", "core_common.h", "kernels.h", "learn_kernels.h", os.path.join("..", "..", "include", "ffm_amd.h")]
+SOURCES = ["core_step.hip", "core_lane.hip", "core_group.hip", "core_multi.hip", "learn_step.hip", "engine.cpp", "learn_engine.cpp"]
+HEADERS = ["device_common.h", "core_common.h", "lane_common.h", "wave_reset.h", "kernels.h", "learn_kernels.h", os.path.join("..", "..", "include", "ffm_amd.h")]
 ARCH = os.environ.get("FFM_OFFLOAD_ARCH", "gfx950")
 FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",

@@ -54,6 +54,9 @@ struct ffm_engine {
     int lane_blocks = 0;    // persistent grid of the lane kernel
     bool group = false;     // group kernel (lane conditions at 12x12): core_group.hip
     int group_blocks = 0;   // persistent grid of the group kernel
+    bool multi = false;     // multi-step kernel available (lane conditions): core_multi.hip
+    int multi_blocks = 0;   // its persistent grid
+    int fused = 1;          // steps per launch (ffm_engine_set_fused_steps)
     float kS32 = 0, kD32 = 0, c0 = 0, c1 = 0;
     double kS64 = 0;
     uint32_t t = 0;
@@ -170,6 +173,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
                          (long long)d.n_envs * HW * 4 < (1ll << 31);   // 32-bit buffer offsets
     e->group = (d.envs_per_block == 0 || d.envs_per_block == -3) && lane_ok && ffm::core_group_supported(H, W) &&
                ffm::core_group_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
+    e->multi = lane_ok && ffm::core_multi_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
     e->lane = !e->group && (d.envs_per_block == 0 || d.envs_per_block == -2) && lane_ok &&
               ffm::core_lane_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
     e->wave = !e->lane && !e->group && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
@@ -253,6 +257,11 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
             const long long per_wave = ffm::core_lane_max_pairs_per_wave();
             e->lane_blocks = (int)std::max<long long>(e->lane_blocks, (groups + 4 * per_wave - 1) / (4 * per_wave));
         }
+        if (e->multi) {
+            const int per_cu = std::max(1, ffm::core_multi_blocks_per_cu(a, d.neighborhood));
+            const long long pairs = (d.n_envs + 1) / 2;
+            e->multi_blocks = (int)std::max<long long>(1, std::min<long long>((pairs + 3) / 4, (long long)cus * per_cu));
+        }
         if (e->group) {
             const int per_cu = std::max(1, ffm::core_group_blocks_per_cu(a, d.neighborhood));
             const long long G = ffm::core_group_envs();
@@ -274,7 +283,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
         const long long blocks = (d.n_envs + K - 1) / K;
         e->ctr_slots = (size_t)std::max<long long>(std::max<long long>(std::max<long long>(1, blocks),
                                                                        (groups + 3) / 4 * 4),
-                                                   (long long)std::max(e->lane_blocks, e->group_blocks) * 4);
+                                                   (long long)std::max(std::max(e->lane_blocks, e->group_blocks), e->multi_blocks) * 4);
     }
     ALLOC(e->d_ctr, e->ctr_slots * 32);
     ALLOC(e->d_dbg, 16 * 8);
@@ -354,6 +363,17 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
 int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     if (!e || n_steps < 0) return fail(FFM_E_INVALID, "bad engine/n_steps");
     hipStream_t s = (hipStream_t)stream;
+    if (e->fused > 1 && e->multi) {
+        // k steps per launch, the state of each env pair on chip (core_multi.hip)
+        for (int done = 0; done < n_steps;) {
+            const int k = std::min(e->fused, n_steps - done);
+            ffm::CoreStepArgs a = make_args(e);
+            HIP_TRY(ffm::launch_core_multi(a, e->d.neighborhood, k, e->multi_blocks, s));
+            e->t += (uint32_t)k;
+            done += k;
+        }
+        return FFM_OK;
+    }
     for (int i = 0; i < n_steps; i++) {
         ffm::CoreStepArgs a = make_args(e);
         if (e->group) HIP_TRY(ffm::launch_core_group(a, e->d.neighborhood, e->group_blocks, s));
@@ -362,6 +382,12 @@ int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
         else HIP_TRY(ffm::launch_core_block(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
         e->t++;
     }
+    return FFM_OK;
+}
+
+int ffm_engine_set_fused_steps(ffm_engine* e, int32_t k) {
+    if (!e || k < 1) return fail(FFM_E_INVALID, "fused steps must be >= 1");
+    e->fused = k;
     return FFM_OK;
 }
 

@@ -49,6 +49,9 @@ int core_group_envs();
 int core_group_max_iters();
 hipError_t launch_core_group(const CoreStepArgs& a, int nb, int blocks, hipStream_t s);
 int core_group_blocks_per_cu(const CoreStepArgs& a, int nb);
+size_t core_multi_smem_bytes(int H, int W, int F, int waves);
+hipError_t launch_core_multi(const CoreStepArgs& a, int nb, int nsteps, int blocks, hipStream_t s);
+int core_multi_blocks_per_cu(const CoreStepArgs& a, int nb);
 hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
 hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
 size_t core_big_scratch_bytes(int H, int W, int A, int F, bool mt);

@@ -27,7 +27,7 @@ EXPORTED = [
     "ffm_engine_reset", "ffm_engine_step", "ffm_engine_update_dff", "ffm_engine_set_state",
     "ffm_engine_get_state", "ffm_engine_set_mt_state", "ffm_engine_get_mt_state",
     "ffm_engine_get_counters", "ffm_engine_device_buffers", "ffm_engine_get_step_index",
-    "ffm_engine_set_step_index", "ffm_np_expf_device",
+    "ffm_engine_set_step_index", "ffm_engine_set_fused_steps", "ffm_np_expf_device",
     "ffm_learner_create", "ffm_learner_destroy", "ffm_learner_reset", "ffm_learner_step",
     "ffm_learner_set_state", "ffm_learner_get_state", "ffm_learner_get_episodes",
     "ffm_learner_set_mt_state", "ffm_learner_get_mt_state", "ffm_learner_get_counters",
@@ -108,6 +108,7 @@ def load_library():
     L.ffm_engine_device_buffers.argtypes = [P, C.POINTER(DeviceBuffers)]
     L.ffm_engine_get_step_index.argtypes = [P, C.POINTER(C.c_uint32)]
     L.ffm_engine_set_step_index.argtypes = [P, C.c_uint32]
+    L.ffm_engine_set_fused_steps.argtypes = [P, i32]
     L.ffm_np_expf_device.argtypes = [P, P, i64, P]
     L.ffm_learner_create.argtypes = [C.POINTER(EngineDesc), C.POINTER(LearnDesc), C.POINTER(P)]
     L.ffm_learner_destroy.argtypes = [P]
@@ -269,6 +270,10 @@ class Engine:
 
     def step(self, n_steps: int = 1, stream=None):
         _check(self._L.ffm_engine_step(self._h, int(n_steps), _stream_handle(stream)))
+
+    def set_fused_steps(self, k: int):
+        """Steps per launch in step(n) (1 = one launch per step); see ffm_engine_set_fused_steps."""
+        _check(self._L.ffm_engine_set_fused_steps(self._h, int(k)))
 
     def update_dff(self, stream=None):
         _check(self._L.ffm_engine_update_dff(self._h, _stream_handle(stream)))

@@ -117,6 +117,13 @@ int ffm_engine_reset(ffm_engine* eng, void* stream);
 /* Advance every env by n_steps steps (model/ffm_core.py:36-104 each). */
 int ffm_engine_step(ffm_engine* eng, int32_t n_steps, void* stream);
 
+/* Steps fused per launch by ffm_engine_step (default 1: one launch per step).
+ * k > 1 lets Philox engines of the small-env kernels (A <= 32, W % 4 == 0,
+ * H*W <= 256, float32 SFF) step each env pair k times with its state on chip;
+ * results equal k single steps bit for bit.  Other engines keep one launch per
+ * step.  Returns FFM_E_INVALID for k < 1. */
+int ffm_engine_set_fused_steps(ffm_engine* eng, int32_t k);
+
 /* Only the diffusion/decay of the DFF (model/ffm_core.py:106-117). */
 int ffm_engine_update_dff(ffm_engine* eng, void* stream);
 

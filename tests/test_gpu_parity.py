@@ -128,7 +128,7 @@ def test_dropin_model_runs_main_py_config():
 # ---------------------------------------------------------------------------
 # Philox mode: GPU == CPU restatement at scale
 # ---------------------------------------------------------------------------
-def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0, nthreads=16):
+def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0, nthreads=16, fused=1):
     from ffm_amd.data import make_room, l1_sff
     from oracle import oracle as O
     m = make_room(H, W)
@@ -148,6 +148,8 @@ def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0
     cnt[:] = N
     for t in range(1, T + 1):
         cpu_steps += core.step_philox_batch(pos, cnt, dff, eps, seed, t, True, N, env_base, nthreads)
+    if fused > 1:
+        eng.set_fused_steps(fused)
     eng.step(T)
     gpos, gcnt, gdff = eng.get_state()
     assert np.array_equal(gcnt, cnt), "counts"
@@ -213,6 +215,29 @@ def test_philox_lane_shapes():
     _philox_compare(14, 16, 20, 999, 90, {"neighborhood": "moore", "k_D": 2}, seed=3, envs_per_block=-2)
     _philox_compare(8, 8, 3, 1000, 60, {"neighborhood": "neumann"}, seed=4, env_base=12345,
                     envs_per_block=-2)
+
+
+@pytest.mark.parametrize("fused", [10, 7])
+def test_philox_multi_step_config2_full_size(fused):
+    """K steps per launch (core_multi_kernel, state on chip) at BASELINE config 2:
+    150 steps in launches of 10 (or 7: a short last launch) equal 150 single steps."""
+    cnt, eps = _philox_compare(12, 12, 32, 65536, 150,
+                               {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"},
+                               fused=fused)
+    assert eps.sum() > 0  # inline auto-reset exercised
+
+
+@pytest.mark.parametrize("args", [
+    (12, 12, 32, 2047, 120, {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "moore"}, 9),
+    (12, 12, 32, 5, 90, {"neighborhood": "neumann"}, 4),
+    (12, 12, 32, 1, 90, {"neighborhood": "neumann"}, 90),
+    (14, 16, 20, 999, 90, {"neighborhood": "moore", "k_D": 2}, 8),
+    (8, 8, 3, 1000, 60, {"neighborhood": "neumann"}, 16),
+    (64, 64, 512, 64, 30, {"neighborhood": "neumann"}, 10),   # not a multi-step shape: one launch per step
+])
+def test_philox_multi_step_shapes(args):
+    H, W, N, E, T, params, k = args
+    _philox_compare(H, W, N, E, T, params, seed=31, fused=k)
 
 
 def test_philox_config3_64x64_matches_cpu():
