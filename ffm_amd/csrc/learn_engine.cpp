@@ -37,6 +37,7 @@ int fail(int code, const std::string& msg) { return ffm::set_error(code, msg); }
 struct DevTable {
     ffm::LearnTable t{};
     int width = 1;
+    int accw = 1;      // accumulator words per slot: V 2 (sum of td, visits), H 5
     size_t cap = 0;
 };
 
@@ -119,6 +120,8 @@ static void release(ffm_learner* l) {
 // the next power of two >= 256 * Bx * By and the table can never fill.
 static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dense_by = 0, size_t dense_n = 0) {
     T.width = width;
+    T.accw = width == 1 ? 2 : width;
+    T.t.accw = (uint32_t)T.accw;
     if (dense_by) {
         log2cap = 8;
         while (((size_t)1 << log2cap) < dense_n) log2cap++;
@@ -130,7 +133,7 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     hipError_t e;
     T.t.stride = width == 1 ? 2 : 8;        // 16 B / 64 B records (key + values [+ pad])
     if ((e = hipMalloc((void**)&T.t.rec, T.cap * T.t.stride * 8)) != hipSuccess) return e;
-    if ((e = hipMalloc((void**)&T.t.acc, T.cap * width * 8)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&T.t.acc, T.cap * T.accw * 8)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.order, T.cap * 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.n, 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.mark, 4)) != hipSuccess) return e;
@@ -191,7 +194,7 @@ static hipError_t clear_table(ffm_learner* l, DevTable& T, double dflt, hipStrea
     hipError_t e;
     (void)l;
     if (T.t.present && (e = hipMemsetAsync(T.t.present, 0, T.cap / 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.width * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.accw * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.n, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.mark, 0, 4, s)) != hipSuccess) return e;
     return ffm::launch_learn_clear(T.t, T.width, T.width == 1 ? dflt : 0.0, s);
@@ -333,6 +336,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         }
     }
     l->dense_bx = dense_by ? (uint32_t)((H - 1) / learn->block_size + 1) : 0;
+    l->V.t.alpha = l->L.alpha_v;   // the visit-averaged V update (learn_step.hip v_visits)
     if ((he = alloc_table(l->V, l->L.log2_v_capacity, 1, dense_by, dense_n)) != hipSuccess ||
         (he = alloc_table(l->H, l->actor || l->trained ? l->L.log2_h_capacity : 8, 5,
                           l->actor || l->trained ? dense_by : 0, dense_n)) != hipSuccess)
@@ -497,7 +501,7 @@ int ffm_learner_delta_export(ffm_learner* l, int32_t which, uint64_t* d_keys, in
     if (cap > 0 && (!d_keys || !d_acc)) return fail(FFM_E_INVALID, "null record buffers");
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemsetAsync(l->d_count, 0, 8, s));
-    HIP_TRY(ffm::launch_learn_delta_export(T->t, T->width, reinterpret_cast<unsigned long long*>(d_keys),
+    HIP_TRY(ffm::launch_learn_delta_export(T->t, T->accw, reinterpret_cast<unsigned long long*>(d_keys),
                                            reinterpret_cast<long long*>(d_acc), cap, l->d_count, s));
     unsigned long long c = 0;
     HIP_TRY(hipMemcpyAsync(&c, l->d_count, 8, hipMemcpyDeviceToHost, s));
@@ -513,7 +517,7 @@ int ffm_learner_delta_merge(ffm_learner* l, int32_t which, const uint64_t* d_key
     DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
     if (l->phase == 0) return fail(FFM_E_INVALID, "delta_merge outside a phased step");
-    HIP_TRY(ffm::launch_learn_delta_merge(T->t, T->width, reinterpret_cast<const unsigned long long*>(d_keys),
+    HIP_TRY(ffm::launch_learn_delta_merge(T->t, T->accw, reinterpret_cast<const unsigned long long*>(d_keys),
                                           reinterpret_cast<const long long*>(d_acc), n, l->d_overflow,
                                           (hipStream_t)stream));
     return FFM_OK;
@@ -796,7 +800,7 @@ int ffm_learner_delta_export_async(ffm_learner* l, int32_t which, uint64_t* d_ke
     hipStream_t s = (hipStream_t)stream;
     auto* cnt = reinterpret_cast<unsigned long long*>(d_count);
     HIP_TRY(hipMemsetAsync(cnt, 0, 8, s));
-    HIP_TRY(ffm::launch_learn_delta_export(T->t, T->width, reinterpret_cast<unsigned long long*>(d_keys),
+    HIP_TRY(ffm::launch_learn_delta_export(T->t, T->accw, reinterpret_cast<unsigned long long*>(d_keys),
                                            reinterpret_cast<long long*>(d_acc), cap, cnt, s));
     HIP_TRY(ffm::launch_learn_delta_check(cnt, cap, l->d_overflow, s));
     return FFM_OK;
@@ -808,7 +812,7 @@ int ffm_learner_delta_merge_async(ffm_learner* l, int32_t which, const uint64_t*
     DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
     if (l->phase == 0) return fail(FFM_E_INVALID, "delta_merge outside a phased step");
-    HIP_TRY(ffm::launch_learn_delta_merge(T->t, T->width, reinterpret_cast<const unsigned long long*>(d_keys),
+    HIP_TRY(ffm::launch_learn_delta_merge(T->t, T->accw, reinterpret_cast<const unsigned long long*>(d_keys),
                                           reinterpret_cast<const long long*>(d_acc), cap, l->d_overflow,
                                           (hipStream_t)stream, reinterpret_cast<const long long*>(d_count)));
     return FFM_OK;
@@ -836,7 +840,7 @@ int ffm_learner_dense_buffers(ffm_learner* l, int32_t which, int64_t** d_acc, in
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
     if (!T->t.dense_by) return fail(FFM_E_UNSUPPORTED, "not a dense (rank-key) table");
     *d_acc = reinterpret_cast<int64_t*>(T->t.acc);
-    *acc_count = (int64_t)(T->cap * (size_t)T->width);
+    *acc_count = (int64_t)(T->cap * (size_t)T->accw);
     *d_present = T->t.present;
     *present_words = (int64_t)(T->cap / 32);
     return FFM_OK;

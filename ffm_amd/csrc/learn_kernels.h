@@ -26,7 +26,14 @@ struct LearnTable {
     // values it then reads share one line: 16 B records for V, 64 B for H.
     unsigned long long* rec;
     uint32_t stride;
-    long long* acc;             // [cap * width] fixed-point (2^-32) increments of the batched step
+    // Batched-step accumulators, accw words per slot.  H (accw = width = 5): the
+    // fixed-point (2^-32) sum of alpha_h * td per action.  V (accw = 2): the
+    // fixed-point sum of td and the visit count k; the apply moves V by
+    // (1 - (1 - alpha)^k) * mean(td), the result of k sequential TD(0) updates
+    // towards one target.
+    long long* acc;
+    uint32_t accw;
+    double alpha;               // V: alpha_v (the visit-averaged update); H: unused
     uint32_t* order;            // [cap] slot of the i-th inserted key
     uint32_t* n;                // [1] keys inserted
     uint32_t* mark;             // [1] n at the start of the current batched step (delta export)

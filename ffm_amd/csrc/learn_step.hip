@@ -69,6 +69,19 @@ __device__ __forceinline__ long long fx(double v) {
     return (long long)q;
 }
 
+// V after k visits of one batched step with summed fixed-point td q: k sequential
+// TD(0) updates towards the mean target, V + (1 - (1 - alpha)^k) * mean(td)
+// (oracle/ffm_learn_oracle.c ffo_v_visits: the same operation sequence).
+__device__ __forceinline__ double v_visits(double v, long long q, long long k, double alpha) {
+    const double mean = (double)q * (1.0 / kFxOne) / (double)k;
+    double p = 1.0, b = 1.0 - alpha;
+    for (long long e = k; e; e >>= 1) {
+        if (e & 1) p = p * b;
+        b = b * b;
+    }
+    return v + (1.0 - p) * mean;
+}
+
 __device__ __forceinline__ void acc_add(long long* p, long long q) {
     atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)q);
 }
@@ -1384,7 +1397,10 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         }
         if (sv < 0) continue;
         const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
-        if (!(FFM_LABLATE & 1)) acc_add(a.V.acc + sv, fx(a.alpha_v * td));
+        if (!(FFM_LABLATE & 1)) {
+            acc_add(a.V.acc + 2 * (size_t)sv, fx(td));
+            acc_add(a.V.acc + 2 * (size_t)sv + 1, 1);
+        }
         if (!actor) continue;
         if (act[j] < 0) continue;
         if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
@@ -1549,8 +1565,17 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
     int nf = 0;
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint32_t slot = T.order[i];
-        const size_t s = (size_t)slot * WIDTH;
         double* vp = tval(T, slot);
+        if (WIDTH == 1) {   // V: visit-averaged
+            const long long k = T.acc[2 * (size_t)slot + 1];
+            if (k != 0) {
+                vp[0] = v_visits(vp[0], T.acc[2 * (size_t)slot], k, T.alpha);
+                T.acc[2 * (size_t)slot] = 0;
+                T.acc[2 * (size_t)slot + 1] = 0;
+            }
+            continue;
+        }
+        const size_t s = (size_t)slot * WIDTH;
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
             const long long q = T.acc[s + k];
@@ -1583,8 +1608,17 @@ __global__ __launch_bounds__(256) void learn_apply_dense_kernel(LearnTable T, do
         // the record and accumulators are loaded with the presence word, not after it
         // (an absent slot holds the default and a zero accumulator)
         const bool pres = (T.present[slot >> 5] >> (slot & 31)) & 1u;
-        const size_t s = slot * WIDTH;
         double* vp = tval(T, slot);
+        if (WIDTH == 1) {   // V: visit-averaged (an absent slot has no visits)
+            const long long q = T.acc[2 * slot], k = T.acc[2 * slot + 1];
+            if (k != 0) {
+                vp[0] = v_visits(vp[0], q, k, T.alpha);
+                T.acc[2 * slot] = 0;
+                T.acc[2 * slot + 1] = 0;
+            }
+            continue;
+        }
+        const size_t s = slot * WIDTH;
         long long qa[WIDTH];
         double va[WIDTH];
 #pragma unroll
@@ -2045,7 +2079,7 @@ hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
 
 hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
                                     long long cap, unsigned long long* count, hipStream_t s) {
-    if (width == 1) learn_delta_export_kernel<1><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
+    if (width == 2) learn_delta_export_kernel<2><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
     else learn_delta_export_kernel<5><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
     return hipGetLastError();
 }
@@ -2055,7 +2089,7 @@ hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsign
                                    const long long* dn) {
     if (n <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)std::min<long long>(4096, (n + 255) / 256);
-    if (width == 1) learn_delta_merge_kernel<1><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
+    if (width == 2) learn_delta_merge_kernel<2><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
     else learn_delta_merge_kernel<5><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
     return hipGetLastError();
 }

@@ -104,7 +104,7 @@ class TableSync:
     def _record_buffers(self, which: str):
         b = self.bufs.get(which)
         if b is None:
-            width, cap, w, dev = (1 if which == "V" else 5), self.capacity, self.world, self.device
+            width, cap, w, dev = (2 if which == "V" else 5), self.capacity, self.world, self.device
             b = (torch.zeros(cap, dtype=torch.int64, device=dev),
                  torch.zeros((cap, width), dtype=torch.int64, device=dev),
                  torch.zeros(1, dtype=torch.int64, device=dev),
@@ -172,7 +172,7 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
         s.set_sync_period(sync_period)
 
     def export(s, which):
-        width = 1 if which == "V" else 5
+        width = 2 if which == "V" else 5   # accumulator words (V: sum of td, visits)
         cap = capacity
         while True:
             k = torch.empty(cap, dtype=torch.int64, device=device)

@@ -40,6 +40,16 @@ def available_cells(map_array, exit_pos, radius) -> int:
     return int((np.abs(free[:, 0] - exit_pos[0]) + np.abs(free[:, 1] - exit_pos[1]) <= radius).sum())
 
 
+def load_critic(L: Learner, path: str):
+    """Import a V table pickled by write_outputs (a dict keyed like the reference's V)."""
+    with open(path, "rb") as f:
+        table = pickle.load(f)   # written by this tool (write_outputs), never a reference file
+    conv = K.from_rank_tuple if L.variant in ("unified", "trained") else K.from_cells_bytes
+    keys = np.array([conv(k) for k in table], np.uint64)
+    vals = np.array(list(table.values()), np.float64)
+    L.import_table("V", keys, vals)
+
+
 def _key_obj(variant, k):
     return K.to_rank_tuple(k) if variant in ("unified", "trained") else K.to_cells_bytes(k)
 
@@ -188,6 +198,9 @@ def main():
     ap.add_argument("--eps", default="0.2,0.01", help="epsilon start,end (actor modes)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--critic", default=None,
+                    help="pretrained V table (a V_table.pkl this tool wrote; the reference's actor drivers "
+                         "load their critic run's pickle, run_unified_actor_training.py PRETRAINED_CRITIC)")
     ap.add_argument("--trajectory-every", type=int, default=None,
                     help="save every n-th episode's trajectory (default 100 for actor modes, as "
                          "run_actor_only_training.py; 0 = none)")
@@ -200,6 +213,8 @@ def main():
     n_list = [int(x) for x in a.n.split(",")]
     L = Learner(m, l1_sff(m), a.variant, n_envs=a.envs, n_agents=max(n_list), mode=a.mode, params=params,
                 seed=a.seed, max_steps=a.max_steps)
+    if a.critic:
+        load_critic(L, a.critic)
     es, ee = (float(x) for x in a.eps.split(","))
     every = a.trajectory_every if a.trajectory_every is not None else (100 if L.actor else 0)
     run_curriculum(L, (0, a.size // 2), [int(x) for x in a.radius.split(",")], n_list, a.episodes, es, ee, a.out,

@@ -238,7 +238,8 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
  *   step_local -> exchange V (and H unless unified actor_only) -> step_apply(V)
  *   -> [unified actor_only: exchange H] -> step_apply(H) (actor variants) -> step_end.
  * ffm_learner_step == the same phases with no exchange.  A delta record is a
- * key (u64) and its pending fixed-point increments (width i64: 1 for V, 5 for H)
+ * key (u64) and its pending accumulators (i64 words: V 2 = the fixed-point sum of td
+ * and the visit count, H 5 = the fixed-point alpha_h * td sums per action)
  * for every entry inserted or incremented during this step; a rank merges the
  * other ranks' records (inserting missing keys) before applying, so every rank
  * ends the step with the tables a single device holding all envs would have.

@@ -26,11 +26,13 @@ static const int NB[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};   /* U, D, L, R:
  * ====================================================================== */
 struct ffo_tab {
     int32_t width;
+    int32_t accw;          /* accumulator words per slot: V 2 (sum of td, visits), H = width */
+    double alpha;          /* V: alpha_v of the visit-averaged batched update */
     int64_t cap, n;
     int64_t mark;          /* n at the start of the current batched step */
     uint64_t* keys;
     double* vals;
-    int64_t* acc;          /* batched fixed-point increments */
+    int64_t* acc;          /* batched fixed-point accumulators */
     int64_t* order;        /* slot of the i-th inserted key */
 };
 
@@ -44,10 +46,11 @@ static uint64_t mix64(uint64_t z) {
 ffo_tab* ffo_tab_new(int32_t width, int32_t log2_cap) {
     ffo_tab* t = (ffo_tab*)calloc(1, sizeof(ffo_tab));
     t->width = width;
+    t->accw = width == 1 ? 2 : width;
     t->cap = (int64_t)1 << log2_cap;
     t->keys = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)t->cap);
     t->vals = (double*)calloc((size_t)(t->cap * width), sizeof(double));
-    t->acc = (int64_t*)calloc((size_t)(t->cap * width), sizeof(int64_t));
+    t->acc = (int64_t*)calloc((size_t)(t->cap * t->accw), sizeof(int64_t));
     t->order = (int64_t*)malloc(sizeof(int64_t) * (size_t)t->cap);
     for (int64_t i = 0; i < t->cap; i++) t->keys[i] = EMPTY_KEY;
     return t;
@@ -110,19 +113,36 @@ static int64_t tab_get_sync(ffo_tab* t, uint64_t key, const double* init, int pa
 void ffo_tab_mark(ffo_tab* t) { t->mark = t->n; }
 
 /* Entries touched since the mark: inserted after it, or with pending increments.
- * keys [n], acc [n][width]; returns n. */
+ * keys [n], acc [n][accw]; returns n. */
 int64_t ffo_tab_delta_export(const ffo_tab* t, uint64_t* keys, int64_t* acc) {
     int64_t m = 0;
+    const int w = t->accw;
     for (int64_t i = 0; i < t->n; i++) {
         const int64_t s = t->order[i];
         int touched = i >= t->mark;
-        for (int k = 0; k < t->width; k++) touched |= t->acc[s * t->width + k] != 0;
+        for (int k = 0; k < w; k++) touched |= t->acc[s * w + k] != 0;
         if (!touched) continue;
         keys[m] = t->keys[s];
-        memcpy(acc + m * t->width, t->acc + s * t->width, sizeof(int64_t) * (size_t)t->width);
+        memcpy(acc + m * w, t->acc + s * w, sizeof(int64_t) * (size_t)w);
         m++;
     }
     return m;
+}
+
+int32_t ffo_tab_accw(const ffo_tab* t) { return t->accw; }
+void ffo_tab_set_alpha(ffo_tab* t, double alpha) { t->alpha = alpha; }
+
+/* V after k visits of one batched step with summed fixed-point td q: k sequential
+ * TD(0) updates towards the mean target, V + (1 - (1 - alpha)^k) * mean(td)
+ * (ffm_amd/csrc/learn_step.hip v_visits: the same operation sequence). */
+static double ffo_v_visits(double v, int64_t q, int64_t k, double alpha) {
+    const double mean = (double)q * (1.0 / FX_ONE) / (double)k;
+    double p = 1.0, b = 1.0 - alpha;
+    for (int64_t e = k; e; e >>= 1) {
+        if (e & 1) p = p * b;
+        b = b * b;
+    }
+    return v + (1.0 - p) * mean;
 }
 
 /* Add another rank's records: insert missing keys with `init`, add increments. */
@@ -130,7 +150,7 @@ int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, in
     for (int64_t r = 0; r < n; r++) {
         const int64_t s = tab_get(t, keys[r], init);
         if (s < 0) return -1;
-        for (int k = 0; k < t->width; k++) t->acc[s * t->width + k] += acc[r * t->width + k];
+        for (int k = 0; k < t->accw; k++) t->acc[s * t->accw + k] += acc[r * t->accw + k];
     }
     return 0;
 }
@@ -138,8 +158,17 @@ int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, in
 /* Applies the pending increments; the next delta export starts from here (the
  * device's apply kernels set their mark the same way). */
 void ffo_tab_apply(ffo_tab* t) {
-    for (int64_t s = 0; s < t->cap * t->width; s++)
-        if (t->acc[s]) { t->vals[s] = t->vals[s] + (double)t->acc[s] * (1.0 / FX_ONE); t->acc[s] = 0; }
+    if (t->width == 1) {   /* V: visit-averaged */
+        for (int64_t s = 0; s < t->cap; s++)
+            if (t->acc[2 * s + 1]) {
+                t->vals[s] = ffo_v_visits(t->vals[s], t->acc[2 * s], t->acc[2 * s + 1], t->alpha);
+                t->acc[2 * s] = 0;
+                t->acc[2 * s + 1] = 0;
+            }
+    } else {
+        for (int64_t s = 0; s < t->cap * t->width; s++)
+            if (t->acc[s]) { t->vals[s] = t->vals[s] + (double)t->acc[s] * (1.0 / FX_ONE); t->acc[s] = 0; }
+    }
     t->mark = t->n;
 }
 
@@ -761,7 +790,8 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
             if (!L->jacobi) {
                 L->V->vals[sv] = v + c->alpha_v * t;                   /* :665 */
             } else {
-                __atomic_fetch_add(&L->V->acc[sv], fx(c->alpha_v * t), __ATOMIC_RELAXED);
+                __atomic_fetch_add(&L->V->acc[2 * sv], fx(t), __ATOMIC_RELAXED);
+                __atomic_fetch_add(&L->V->acc[2 * sv + 1], (int64_t)1, __ATOMIC_RELAXED);
             }
             if (rec) { rec[i].sv = (int32_t)sv; rec[i].snv = (int32_t)sn; rec[i].r = r; }
         }
@@ -873,6 +903,7 @@ static double eps_of(const ffo_learn_cfg* c, int32_t k) {
 ffo_lbatch* ffo_lbatch_new(const ffo_learn_cfg* c, ffo_tab* V, ffo_tab* Ht, int64_t E, int32_t A_cap) {
     ffo_lbatch* b = (ffo_lbatch*)calloc(1, sizeof(ffo_lbatch));
     b->c = c; b->V = V; b->Ht = Ht; b->E = E; b->A_cap = A_cap;
+    V->alpha = c->alpha_v;   /* the visit-averaged V update of the batched step */
     b->recs = (lrec*)calloc((size_t)(E * A_cap), sizeof(lrec));
     b->nstart = (int32_t*)calloc((size_t)E, sizeof(int32_t));
     return b;

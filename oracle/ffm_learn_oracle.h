@@ -100,6 +100,8 @@ int64_t ffo_lbatch_end(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff
                        int32_t max_steps, int64_t env_base, int32_t* log);
 void ffo_tab_mark(ffo_tab* t);
 int64_t ffo_tab_delta_export(const ffo_tab* t, uint64_t* keys, int64_t* acc);
+int32_t ffo_tab_accw(const ffo_tab* t);
+void ffo_tab_set_alpha(ffo_tab* t, double alpha);
 int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, int64_t n, const double* init);
 void ffo_tab_apply(ffo_tab* t);
 

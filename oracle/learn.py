@@ -100,6 +100,7 @@ def _lib():
 class Table:
     def __init__(self, width: int, log2_cap: int = 20):
         self.width = width
+        self.accw = 2 if width == 1 else width   # accumulator words (V: sum of td, visits)
         self.h = _lib().ffo_tab_new(width, log2_cap)
 
     def __del__(self):
@@ -274,11 +275,11 @@ class Shard:
         """The engine's asynchronous export: the count goes to memory (here host memory)."""
         T = self._tab(which)
         tmp_k = np.empty(max(len(T), 1), np.uint64)
-        tmp_a = np.empty((max(len(T), 1), T.width), np.int64)
+        tmp_a = np.empty((max(len(T), 1), T.accw), np.int64)
         n = int(_lib().ffo_tab_delta_export(T.h, O._ptr(tmp_k), O._ptr(tmp_a)))
         m = min(n, int(cap))
         C.memmove(keys_ptr, tmp_k.ctypes.data, m * 8)
-        C.memmove(acc_ptr, tmp_a.ctypes.data, m * 8 * T.width)
+        C.memmove(acc_ptr, tmp_a.ctypes.data, m * 8 * T.accw)
         C.c_int64.from_address(count_ptr).value = n
         if n > cap:
             raise RuntimeError("asynchronous delta export: record buffer too small")

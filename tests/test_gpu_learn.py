@@ -552,3 +552,45 @@ def test_batched_critic_curriculum_matches_reference_logged_means(tmp_path):
     assert len(rows) == 1 + 4096 * len(res["configs"])      # 2 episodes of every one of the 2048 envs
     assert (tmp_path / "summary.txt").exists() and (tmp_path / "V_table.pkl").exists()
     L.close()
+
+
+# The reference's unified actor_only run on its block_size-1 critic
+# (output/logs/unified_actor_training/run_20260119_070834/steps_per_episode.csv of the
+# reference, 100 episodes per configuration): mean steps and standard errors.
+REF_ACTOR_MEAN_STEPS = {(9, 40): (80.30, 0.14), (11, 70): (139.87, 0.13), (15, 90): (179.75, 0.13)}
+
+
+def test_batched_actor_curriculum_on_batched_critic_matches_reference_log(tmp_path):
+    """Batched actor-learning dynamics against the reference's logged actor run.  A
+    critic is trained by the batched critic_only curriculum (its V must stay in the
+    range the rewards allow: a state visited k times in a step moves by
+    (1 - (1 - alpha)^k) * mean(td), never by k * alpha * td), then the unified
+    actor_only curriculum runs on it with 10 envs (the reference's per-configuration
+    epsilon decay over 10 episodes per env).  Agents must learn to leave: the mean
+    episode length of the crowded configurations lies within 3 % of the logged one
+    (the logged standard errors are 0.1 %; our 100-episode means carry the batched
+    semantics and a different critic)."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.engine import Learner
+    from ffm_amd.train import run_curriculum
+    m = make_room(12, 12)
+    p = {"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99, "exit_reward": 100.0,
+         "step_penalty": -1.0, "collision_penalty": -1.0, "neighborhood": "neumann", "block_size": 1}
+    C = Learner(m, l1_sff(m), "unified", n_envs=4096, n_agents=90, mode="critic_only", params=p, seed=5,
+                max_steps=300)
+    run_curriculum(C, (0, 6), [3, 5, 7, 9, 11, 13, 15], [1, 10, 20, 30, 40, 50, 60, 70, 80, 90], 1000,
+                   verbose=False)
+    vk, vv = C.export_table("V")
+    C.close()
+    assert np.isfinite(vv).all() and vv.min() > -150.0 and vv.max() < 150.0, (vv.min(), vv.max())
+    A = Learner(m, l1_sff(m), "unified", n_envs=10, n_agents=90, mode="actor_only", params=p, seed=6,
+                max_steps=300)
+    A.import_table("V", vk, vv)
+    res = run_curriculum(A, (0, 6), [9, 11, 15], [40, 70, 90], 100, 0.2, 0.01, verbose=False)
+    got = {(c["radius"], c["N"]): c for c in res["configs"]}
+    for key, (ref, _se) in REF_ACTOR_MEAN_STEPS.items():
+        c = got[key]
+        assert abs(c["mean_steps"] - ref) <= 0.03 * ref, (key, c["mean_steps"], ref)
+        assert c["emptied"] == c["episodes"]                # every episode ends with the room empty
+    assert A.table_size("H") > 1000
+    A.close()
