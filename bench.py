@@ -63,8 +63,8 @@ def parse():
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed regions of K steps each, back to back; value = their median (BASELINE.md 3)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--multi-step", type=int, default=10,
-                    help="configs 2/3: also time step(K) with this many steps fused per launch "
+    ap.add_argument("--multi-step", type=int, default=50,
+                    help="config 2: also time step(K) with this many steps fused per launch "
                          "(ffm_engine_set_fused_steps; a secondary field, 0 = skip)")
     ap.add_argument("--log2-table", type=int, default=0, help="learner V/H hash capacity (0 = engine default)")
     ap.add_argument("--sync-period", type=int, default=1,
@@ -146,7 +146,7 @@ def main():
     # Secondary line: the same steps with K fused per launch (state on chip between
     # the K steps of an env pair; bit-identical results, tests/test_gpu_parity.py).
     multi = None
-    if args.multi_step > 1:
+    if args.multi_step > 1 and args.config == 2:
         eng.set_fused_steps(args.multi_step)
         eng.step(args.multi_step, stream)
         torch.cuda.synchronize()

@@ -157,7 +157,8 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     // a float32 array (model/ffm_unified.py:361-364, 442-445).
     a.kS32 = (float)(-d.k_S); a.kD32 = (float)d.k_D; a.kS64 = -d.k_S; a.nkA = -l->L.k_A;
     a.c0 = (float)((1.0 - d.decay) * (1.0 - d.diffuse));
-    a.c1 = (float)(d.decay * (1.0 - d.diffuse) / 4.0);
+    a.c1 = (float)(d.decay * (1.0 - d.diffuse) / (double)d.neighborhood);
+    a.nb = d.neighborhood;
     a.alpha_v = l->L.alpha_v; a.alpha_h = l->L.alpha_h; a.gamma = l->L.gamma;
     a.exit_reward = l->L.exit_reward; a.step_penalty = l->L.step_penalty;
     a.collision_penalty = l->L.collision_penalty; a.epsilon = l->L.epsilon; a.v_default = l->L.v_default;
@@ -219,7 +220,10 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
     if ((long long)d.H * d.W == 65536 && (d.map[65535] == 0 || d.map[65535] == 3))
         return fail(FFM_E_UNSUPPORTED, "the last cell of a 65536-cell map must be blocked");
-    if (d.neighborhood != 4) return fail(FFM_E_UNSUPPORTED, "learning variants are built for neighborhood 'neumann'");
+    if (d.neighborhood != 4 &&
+        !(d.neighborhood == 8 && d.variant == FFM_VARIANT_AC && d.rng_mode == FFM_RNG_MT))
+        return fail(FFM_E_UNSUPPORTED, "neighborhood 'moore' is built for ffm_ac_core in MT (reference-exact) mode "
+                                       "only; the other learning variants and the batched step use 'neumann'");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
     // batched: LDS grid codes and placement sorts hold <= 16384 agents; the exact (MT) step

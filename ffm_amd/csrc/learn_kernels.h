@@ -62,6 +62,7 @@ struct LearnArgs {
     float kS32, kD32;           // f32(-k_S), f32(k_D)
     double kS64, nkA;           // -k_S, -k_A
     float c0, c1;               // DFF coefficients (model/ffm_unified.py:779-798)
+    int nb;                     // neighbours: 4 (neumann) or 8 (moore: ffm_ac_core, MT mode only)
     double alpha_v, alpha_h, gamma, exit_reward, step_penalty, collision_penalty, epsilon, v_default;
     uint16_t* pos;              // [E][A]
     int* cnt;                   // [E]

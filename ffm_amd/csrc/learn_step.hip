@@ -210,6 +210,28 @@ __device__ __forceinline__ unsigned long long pack_key(unsigned long long cells,
 
 __constant__ int kNBx[4] = {-1, 1, 0, 0};   // U, D, L, R (model/ffm_unified.py:174-175)
 __constant__ int kNBy[4] = {0, 0, -1, 1};
+// Moore order of ffm_ac_core.get_neighbors (model/ffm_ac_core.py:51-60): row-major.
+__constant__ int kMBx[8] = {-1, -1, -1, 0, 0, 1, 1, 1};
+__constant__ int kMBy[8] = {-1, 0, 1, -1, 1, -1, 0, 1};
+
+// NumPy's pairwise add.reduce (numpy/_core/src/umath/loops_utils.h.src): n < 8 a
+// left fold from -0, else eight running partial sums, combined pairwise, then the tail.
+template <class T>
+__device__ __forceinline__ T np_sum_n(const T* a, int n) {
+    if (n < 8) {
+        T res = T(-0.0);
+        for (int i = 0; i < n; i++) res += a[i];
+        return res;
+    }
+    T r[8];
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += a[i];
+    return res;
+}
 
 // model/ffm_unified.py:188-269.  The rank of direction d from the neighbour n1,
 // the two cells beside n1 (diagonals of the agent) and the cell two ahead n2:
@@ -305,9 +327,9 @@ struct DrawPh {                  // one keyed Philox stream per decision
 };
 
 __device__ __forceinline__ int choice_cdf(const double* p, int n, double u) {
-    double cdf[5], acc = 0.0;
+    double cdf[9], acc = 0.0;   // n <= 9: eight Moore neighbours + stay (ffm_ac_core)
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < 9; k++) {
         if (k < n) { acc += p[k]; cdf[k] = acc; }
     }
     const double last = cdf[n - 1];
@@ -456,10 +478,9 @@ __device__ int critic_choose(const LearnArgs& a, const int* coord, const int* va
 template <class OCC, class R>
 __device__ int ac_decide(const LearnArgs& a, int x, int y, const OCC& occ, const float* dff, int& wexit, R& rng) {
     const int W = a.W;
-    int cand[5], nc = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int cell = (x + kNBx[k]) * W + (y + kNBy[k]);
+    int cand[9], nc = 0;
+    for (int k = 0; k < a.nb; k++) {
+        const int cell = a.nb == 8 ? (x + kMBx[k]) * W + (y + kMBy[k]) : (x + kNBx[k]) * W + (y + kNBy[k]);
         const int m = a.map[cell];
         if (!(m == 0 || m == 3)) continue;
         if (occ(cell)) continue;
@@ -469,9 +490,9 @@ __device__ int ac_decide(const LearnArgs& a, int x, int y, const OCC& occ, const
     cand[nc++] = x * W + y;
     for (int k = 0; k < nc; k++)
         if (a.map[cand[k]] == 3) { wexit = 1; return cand[k]; }
-    double p[5];
+    double p[9];
     if (a.sff32) {
-        float s[5], e[5];
+        float s[9], e[9];
         for (int k = 0; k < nc; k++) {
             const float u = a.kS32 * a.sff32[cand[k]];
             const float v = a.kD32 * dff[cand[k]];
@@ -480,11 +501,11 @@ __device__ int ac_decide(const LearnArgs& a, int x, int y, const OCC& occ, const
         float mx = s[0];
         for (int k = 1; k < nc; k++) mx = s[k] > mx ? s[k] : mx;
         for (int k = 0; k < nc; k++) e[k] = np_expf(s[k] - mx);
-        const float sum = sum_seqf(e, nc);
+        const float sum = np_sum_n(e, nc);
         if (!(__builtin_isfinite(sum) && sum != 0.0f)) return -1;
         for (int k = 0; k < nc; k++) p[k] = (double)(e[k] / sum);
     } else {
-        double s[5], e[5];
+        double s[9], e[9];
         for (int k = 0; k < nc; k++) {
             const float v = a.kD32 * dff[cand[k]];
             s[k] = a.kS64 * a.sff64[cand[k]] + (double)v;
@@ -492,7 +513,7 @@ __device__ int ac_decide(const LearnArgs& a, int x, int y, const OCC& occ, const
         double mx = s[0];
         for (int k = 1; k < nc; k++) mx = s[k] > mx ? s[k] : mx;
         for (int k = 0; k < nc; k++) e[k] = det_exp(s[k] - mx);
-        const double sum = sum_seq(e, nc);
+        const double sum = np_sum_n(e, nc);
         if (!(__builtin_isfinite(sum) && sum != 0.0)) return -1;
         for (int k = 0; k < nc; k++) p[k] = e[k] / sum;
     }
@@ -521,8 +542,8 @@ __device__ void update_dff_seq(const LearnArgs& a, float* dff, float* B) {
     for (int x = 0; x < H; x++)
         for (int y = 0; y < W; y++) {
             float acc = B[x * W + y];
-            for (int k = 0; k < 4; k++) {
-                const int nx = x + kNBx[k], ny = y + kNBy[k];
+            for (int k = 0; k < a.nb; k++) {   // model/ffm_ac_core.py:298-317: every neighbour in order
+                const int nx = x + (a.nb == 8 ? kMBx[k] : kNBx[k]), ny = y + (a.nb == 8 ? kMBy[k] : kNBy[k]);
                 const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? B[nx * W + ny] : 0.0f;
                 const float t = a.c1 * v;
                 acc = acc + t;

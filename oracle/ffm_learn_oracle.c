@@ -20,6 +20,11 @@
 #define MAXR 4                         /* decisions per agent (ffm_actor_only inner loop) */
 
 static const int NB[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};   /* U, D, L, R: model/ffm_unified.py:174-175 */
+/* Moore order of ffm_ac_core.get_neighbors (model/ffm_ac_core.py:51-60) */
+static const int MB[8][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 1}, {1, -1}, {1, 0}, {1, 1}};
+static int cfg_nb(const ffo_learn_cfg* c) { return c->nb == 8 ? 8 : 4; }
+static int nbx(int nb, int k) { return nb == 8 ? MB[k][0] : NB[k][0]; }
+static int nby(int nb, int k) { return nb == 8 ? MB[k][1] : NB[k][1]; }
 
 /* ======================================================================
  * Hash table with insertion order (a Python dict of packed keys).
@@ -564,10 +569,11 @@ static int trained_choose(lctx* L, int64_t hslot, const int32_t* coord, const in
 static int32_t ac_decide(lctx* L, int x, int y, const int32_t* occ, const float* dff, int* will_exit) {
     const ffo_learn_cfg* c = L->c;
     const int W = c->W;
-    int32_t cand[5];
+    const int nb = cfg_nb(c);
+    int32_t cand[9];
     int nc = 0;
-    for (int k = 0; k < 4; k++) {
-        const int32_t cell = (x + NB[k][0]) * W + (y + NB[k][1]);
+    for (int k = 0; k < nb; k++) {
+        const int32_t cell = (x + nbx(nb, k)) * W + (y + nby(nb, k));
         const uint8_t m = c->map[cell];
         if (!(m == 0 || m == 3)) continue;
         if (occ[cell] >= 0) continue;
@@ -577,10 +583,10 @@ static int32_t ac_decide(lctx* L, int x, int y, const int32_t* occ, const float*
     cand[nc++] = x * W + y;
     for (int k = 0; k < nc; k++)
         if (c->map[cand[k]] == 3) { *will_exit = 1; return cand[k]; }   /* :166-172 */
-    double p[5];
+    double p[9];
     if (c->sff32) {
         const float kS = (float)(-c->k_S), kD = (float)c->k_D;
-        float s[5], e[5];
+        float s[9], e[9];
         for (int k = 0; k < nc; k++) {
             const float a = kS * c->sff32[cand[k]];
             const float b = kD * dff[cand[k]];
@@ -595,7 +601,7 @@ static int32_t ac_decide(lctx* L, int x, int y, const int32_t* occ, const float*
     } else {
         const double kS = -c->k_S;
         const float kD = (float)c->k_D;
-        double s[5], e[5];
+        double s[9], e[9];
         for (int k = 0; k < nc; k++) {
             const float b = kD * dff[cand[k]];
             s[k] = kS * c->sff64[cand[k]] + (double)b;
@@ -614,13 +620,14 @@ static void update_dff4(const ffo_learn_cfg* c, float* dff, float* B) {
     /* model/ffm_unified.py:779-798 (same as ffm_core.update_dff, neumann) */
     const int H = c->H, W = c->W, HW = H * W;
     const float c0 = (float)((1.0 - c->decay) * (1.0 - c->diffuse));
-    const float c1 = (float)(c->decay * (1.0 - c->diffuse) / 4.0);
+    const int nb = cfg_nb(c);
+    const float c1 = (float)(c->decay * (1.0 - c->diffuse) / (double)nb);
     for (int i = 0; i < HW; i++) B[i] = c0 * dff[i];
     for (int x = 0; x < H; x++)
         for (int y = 0; y < W; y++) {
             float a = B[x * W + y];
-            for (int k = 0; k < 4; k++) {
-                const int nx = x + NB[k][0], ny = y + NB[k][1];
+            for (int k = 0; k < nb; k++) {
+                const int nx = x + nbx(nb, k), ny = y + nby(nb, k);
                 const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? B[nx * W + ny] : 0.0f;
                 const float t = c1 * v;
                 a = a + t;

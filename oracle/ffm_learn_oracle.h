@@ -52,6 +52,7 @@ typedef struct {
      * (run_actor_only_training.py:190-196: offset 0, span total-1;
      * run_unified_actor_training.py:253-259: offset 1, span episodes per config) */
     double eps_start, eps_end, eps_offset, eps_span;
+    int32_t nb;               /* neighbours: 4 (neumann; 0 means 4) or 8 (moore, ffm_ac_core) */
 } ffo_learn_cfg;
 
 typedef struct ffo_tab ffo_tab;

@@ -46,6 +46,7 @@ class LearnCfg(C.Structure):
         ("exit_reward", C.c_double), ("step_penalty", C.c_double), ("collision_penalty", C.c_double),
         ("epsilon", C.c_double), ("v_default", C.c_double), ("block_size", C.c_int32),
         ("eps_start", C.c_double), ("eps_end", C.c_double), ("eps_offset", C.c_double), ("eps_span", C.c_double),
+        ("nb", C.c_int32),
     ]
 
 
@@ -149,6 +150,7 @@ class Learn:
             float(p["decay"]), float(p.get("alpha_v", 0.0)), float(p.get("alpha_h", 0.0)), float(p.get("gamma", 0.0)),
             float(p.get("exit_reward", 0.0)), float(p.get("step_penalty", 0.0)), float(p.get("collision_penalty", 0.0)),
             float(p.get("epsilon", 0.0)), 0.0, int(p.get("block_size", 5)))
+        self.cfg.nb = 8 if p.get("neighborhood", "neumann") == "moore" else 4
 
     def set_epsilon(self, e: float):
         self.cfg.epsilon = float(min(max(e, 0.0), 1.0))

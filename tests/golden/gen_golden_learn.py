@@ -207,6 +207,8 @@ def main():
     run_case("ac_12x12_N8", "ac", AC, m12, s12, {}, 8, [0, 1, 2], 3, 400)
     run_case("ac_12x12_N32_reload", "ac", AC, m12, s12, {"k_S": 3, "block_size": 5}, 32, [3, 4], 3, 400,
              reload_v=True)
+    # ffm_ac_core with the Moore neighbourhood (model/ffm_ac_core.py:47-60; update_dff's 8 terms)
+    run_case("ac_moore_12x12_N16", "ac", AC, m12, s12, {"k_S": 3, "neighborhood": "moore"}, 16, [7, 8], 3, 400)
     # ffm_unified, run_unified_*_training.py parameters (block 1) and class defaults (block 5)
     uni_p = {"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99,
              "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0,

@@ -566,7 +566,8 @@ def test_batched_actor_curriculum_on_batched_critic_matches_reference_log(tmp_pa
     range the rewards allow: a state visited k times in a step moves by
     (1 - (1 - alpha)^k) * mean(td), never by k * alpha * td), then the unified
     actor_only curriculum runs on it with 10 envs (the reference's per-configuration
-    epsilon decay over 10 episodes per env).  Agents must learn to leave: the mean
+    epsilon decay over 10 episodes per env), the whole curriculum as the logged run
+    did (H carries over from one configuration to the next).  Agents must learn to leave: the mean
     episode length of the crowded configurations lies within 3 % of the logged one
     (the logged standard errors are 0.1 %; our 100-episode means carry the batched
     semantics and a different critic)."""
@@ -586,7 +587,8 @@ def test_batched_actor_curriculum_on_batched_critic_matches_reference_log(tmp_pa
     A = Learner(m, l1_sff(m), "unified", n_envs=10, n_agents=90, mode="actor_only", params=p, seed=6,
                 max_steps=300)
     A.import_table("V", vk, vv)
-    res = run_curriculum(A, (0, 6), [9, 11, 15], [40, 70, 90], 100, 0.2, 0.01, verbose=False)
+    res = run_curriculum(A, (0, 6), [3, 5, 7, 9, 11, 13, 15], [1, 10, 20, 30, 40, 50, 60, 70, 80, 90], 100,
+                         0.2, 0.01, verbose=False)   # H learns along the whole curriculum, as in the log
     got = {(c["radius"], c["N"]): c for c in res["configs"]}
     for key, (ref, _se) in REF_ACTOR_MEAN_STEPS.items():
         c = got[key]

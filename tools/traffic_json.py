@@ -19,7 +19,7 @@ def arg(name, default):
 
 
 cfg = int(arg("--config", 2))
-KERNELS = ("learn_batch_kernel",) if cfg in (4, 5) else ("core_wave_kernel", "core_block_kernel")
+KERNELS = ("learn_batch_kernel",) if cfg in (4, 5) else ("core_group_kernel", "core_lane_kernel", "core_wave_kernel", "core_block_kernel")
 
 
 def per_dispatch(path, counter):
