@@ -934,20 +934,51 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     }
 
     // ---- update_dff (model/ffm_core.py:106-117) --------------------------------------------------
-    for (int i = tid; i < nP; i += BS) tile[i] = a.c0 * tile[i];                       // :109 (halo stays 0)
-    __syncthreads();
-    Idx3 ix(tid, BS, H, W);
-    for (int c = tid; c < K * HW; c += BS, ix.advance()) {
-        const int k = ix.k, x = ix.r, y = ix.c;
-        const float* p = tile + k * PHW + (x + 1) * PW + y + 1;
-        float acc = *p;
+    // B = c0 * D (:109) is formed on the fly from each operand, rounded exactly as the
+    // reference's separate pass, so the tile is read once and needs no extra barrier.
+    __syncthreads();   // every deposit of the resolve is in the tile
+    const float c0 = a.c0, c1 = a.c1;
+    if ((W & 3) == 0) {
+        // four cells of a row per thread: 16-B DFF stores, shared row operands
+        const int W4 = W >> 2;
+        Idx3 ix(tid, BS, H, W4);
+        for (int q = tid; q < K * H * W4; q += BS, ix.advance()) {
+            const int k = ix.k, x = ix.r, y = 4 * ix.c;
+            const float* p = tile + k * PHW + (x + 1) * PW + y + 1;
+            float b[3][6];   // rows dx = -1..1, columns y-1..y+4
 #pragma unroll
-        for (int q = 0; q < NB; q++) {
-            const float t = a.c1 * p[nb_dx<NB>(q) * PW + nb_dy<NB>(q)];               // :113
-            acc = acc + t;
+            for (int dx = -1; dx <= 1; dx++)
+#pragma unroll
+                for (int j = -1; j <= 4; j++) b[dx + 1][j + 1] = (NB == 4 && dx != 0 && (j < 0 || j > 3)) ? 0.0f
+                                                                  : c0 * p[dx * PW + j];
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float acc = b[1][j + 1];
+#pragma unroll
+                for (int s2 = 0; s2 < NB; s2++) {
+                    const float t = c1 * b[1 + nb_dx<NB>(s2)][j + 1 + nb_dy<NB>(s2)];   // :113
+                    acc = acc + t;
+                }
+                o[j] = (acc < 1e-4f || sreset[k]) ? 0.0f : acc;                      // :116-117
+            }
+            *reinterpret_cast<float4*>(a.dff + (e0 * H + (long long)k * H + x) * W + y) =
+                make_float4(o[0], o[1], o[2], o[3]);
         }
-        // :116-117; an env reset this step starts its next episode with a zero DFF
-        a.dff[e0 * HW + c] = (acc < 1e-4f || sreset[k]) ? 0.0f : acc;
+    } else {
+        Idx3 ix(tid, BS, H, W);
+        for (int c = tid; c < K * HW; c += BS, ix.advance()) {
+            const int k = ix.k, x = ix.r, y = ix.c;
+            const float* p = tile + k * PHW + (x + 1) * PW + y + 1;
+            float acc = c0 * *p;
+#pragma unroll
+            for (int q = 0; q < NB; q++) {
+                const float t = c1 * (c0 * p[nb_dx<NB>(q) * PW + nb_dy<NB>(q)]);   // :113
+                acc = acc + t;
+            }
+            // :116-117; an env reset this step starts its next episode with a zero DFF
+            a.dff[e0 * HW + c] = (acc < 1e-4f || sreset[k]) ? 0.0f : acc;
+        }
     }
 }
 
