@@ -730,7 +730,23 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     const AgentIdx ag0(tid, BS, A);   // this thread's first (env, agent) slot
 
     // ---- load -------------------------------------------------------------------
-    {
+    if ((W & 3) == 0) {
+        // interior cells as 16-B loads of four cells of a row; the halo ring is zeroed
+        // with the grid pass (disjoint cells, one barrier below)
+        const int W4 = W >> 2;
+        Idx3 iq(tid, BS, H, W4);
+        for (int q = tid; q < K * H * W4; q += BS, iq.advance()) {
+            const float4 v = *reinterpret_cast<const float4*>(a.dff + ((e0 + iq.k) * H + iq.r) * W + 4 * iq.c);
+            float* t = tile + iq.k * PHW + (iq.r + 1) * PW + 4 * iq.c + 1;
+            t[0] = v.x; t[1] = v.y; t[2] = v.z; t[3] = v.w;
+        }
+        Idx3 ix(tid, BS, H + 2, PW);
+        for (int i = tid; i < nP; i += BS, ix.advance()) {
+            const bool halo = ix.r == 0 || ix.r == H + 1 || ix.c == 0 || ix.c == W + 1;
+            if (halo) tile[i] = 0.0f;
+            grid[i] = a.pmap[ix.r * PW + ix.c];
+        }
+    } else {
         Idx3 ix(tid, BS, H + 2, PW);
         for (int i = tid; i < nP; i += BS, ix.advance()) {
             const int x = ix.r - 1, y = ix.c - 1, pc = ix.r * PW + ix.c;
