@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 
 // Diagnostic builds only (tools/learn_ablate.sh): FFM_LABLATE bits drop parts of the
 // batched step to time them.  1: table increments, 2: learning phase,
-// 4: policy (agents stay; no H lookup), 8: DFF stencil.
+// 4: policy (agents stay; no H lookup), 8: DFF stencil, 16: V visit counts.
 #ifndef FFM_SMALL_EPB
 #define FFM_SMALL_EPB 8
 #endif
@@ -1420,7 +1420,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
         if (!(FFM_LABLATE & 1)) {
             acc_add(a.V.acc + 2 * (size_t)sv, fx(td));
-            acc_add(a.V.acc + 2 * (size_t)sv + 1, 1);
+            if (!(FFM_LABLATE & 16)) acc_add(a.V.acc + 2 * (size_t)sv + 1, 1);
         }
         if (!actor) continue;
         if (act[j] < 0) continue;
