@@ -413,6 +413,8 @@ void core_group_kernel(CoreStepArgs a) {
             m &= m - 1u;
             const long long e = (long long)(g_first + (bit >> 3) * wstride) * G + (bit & 7);
             wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + e * A, lane);
+            if (FFM_GROUP_ABLATE & 1)   // diagnostic: the same placement again (identical result)
+                wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + e * A, lane);
         }
     }
 

@@ -24,16 +24,29 @@ __device__ inline void wave_reset_env(const CoreStepArgs& a, uint32_t genv, unsi
     const int PW = a.W + 2;
     const int F = a.F, N = a.N;
     if (F <= 128) {
-        for (int j = lane; j < F; j += 64)
-            keys[j] = ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j) << 32) | (unsigned)j;
+        // lane holds keys j0 = lane and j1 = lane + 64 and ranks both in one pass over
+        // 16-B broadcast reads of the key list (two keys per read; keys is 16-B aligned)
+        const int j0 = lane, j1 = lane + 64;
+        const unsigned long long k0 =
+            j0 < F ? ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j0) << 32) | (unsigned)j0
+                   : ~0ull;
+        const unsigned long long k1 =
+            j1 < F ? ((unsigned long long)reset_key(a.key0, a.key1, a.t, genv, (uint32_t)j1) << 32) | (unsigned)j1
+                   : ~0ull;
+        if (j0 < F) keys[j0] = k0;
+        if (j1 < F) keys[j1] = k1;
+        if (lane == 0 && (F & 1)) keys[F] = ~0ull;   // pad to pairs: ~0 is never below a key
         wave_sync();
-        for (int j = lane; j < F; j += 64) {
-            const unsigned long long kj = keys[j];
-            int r = 0;
-#pragma unroll 4
-            for (int q = 0; q < F; q++) r += keys[q] < kj ? 1 : 0;
-            if (r < N) gpos[r] = (uint16_t)unpad(fl[j], PW);
+        int r0 = 0, r1 = 0;
+        const ulonglong2* kv = reinterpret_cast<const ulonglong2*>(keys);
+#pragma unroll 8
+        for (int q = 0; q < (F + 1) / 2; q++) {
+            const ulonglong2 p = kv[q];
+            r0 += (p.x < k0 ? 1 : 0) + (p.y < k0 ? 1 : 0);
+            r1 += (p.x < k1 ? 1 : 0) + (p.y < k1 ? 1 : 0);
         }
+        if (j0 < F && r0 < N) gpos[r0] = (uint16_t)unpad(fl[j0], PW);
+        if (j1 < F && r1 < N) gpos[r1] = (uint16_t)unpad(fl[j1], PW);
         wave_sync();
         return;
     }
