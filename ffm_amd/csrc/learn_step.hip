@@ -1863,7 +1863,7 @@ __global__ __launch_bounds__(256) void learn_dense_adopt_kernel(LearnTable T, co
 constexpr int kResetSmallF = 256;
 
 __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int all) {
-    __shared__ unsigned long long keys[kResetSmallF];
+    __shared__ __attribute__((aligned(16))) unsigned long long keys[kResetSmallF + 2];
     const int lane = threadIdx.x;
     const long long e0 = (long long)blockIdx.x * 64;
     const long long me = e0 + lane;
@@ -1880,11 +1880,26 @@ __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int 
             keys[j] = ((unsigned long long)k << 32) | (unsigned)j;
         }
         __syncthreads();
-        for (int j = lane; j < F; j += 64) {
-            const unsigned long long kj = keys[j];
-            int rank = 0;
-            for (int i = 0; i < F; i++) rank += keys[i] < kj ? 1 : 0;
-            if (rank < N) a.pos[e * a.A + rank] = a.free_cells[j];
+        // each lane ranks its (up to four) keys in one pass over 16-B broadcast reads
+        if (lane == 0 && (F & 1)) keys[F] = ~0ull;   // pad to pairs: ~0 is never below a key
+        __syncthreads();
+        unsigned long long kj[kResetSmallF / 64];
+        int rank[kResetSmallF / 64];
+#pragma unroll
+        for (int q = 0; q < kResetSmallF / 64; q++) {
+            kj[q] = lane + 64 * q < F ? keys[lane + 64 * q] : ~0ull;
+            rank[q] = 0;
+        }
+        const ulonglong2* kv = reinterpret_cast<const ulonglong2*>(keys);
+        for (int i = 0; i < (F + 1) / 2; i++) {
+            const ulonglong2 p = kv[i];
+#pragma unroll
+            for (int q = 0; q < kResetSmallF / 64; q++) rank[q] += (p.x < kj[q] ? 1 : 0) + (p.y < kj[q] ? 1 : 0);
+        }
+#pragma unroll
+        for (int q = 0; q < kResetSmallF / 64; q++) {
+            const int j = lane + 64 * q;
+            if (j < F && rank[q] < N) a.pos[e * a.A + rank[q]] = a.free_cells[j];
         }
         float* d = a.dff_in + e * (long long)HW;
         for (int c = lane; c < HW; c += 64) d[c] = 0.0f;
