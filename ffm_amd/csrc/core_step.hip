@@ -551,7 +551,7 @@ __host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, 
     c.nxt = o;  o += align16((size_t)K * A * ix);
     c.misc = big ? 0 : o;
     o += big ? 0 : misc;
-    c.u = o;    o += mt ? align16((size_t)K * A * 8) : 0;
+    c.u = o;    o += align16((size_t)K * A * 8);   // MT: the pending draws; Philox: the friction words
     c.flag = o; o += mt ? align16((size_t)K * A * 2) : 0;
     c.keys = o; o += reset ? align16((size_t)block_keys_cap(A, F) * 8) : 0;
     c.total = o;
@@ -794,9 +794,13 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32,
                                                      a.kS64, DrawPending{}), pp, PW);
         } else {
-            const DrawPhilox d{a.key0, a.key1, a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i};
+            // the agent's draw block; its words z, w are the friction draw if it owns a
+            // contested target (the resolve reads them instead of recomputing the block)
+            const uint4 pb = philox(make_uint4(a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i, kPurDecide << 28),
+                                    a.key0, a.key1);
+            reinterpret_cast<uint2*>(gbase + cv.u)[it] = make_uint2(pb.z, pb.w);
             r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32,
-                                                     a.kS64, d), pp, PW);
+                                                     a.kS64, DrawFixed{u53(pb.x, pb.y)}), pp, PW);
         }
         sreq[it] = r;
     }
@@ -878,8 +882,8 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             if (f & 0x100) ws = kth_slot<NB>(who, is, f & 0xFF);
         } else {
             const uint32_t genv = (uint32_t)(a.env_base + e0 + k);
-            const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)i, kPurDecide << 28), a.key0, a.key1);
-            const int kk = philox_friction(pb.z, pb.w, (uint32_t)m, a.key0, a.key1, a.t, genv, (uint32_t)i);
+            const uint2 f = reinterpret_cast<const uint2*>(gbase + cv.u)[it];
+            const int kk = philox_friction(f.x, f.y, (uint32_t)m, a.key0, a.key1, a.t, genv, (uint32_t)i);
             if (kk >= 0) ws = kth_slot<NB>(who, is, kk);                                // :95-96
         }
         if (ws >= 0) {
