@@ -52,8 +52,13 @@ __host__ __device__ inline size_t multi_shared_bytes(int PHW, int F) {
 
 }  // namespace
 
+#ifndef FFM_MULTI_WAVES
+#define FFM_MULTI_WAVES 1   // minimum waves per SIMD asked of the register allocator
+#endif
+
 template <int NB, int HT, int WT>
-__global__ __launch_bounds__(256) void core_multi_kernel(CoreStepArgs a, int nsteps) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FFM_MULTI_WAVES, 8)))
+void core_multi_kernel(CoreStepArgs a, int nsteps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = HT ? HT : a.H, W = WT ? WT : a.W;
     const int HW = H * W, PW = W + 2, PHW = (H + 2) * PW;
