@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -133,7 +134,16 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     hipError_t e;
     T.t.stride = width == 1 ? 2 : 8;        // 16 B / 64 B records (key + values [+ pad])
     if ((e = hipMalloc((void**)&T.t.rec, T.cap * T.t.stride * 8)) != hipSuccess) return e;
-    if ((e = hipMalloc((void**)&T.t.acc, T.cap * T.accw * 8)) != hipSuccess) return e;
+    // hashed tables: copies of the accumulators (LearnTable::reps); FFM_ACC_REPS overrides
+    uint32_t reps = dense_by ? 1u : 8u;
+    if (!dense_by)
+        if (const char* ev = getenv("FFM_ACC_REPS")) {
+            const long r = strtol(ev, nullptr, 10);
+            if (r >= 1 && r <= 64 && (r & (r - 1)) == 0) reps = (uint32_t)r;
+        }
+    T.t.reps = reps;
+    T.t.rep_stride = (unsigned long long)(T.cap * T.accw);
+    if ((e = hipMalloc((void**)&T.t.acc, T.cap * T.accw * 8 * reps)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.order, T.cap * 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.n, 4)) != hipSuccess) return e;
     if ((e = hipMalloc((void**)&T.t.mark, 4)) != hipSuccess) return e;
@@ -195,7 +205,7 @@ static hipError_t clear_table(ffm_learner* l, DevTable& T, double dflt, hipStrea
     hipError_t e;
     (void)l;
     if (T.t.present && (e = hipMemsetAsync(T.t.present, 0, T.cap / 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.accw * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(T.t.acc, 0, T.cap * T.accw * 8 * T.t.reps, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.n, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(T.t.mark, 0, 4, s)) != hipSuccess) return e;
     return ffm::launch_learn_clear(T.t, T.width, T.width == 1 ? dflt : 0.0, s);

@@ -33,6 +33,14 @@ struct LearnTable {
     // towards one target.
     long long* acc;
     uint32_t accw;
+    // Hashed tables: `reps` (a power of two) copies of the accumulator array,
+    // `rep_stride` words apart; workgroup b adds into copy b % reps.  The 13-cell
+    // tables hold a few 10^4 keys, and the popular states take thousands of adds
+    // per step: on one copy those adds queue on a few memory-side atomic units.
+    // Integer sums do not depend on how they are split, so the apply sums the
+    // copies to the same bits.  Dense tables: reps = 1.
+    uint32_t reps;
+    unsigned long long rep_stride;
     double alpha;               // V: alpha_v (the visit-averaged update); H: unused
     uint32_t* order;            // [cap] slot of the i-th inserted key
     uint32_t* n;                // [1] keys inserted

@@ -86,6 +86,23 @@ __device__ __forceinline__ void acc_add(long long* p, long long q) {
     atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)q);
 }
 
+// Accumulator word `i` of this workgroup's copy (LearnTable::reps).
+__device__ __forceinline__ long long* acc_at(const LearnTable& T, size_t i) {
+    return T.acc + (size_t)(blockIdx.x & (T.reps - 1u)) * T.rep_stride + i;
+}
+
+// Word `i` summed over the copies, the copies cleared (apply / export passes).
+__device__ __forceinline__ long long acc_take(const LearnTable& T, size_t i, bool clear) {
+    long long q = 0;
+    for (uint32_t r = 0; r < T.reps; r++) {
+        long long* p = T.acc + (size_t)r * T.rep_stride + i;
+        const long long v = *p;
+        if (v != 0 && clear) *p = 0;
+        q += v;
+    }
+    return q;
+}
+
 // ---- hash tables ------------------------------------------------------------
 // Slot of `key`, inserting it when absent (a defaultdict read inserts,
 // model/ffm_unified.py:658).  Empty slots already hold the default value, so
@@ -1419,8 +1436,8 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
         if (sv < 0) continue;
         const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
         if (!(FFM_LABLATE & 1)) {
-            acc_add(a.V.acc + 2 * (size_t)sv, fx(td));
-            if (!(FFM_LABLATE & 16)) acc_add(a.V.acc + 2 * (size_t)sv + 1, 1);
+            acc_add(acc_at(a.V, 2 * (size_t)sv), fx(td));
+            if (!(FFM_LABLATE & 16)) acc_add(acc_at(a.V, 2 * (size_t)sv + 1), 1);
         }
         if (!actor) continue;
         if (act[j] < 0) continue;
@@ -1431,7 +1448,7 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
             rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
             a.recs[e * A + i] = rc;
         } else if (avalid[j] && !(FFM_LABLATE & 1)) {
-            acc_add(a.Ht.acc + (size_t)hsl[j] * 5 + act[j], fx(a.alpha_h * td));
+            acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + act[j]), fx(a.alpha_h * td));
         }
     }
 
@@ -1588,23 +1605,18 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
         const uint32_t slot = T.order[i];
         double* vp = tval(T, slot);
         if (WIDTH == 1) {   // V: visit-averaged
-            const long long k = T.acc[2 * (size_t)slot + 1];
-            if (k != 0) {
-                vp[0] = v_visits(vp[0], T.acc[2 * (size_t)slot], k, T.alpha);
-                T.acc[2 * (size_t)slot] = 0;
-                T.acc[2 * (size_t)slot + 1] = 0;
-            }
+            const long long k = acc_take(T, 2 * (size_t)slot + 1, true);
+            if (k != 0) vp[0] = v_visits(vp[0], acc_take(T, 2 * (size_t)slot, true), k, T.alpha);
             continue;
         }
         const size_t s = (size_t)slot * WIDTH;
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
-            const long long q = T.acc[s + k];
+            const long long q = acc_take(T, s + k, true);
             double v = vp[k];
             if (q != 0) {
                 v = v + (double)q * (1.0 / kFxOne);
                 vp[k] = v;
-                T.acc[s + k] = 0;
             }
             if (STATS) {
                 nf |= !__builtin_isfinite(v);
@@ -1676,7 +1688,7 @@ __global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
     if (rc.k < 0) return;
     const double vn = rc.snv >= 0 ? tval(a.V, rc.snv)[0] : 0.0;
     const double td = (rc.r + a.gamma * vn) - tval(a.V, rc.sv)[0];
-    acc_add(a.Ht.acc + (size_t)rc.hslot * 5 + rc.k, fx(a.alpha_h * td));
+    acc_add(acc_at(a.Ht, (size_t)rc.hslot * 5 + rc.k), fx(a.alpha_h * td));
 }
 
 __global__ __launch_bounds__(256) void learn_fill_default_kernel(LearnTable T, double v) {
@@ -1803,7 +1815,7 @@ __global__ __launch_bounds__(256) void learn_delta_export_kernel(LearnTable T, u
         bool touched = i >= mark;
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
-            q[k] = T.acc[s * WIDTH + k];
+            q[k] = acc_take(T, s * WIDTH + k, false);
             touched = touched || q[k] != 0;
         }
         if (!touched) continue;
@@ -1828,7 +1840,7 @@ __global__ __launch_bounds__(256) void learn_delta_merge_kernel(LearnTable T, co
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
             const long long q = acc[r * WIDTH + k];
-            if (q != 0) acc_add(T.acc + (size_t)s * WIDTH + k, q);
+            if (q != 0) acc_add(T.acc + (size_t)s * WIDTH + k, q);   // into copy 0
         }
     }
 }
