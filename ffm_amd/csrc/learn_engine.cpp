@@ -139,7 +139,7 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     if (!dense_by)
         if (const char* ev = getenv("FFM_ACC_REPS")) {
             const long r = strtol(ev, nullptr, 10);
-            if (r >= 1 && r <= 64 && (r & (r - 1)) == 0) reps = (uint32_t)r;
+            if (r >= 1 && r <= 8 && (r & (r - 1)) == 0) reps = (uint32_t)r;   // kMaxAccReps
         }
     T.t.reps = reps;
     T.t.rep_stride = (unsigned long long)(T.cap * T.accw);

@@ -91,16 +91,29 @@ __device__ __forceinline__ long long* acc_at(const LearnTable& T, size_t i) {
     return T.acc + (size_t)(blockIdx.x & (T.reps - 1u)) * T.rep_stride + i;
 }
 
-// Word `i` summed over the copies, the copies cleared (apply / export passes).
-__device__ __forceinline__ long long acc_take(const LearnTable& T, size_t i, bool clear) {
-    long long q = 0;
-    for (uint32_t r = 0; r < T.reps; r++) {
-        long long* p = T.acc + (size_t)r * T.rep_stride + i;
-        const long long v = *p;
-        if (v != 0 && clear) *p = 0;
-        q += v;
+// Words i .. i + NW - 1 summed over the copies (apply / export passes; `clear` zeroes
+// them).  Every copy's load is issued before any store, so the gather is one round
+// trip, not one per copy.
+constexpr uint32_t kMaxAccReps = 8;
+template <int NW>
+__device__ __forceinline__ void acc_take(const LearnTable& T, size_t i, long long (&q)[NW], bool clear) {
+    long long v[kMaxAccReps][NW];
+#pragma unroll
+    for (uint32_t r = 0; r < kMaxAccReps; r++)
+#pragma unroll
+        for (int k = 0; k < NW; k++) v[r][k] = r < T.reps ? T.acc[(size_t)r * T.rep_stride + i + k] : 0;
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        q[k] = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < kMaxAccReps; r++) q[k] += v[r][k];
     }
-    return q;
+    if (clear)
+#pragma unroll
+        for (uint32_t r = 0; r < kMaxAccReps; r++)
+#pragma unroll
+            for (int k = 0; k < NW; k++)
+                if (r < T.reps && v[r][k] != 0) T.acc[(size_t)r * T.rep_stride + i + k] = 0;
 }
 
 // ---- hash tables ------------------------------------------------------------
@@ -1605,14 +1618,17 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
         const uint32_t slot = T.order[i];
         double* vp = tval(T, slot);
         if (WIDTH == 1) {   // V: visit-averaged
-            const long long k = acc_take(T, 2 * (size_t)slot + 1, true);
-            if (k != 0) vp[0] = v_visits(vp[0], acc_take(T, 2 * (size_t)slot, true), k, T.alpha);
+            long long qk[2];
+            acc_take<2>(T, 2 * (size_t)slot, qk, true);
+            if (qk[1] != 0) vp[0] = v_visits(vp[0], qk[0], qk[1], T.alpha);
             continue;
         }
         const size_t s = (size_t)slot * WIDTH;
+        long long qa[WIDTH];
+        acc_take<WIDTH>(T, s, qa, true);
 #pragma unroll
         for (int k = 0; k < WIDTH; k++) {
-            const long long q = acc_take(T, s + k, true);
+            const long long q = qa[k];
             double v = vp[k];
             if (q != 0) {
                 v = v + (double)q * (1.0 / kFxOne);
@@ -1813,11 +1829,9 @@ __global__ __launch_bounds__(256) void learn_delta_export_kernel(LearnTable T, u
         const size_t s = T.order[i];
         long long q[WIDTH];
         bool touched = i >= mark;
+        acc_take<WIDTH>(T, s * WIDTH, q, false);
 #pragma unroll
-        for (int k = 0; k < WIDTH; k++) {
-            q[k] = acc_take(T, s * WIDTH + k, false);
-            touched = touched || q[k] != 0;
-        }
+        for (int k = 0; k < WIDTH; k++) touched = touched || q[k] != 0;
         if (!touched) continue;
         const unsigned long long r = atomicAdd(count, 1ull);
         if ((long long)r >= cap) continue;     // the caller checks *count against cap
