@@ -116,6 +116,20 @@ __device__ __forceinline__ void acc_take(const LearnTable& T, size_t i, long lon
                 if (r < T.reps && v[r][k] != 0) T.acc[(size_t)r * T.rep_stride + i + k] = 0;
 }
 
+// V increment of every lane in the wave: the td sum and the visit count of a slot
+// share a line, and an atomic wave-instruction costs one memory-side request per
+// distinct line, so lane pairs (l, l ^ 1) put a sum and its count into the same
+// instruction: even lanes add their own sum and then the partner's count, odd lanes
+// the partner's count and then their own sum (one request per visit, not two).
+// Called by every lane of the wave (sv < 0: nothing to add).
+__device__ __forceinline__ void v_pair_add(const LearnTable& V, int sv, long long q) {
+    const bool odd = (__lane_id() & 1u) != 0u;
+    const int psv = __shfl_xor(sv, 1);
+    const int s1 = odd ? psv : sv, s2 = odd ? sv : psv;
+    if (s1 >= 0) acc_add(acc_at(V, 2 * (size_t)s1 + (odd ? 1 : 0)), odd ? 1 : q);
+    if (s2 >= 0) acc_add(acc_at(V, 2 * (size_t)s2 + (odd ? 0 : 1)), odd ? q : 1);
+}
+
 // ---- hash tables ------------------------------------------------------------
 // Slot of `key`, inserting it when absent (a defaultdict read inserts,
 // model/ffm_unified.py:658).  Empty slots already hold the default value, so
@@ -1421,50 +1435,52 @@ __global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;   // recs in lane-rank order: the post kernel inherits the locality
-        if (i >= n || trained || (FFM_LABLATE & 2)) continue;
-        double r = a.step_penalty;
-        if (wexit[j]) r = r + a.exit_reward;
-        if (coll[j] >= 0) r = r + (double)coll[j] * a.collision_penalty;
-        int sn = -1;
-        double vn = 0.0;
-        if (!wexit[j]) {
-            const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
-            const unsigned long long nk = encode(a, smn, nx, ny);
-            if (a.V.dense_by) {
-                sn = (int)dense_slot(nk, a.V);
-                vn = tval(a.V, sn)[0];
-                dense_ensure(a.V, (uint32_t)sn, nk);
-            } else {
-                sn = tab_get(a.V, nk, a.overflow);
-                vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
+        int vsl = -1;      // this lane's V slot and fixed-point td, added after the block
+        long long vq = 0;
+        do {
+            if (i >= n || trained || (FFM_LABLATE & 2)) break;
+            double r = a.step_penalty;
+            if (wexit[j]) r = r + a.exit_reward;
+            if (coll[j] >= 0) r = r + (double)coll[j] * a.collision_penalty;
+            int sn = -1;
+            double vn = 0.0;
+            if (!wexit[j]) {
+                const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
+                const unsigned long long nk = encode(a, smn, nx, ny);
+                if (a.V.dense_by) {
+                    sn = (int)dense_slot(nk, a.V);
+                    vn = tval(a.V, sn)[0];
+                    dense_ensure(a.V, (uint32_t)sn, nk);
+                } else {
+                    sn = tab_get(a.V, nk, a.overflow);
+                    vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
+                }
             }
-        }
-        int sv;
-        if (a.V.dense_by) {
-            sv = (int)dense_slot(skey[j], a.V);
-            dense_ensure(a.V, (uint32_t)sv, skey[j]);
-        } else {
-            sv = tab_get(a.V, skey[j], a.overflow);
-        }
-        if (sv < 0) continue;
-        const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
-        if (!(FFM_LABLATE & 1)) {
-            acc_add(acc_at(a.V, 2 * (size_t)sv), fx(td));
-            if (!(FFM_LABLATE & 16)) acc_add(acc_at(a.V, 2 * (size_t)sv + 1), 1);
-        }
-        if (!actor) continue;
-        if (act[j] < 0) continue;
-        if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
-        if (hsl[j] < 0) continue;
-        if (post_update) {
-            LearnRec rc;
-            rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
-            a.recs[e * A + i] = rc;
-        } else if (avalid[j] && !(FFM_LABLATE & 1)) {
-            acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + act[j]), fx(a.alpha_h * td));
-        }
+            int sv;
+            if (a.V.dense_by) {
+                sv = (int)dense_slot(skey[j], a.V);
+                dense_ensure(a.V, (uint32_t)sv, skey[j]);
+            } else {
+                sv = tab_get(a.V, skey[j], a.overflow);
+            }
+            if (sv < 0) break;
+            const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
+            vsl = sv;
+            vq = fx(td);
+            if (!actor) break;
+            if (act[j] < 0) break;
+            if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
+            if (hsl[j] < 0) break;
+            if (post_update) {
+                LearnRec rc;
+                rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
+                a.recs[e * A + i] = rc;
+            } else if (avalid[j] && !(FFM_LABLATE & 1)) {
+                acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + act[j]), fx(a.alpha_h * td));
+            }
+        } while (false);
+        if (!(FFM_LABLATE & 1)) v_pair_add(a.V, vsl, vq);
     }
-
     LSTAMP(4);
     // ---- exit removal (order preserving), counters ---------------------------------------
     int base_ = 0;
