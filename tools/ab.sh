@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 LIBS=$1; shift
 for r in 1 2 3; do
   for f in $LIBS; do
-    v=$(FFM_LIB_PATH=$PWD/$f timeout -k 10 120 python3 bench.py --no-cpu "$@" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['step_ms_events']*1000,1), 'us')") || exit 1
+    v=$(FFM_LIB_PATH=$PWD/$f timeout -k 10 120 python3 bench.py --no-cpu "$@" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d.get('step_ms_events', d.get('kernel_ms_mean'))*1000,1), 'us', round(d['value']/1e9,2), 'G')") || exit 1
     echo "$(basename $f .so) $v"
   done
 done
