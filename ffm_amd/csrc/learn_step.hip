@@ -1088,6 +1088,9 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 // Diagnostic builds only (tools/learn_ablate.sh): FFM_LABLATE bits drop parts of the
 // batched step to time them.  1: table increments, 2: learning phase,
 // 4: policy (agents stay; no H lookup), 8: DFF stencil, 16: V visit counts.
+#ifndef FFM_SMALL_LPE
+#define FFM_SMALL_LPE 32
+#endif
 #ifndef FFM_SMALL_EPB
 #define FFM_SMALL_EPB 8
 #endif
@@ -2071,6 +2074,11 @@ hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
     constexpr size_t kLds = 64 * 1024;
     // 32-lane envs: FFM_SMALL_EPB of them per workgroup (a CU holds a limited
     // number of workgroups; one-wave workgroups would leave most of its wave slots idle)
+    // FFM_SMALL_LPE = 16: two agent slots per lane (agents i and i + 16), 16 envs per
+    // workgroup: at steady state most envs hold <= 16 live agents, so the second slot's
+    // phases are skipped wave-wide and half as many waves carry the same agents
+    if (FFM_SMALL_LPE == 16 && A <= 32 && batch_carve(HW, A, D, 16, true).shared <= kLds)
+        return launch_batch_t<256, 16, 2, D, true>(a, s);
     if (A <= 32 && batch_carve(HW, A, D, FFM_SMALL_EPB, true).shared <= kLds)
         return launch_batch_t<32 * FFM_SMALL_EPB, FFM_SMALL_EPB, 1, D, true>(a, s);
     if (A <= 32 && batch_carve(HW, A, D, 2).shared <= kLds) return launch_batch_t<64, 2, 1, D, false>(a, s);
