@@ -1188,8 +1188,13 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB,
     return c;
 }
 
+#ifndef FFM_LBATCH_WAVES
+#define FFM_LBATCH_WAVES 1   // minimum waves per SIMD asked of the register allocator
+#endif
+
 template <int BS, int EPB, int APT, int D, bool DL>
-__global__ __launch_bounds__(BS) void learn_batch_kernel(LearnArgs a) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(FFM_LBATCH_WAVES, 8)))
+void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LPE = BS / EPB;
     const int H = a.H, W = a.W, HW = a.HW, A = a.A;
