@@ -154,3 +154,46 @@ def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_peri
             np.savez(out_path, **summ)
     finally:
         dist.destroy_process_group()
+
+
+def rccl_learn_worker(rank, world, port, variant, mode, n, steps, sync_period, dense, out_path):
+    """RCCL (backend "nccl") TableSync over a GPU Learner on cuda:0 (world 1 on the
+    one-GPU box: the collectives run through RCCL on device buffers), against one
+    Learner stepping the same envs without the exchange, same sync period."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from ffm_amd.data import make_room, l1_sff
+        from ffm_amd.dist import TableSync
+        from ffm_amd.engine import Learner
+        m = make_room(12, 12)
+        s = l1_sff(m)
+        kw = dict(mode=mode, params={"epsilon": 0.1, "block_size": 1}, rng="philox", seed=21, auto_reset=True,
+                  max_steps=40, n_envs=n, n_agents=32)
+        one = Learner(m, s, variant, **kw)
+        one.set_sync_period(sync_period)
+        one.reset()
+        one.step(steps)
+        sh = Learner(m, s, variant, **kw)
+        sh.reset()
+        sync = TableSync(sh, device="cuda", capacity=1 << 16, sync_period=sync_period, dense=dense)
+        sync.step(steps)
+        torch.cuda.synchronize()
+        res = {"exchanges": np.array(sync.exchanges)}
+        for which in ["V"] + (["H"] if one.actor else []):
+            for tag, L in (("one", one), ("sync", sh)):
+                k, v = L.export_table(which)
+                o = np.argsort(k)
+                res[f"{tag}_{which}_k"] = np.asarray(k)[o]
+                res[f"{tag}_{which}_v"] = np.asarray(v)[o].view(np.uint64)
+        for tag, L in (("one", one), ("sync", sh)):
+            p, c, d = L.get_state()
+            res[f"{tag}_cnt"] = c
+            res[f"{tag}_dff"] = d.view(np.uint32)
+        one.close()
+        sh.close()
+        np.savez(out_path, **res)
+    finally:
+        dist.destroy_process_group()

@@ -371,6 +371,26 @@ def test_learner_coupled_shards_equal_one_learner(variant, mode, sync, dense):
         L.close()
 
 
+@pytest.mark.parametrize("variant,mode,dense", [("unified", "actor_only", True), ("actor_only", None, False)])
+def test_rccl_table_sync_equals_one_learner(variant, mode, dense, tmp_path):
+    """The RCCL branch of ffm_amd.dist.TableSync (backend "nccl" = RCCL on ROCm) on the
+    one-GPU box, world 1: the dense accumulator all-reduce + presence all-gather / the
+    fixed-capacity record all-gathers run through RCCL on device buffers, and the
+    tables end bit-equal to one Learner stepping the same envs (sync period 4)."""
+    import socket
+    import torch.multiprocessing as mp
+    import dist_worker as W
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    out = str(tmp_path / "rccl.npz")
+    mp.spawn(W.rccl_learn_worker, args=(1, port, variant, mode, 512, 24, 4, dense, out), nprocs=1, join=True)
+    r = dict(np.load(out))
+    assert int(r["exchanges"]) > 0
+    for k in [k for k in r if k.startswith("one_")]:
+        assert np.array_equal(r[k], r["sync_" + k[4:]]), k
+
+
 @pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None), ("unified", "critic_only")])
 def test_learner_curriculum_schedule_and_episode_log(variant, mode):
     """The batched training drivers' knobs against the CPU restatement: radius-limited
