@@ -135,7 +135,7 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     T.t.stride = width == 1 ? 2 : 8;        // 16 B / 64 B records (key + values [+ pad])
     if ((e = hipMalloc((void**)&T.t.rec, T.cap * T.t.stride * 8)) != hipSuccess) return e;
     // hashed tables: copies of the accumulators (LearnTable::reps); FFM_ACC_REPS overrides
-    uint32_t reps = dense_by ? 1u : 8u;
+    uint32_t reps = dense_by ? 1u : 4u;
     if (!dense_by)
         if (const char* ev = getenv("FFM_ACC_REPS")) {
             const long r = strtol(ev, nullptr, 10);
