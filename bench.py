@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
     ap.add_argument("--steps", type=int, default=None, help="default 500 (configs 2-4), 50 (config 5)")
     ap.add_argument("--warmup", type=int, default=None, help="default 50 (configs 2-4), 5 (config 5)")
+    ap.add_argument("--burn-in", type=int, default=None,
+                    help="untimed steps after reset before the warmup, so the timed envs are desynchronised "
+                         "(steady state) instead of all starting their first episode together; default 1000 "
+                         "(config 2), 400 (config 3), 0 (learner configs)")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
     ap.add_argument("--size", type=int, default=None)
     ap.add_argument("--agents", type=int, default=None)
@@ -58,6 +62,9 @@ def parse():
     ap.add_argument("--envs-per-block", type=int, default=0)
     ap.add_argument("--cpu-envs", type=int, default=4096)
     ap.add_argument("--cpu-steps", type=int, default=0, help="0 = size the sample to ~15 s")
+    ap.add_argument("--cpu-budget", type=float, default=60.0,
+                    help="configs 2/3: seconds the CPU baseline may take to replay ALL envs of the timed engine "
+                         "through every step it ran (and check them bit-exactly); beyond it a bounded sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = this process's CPU share (OMP_NUM_THREADS, else its affinity set)")
     ap.add_argument("--repeats", type=int, default=5,
@@ -79,6 +86,7 @@ def parse():
     a.envs = a.envs or envs
     a.steps = a.steps if a.steps is not None else steps
     a.warmup = a.warmup if a.warmup is not None else warmup
+    a.burn_in = a.burn_in if a.burn_in is not None else {2: 1000, 3: 400}.get(a.config, 0)
     return a
 
 
@@ -119,7 +127,9 @@ def main():
                  envs_per_block=args.envs_per_block)
     stream = torch.cuda.current_stream()
     eng.reset(stream)
-    eng.step(args.warmup, stream)
+    # burn-in: every env starts its first episode at the same step; after ~10 episodes
+    # the episode phases are spread out and each step sees the steady-state population
+    eng.step(args.burn_in + args.warmup, stream)
     torch.cuda.synchronize()
 
     # Timed regions: K back-to-back step launches on the stream, nothing in between.
@@ -138,6 +148,10 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize()
     kern_ms = [ev0.elapsed_time(ev1) / nk]
+    # the engine's state after every single-step launch it ran (the CPU baseline replays
+    # all envs through the same steps and compares them bit for bit)
+    single_steps = args.burn_in + args.warmup + reps["summary"]["n"] * args.steps + nk
+    snap = eng.get_state() if rank == 0 and not args.no_cpu else None
 
     # Achievable HBM bandwidth on this box: a device-to-device copy of the same
     # number of bytes one launch moves (read + write), for context beside `peak`.
@@ -186,7 +200,11 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": (f"ffm_core step, {H}x{W} room, {A} agents/env, {E} envs/GPU, "
-                             f"{args.neighborhood}, Philox seed {args.seed}, on-device auto-reset"),
+                             f"{args.neighborhood}, Philox seed {args.seed}, on-device auto-reset, "
+                             + (f"steady state (envs desynchronised by a {args.burn_in}-step untimed burn-in "
+                                f"after reset)" if args.burn_in else
+                                "all envs start their first episode in phase (no burn-in)")),
+                "burn_in_steps": args.burn_in,
                 "map": f"{H}x{W}", "agents_per_env": A, "envs_per_gpu": E,
                 "global_envs": E * world, "parallelism": f"env-sharded x{world}",
             },
@@ -206,7 +224,7 @@ def main():
             "multi_step": multi,
         }
         if not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(args, m, s, params, torch)
+            out["cpu_baseline"] = cpu_baseline(args, m, s, params, snap, single_steps)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
@@ -455,30 +473,59 @@ def copy_bandwidth(torch, stream, nbytes, reps=50):
     return 2 * n * 4 / sec / 1e9
 
 
-def cpu_baseline(args, m, s, params, torch):
-    """Time the CPU restatement (oracle/, Philox mode) on a bounded sample of the
-    same workload; check its first envs bit-exactly against a fresh GPU run."""
+def cpu_baseline(args, m, s, params, snap, single_steps):
+    """Time the CPU restatement (oracle/, Philox mode) on the same workload.
+
+    Full replay (the default whenever it fits --cpu-budget): every env of the timed
+    engine, from the same reset, through every single-step launch the engine ran
+    (burn-in, warmup, timed regions, event pass); the oracle's state is then compared
+    bit for bit with the engine's snapshot -- all envs, positions, counts and DFF.
+    The timed span is the replay's steady-state tail, the last ~15 s (the first
+    steps are the post-reset transient).  Otherwise a bounded sample of --cpu-envs
+    envs, checked against a fresh GPU engine."""
     from oracle import oracle as O
     from ffm_amd.engine import Engine
-    A, E = args.agents, args.cpu_envs
+    A = args.agents
     H, W = m.shape
     share, host = cpu_share()
     threads = args.cpu_threads or share
     core = O.Core(m, s, params)
-    pos = np.stack([core.reset_philox(A, args.seed, 0, e) for e in range(E)])
-    cnt = np.full(E, A, np.int32)
-    dff = np.zeros((E, H, W), np.float32)
-    eps = np.zeros(E, np.int32)
-    # a bounded sample: whole steps until ~15 s of CPU work (--cpu-steps fixes the count)
-    t = 1
-    total = 0
+
+    def fresh(E):
+        pos = np.stack([core.reset_philox(A, args.seed, 0, e) for e in range(E)])
+        return pos, np.full(E, A, np.int32), np.zeros((E, H, W), np.float32), np.zeros(E, np.int32)
+
+    # calibrate on 512 envs x 8 steps, then decide between the full replay and a sample
+    pc, cc, dc, ec = fresh(min(512, args.envs))
     tb = time.perf_counter()
-    steps = 0
-    while (args.cpu_steps and steps < args.cpu_steps) or (not args.cpu_steps and time.perf_counter() - tb < 15.0):
-        total += core.step_philox_batch(pos, cnt, dff, eps, args.seed, t, True, A, 0, threads)
-        t += 1
-        steps += 1
-    elapsed = time.perf_counter() - tb
+    for t in range(1, 9):
+        core.step_philox_batch(pc, cc, dc, ec, args.seed, t, True, A, 0, threads)
+    env_step_s = (time.perf_counter() - tb) / (8 * len(cc))
+    full = (snap is not None and not args.cpu_steps
+            and env_step_s * args.envs * single_steps < args.cpu_budget)
+    E = args.envs if full else args.cpu_envs
+    pos, cnt, dff, eps = fresh(E)
+    total = 0
+    t = 1
+    tb = time.perf_counter()
+    if full:
+        # time the replay's last ~15 s: steps from t_timed on
+        t_timed = max(1, single_steps - int(15.0 / max(env_step_s * E, 1e-9)))
+        t_start = None
+        while t <= single_steps:
+            if t == t_timed:
+                t_start, total = time.perf_counter(), 0
+            total += core.step_philox_batch(pos, cnt, dff, eps, args.seed, t, True, A, 0, threads)
+            t += 1
+        elapsed = time.perf_counter() - t_start
+        steps = single_steps - t_timed + 1
+    else:
+        steps = 0
+        while (args.cpu_steps and steps < args.cpu_steps) or (not args.cpu_steps and time.perf_counter() - tb < 15.0):
+            total += core.step_philox_batch(pos, cnt, dff, eps, args.seed, t, True, A, 0, threads)
+            t += 1
+            steps += 1
+        elapsed = time.perf_counter() - tb
     # single-thread rate on a smaller slice of the same state (~3 s)
     n1 = min(E, 512)
     p1, c1_, d1, e1 = pos[:n1].copy(), cnt[:n1].copy(), dff[:n1].copy(), eps[:n1].copy()
@@ -487,21 +534,26 @@ def cpu_baseline(args, m, s, params, torch):
         tot1 += core.step_philox_batch(p1, c1_, d1, e1, args.seed, t1, True, A, 0, 1)
         t1 += 1
     one_thread = tot1 / (time.perf_counter() - st1)
-    # bit-exact check of the first envs against a fresh GPU engine
-    nchk = min(1024, E)
-    g = Engine(m, s, n_envs=nchk, n_agents=A, params=params, rng="philox", seed=args.seed,
-               auto_reset=True, env_base=0)
-    g.reset()
-    g.step(t - 1)
-    gp, gc, gd = g.get_state()
-    g.close()
-    ok = bool(np.array_equal(gc, cnt[:nchk]) and np.array_equal(gd.view(np.uint32), dff[:nchk].view(np.uint32))
-              and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(nchk)))
+    if full:
+        gp, gc, gd = snap
+        what = f"all {E} envs of the timed engine after its {single_steps} single-step launches"
+    else:
+        g = Engine(m, s, n_envs=E, n_agents=A, params=params, rng="philox", seed=args.seed,
+                   auto_reset=True, env_base=0)
+        g.reset()
+        g.step(t - 1)
+        gp, gc, gd = g.get_state()
+        g.close()
+        what = f"all {E} envs of a fresh GPU engine after {t - 1} steps"
+    ok = bool(np.array_equal(gc, cnt) and np.array_equal(gd.view(np.uint32), dff.view(np.uint32))
+              and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(E)))
     return {
         "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
         "sample": (f"oracle/ffm_oracle.c Philox mode, {E} envs x {steps} steps of the same workload "
-                   f"(OpenMP {threads} threads, {host['cpu_model']}); first {nchk} envs bit-exact vs GPU: {ok}"),
-        "seconds": elapsed, "bit_exact_vs_gpu": ok, "value_1thread": one_thread,
+                   + (f"(the last {steps} of a {single_steps}-step replay) " if full else "")
+                   + f"(OpenMP {threads} threads, {host['cpu_model']}); {what} bit-exact vs the oracle: {ok}"),
+        "seconds": elapsed, "bit_exact_vs_gpu": ok, "checked_envs": E, "checked_steps": single_steps if full else t - 1,
+        "value_1thread": one_thread,
         "value_per_core_x_nproc": one_thread * (host["nproc"] or 1), "host": host,
         "threads_note": ("the GPU's host-CPU share on the box (OMP_NUM_THREADS); nproc is the whole machine, "
                          "value_per_core_x_nproc extrapolates the 1-thread rate to every core"),

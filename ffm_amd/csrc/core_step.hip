@@ -1145,6 +1145,64 @@ hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---- trajectory capture (model/ffm_core.py:119-133 run() / main.py:44-54 keep a copy of
+// `positions` after every step; the last row of an episode is the empty one) ---------
+// One wave per selected env, launched after every step.  An env whose episode counter
+// moved during the step was emptied by it (and re-placed by the auto-reset): its row is
+// the empty row that ended the logged episode.  An env that was already empty (no
+// auto-reset) logs nothing.
+__global__ __launch_bounds__(64) void core_capture_init_kernel(CoreStepArgs a, CoreCapture c) {
+    const int i = (int)(blockIdx.x * 64 + threadIdx.x);
+    if (i >= c.n_sel) return;
+    const long long e = c.envs[i];
+    c.state[3 * i] = a.episodes[e];
+    c.state[3 * i + 1] = 0;
+    c.state[3 * i + 2] = a.cnt[e];
+}
+
+__global__ __launch_bounds__(64) void core_capture_kernel(CoreStepArgs a, CoreCapture c) {
+    const int b = (int)blockIdx.x, lane = (int)threadIdx.x;
+    const long long e = c.envs[b];
+    int* st = c.state + 3 * b;
+    const int k = st[0], steps = st[1] + 1, last = st[2];
+    const int know = a.episodes[e], n = a.cnt[e];
+    const bool ended = know != k;
+    const int rc = ended ? 0 : n;
+    const int ph = c.phase ? c.phase[b] : 0;
+    const bool log = !(rc == 0 && last == 0) && (k + ph) % c.period == 0;
+    if (log) {
+        unsigned long long row = 0;
+        if (lane == 0) row = atomicAdd(c.n, 1ull);
+        row = (unsigned long long)__shfl((long long)row, 0);
+        if ((long long)row < c.cap) {
+            if (lane == 0) {
+                int* m = c.meta + 4 * row;
+                m[0] = (int)(a.env_base + e);
+                m[1] = k;
+                m[2] = steps;
+                m[3] = rc;
+            }
+            for (int j = lane; j < a.A; j += 64)
+                c.cells[row * a.A + j] = j < rc ? a.pos[e * a.A + j] : (uint16_t)0xFFFF;
+        }
+    }
+    if (lane == 0) {
+        st[0] = know;
+        st[1] = ended ? 0 : (rc == 0 && last == 0 ? st[1] : steps);
+        st[2] = n;
+    }
+}
+
+hipError_t launch_core_capture_init(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s) {
+    core_capture_init_kernel<<<dim3((unsigned)((c.n_sel + 63) / 64)), dim3(64), 0, s>>>(a, c);
+    return hipGetLastError();
+}
+
+hipError_t launch_core_capture(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s) {
+    core_capture_kernel<<<dim3((unsigned)c.n_sel), dim3(64), 0, s>>>(a, c);
+    return hipGetLastError();
+}
+
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0, float c1,
                              hipStream_t s) {
     const long long total = E * H * W;

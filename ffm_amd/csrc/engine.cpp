@@ -78,7 +78,14 @@ struct ffm_engine {
     bool block_reset = false;    // placement by core_block_reset_kernel (free list beyond the wave reset's LDS)
     unsigned char* d_scratch = nullptr;    // [E][scratch_stride]
     size_t scratch_stride = 0;
+    ffm::CoreCapture cap{};      // trajectory capture (n_sel = 0: off)
 };
+
+static void free_capture(ffm_engine* e) {
+    void* bufs[] = {(void*)e->cap.envs, (void*)e->cap.phase, e->cap.state, e->cap.meta, e->cap.cells, e->cap.n};
+    for (void* p : bufs) (void)hipFree(p);
+    e->cap = ffm::CoreCapture{};
+}
 
 extern "C" {
 
@@ -101,6 +108,7 @@ static void release(ffm_engine* e) {
     (void)hipFree(e->d_mt_py);
     (void)hipFree(e->d_dbg);
     (void)hipFree(e->d_scratch);
+    free_capture(e);
     delete e;
 }
 
@@ -363,7 +371,7 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
 int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     if (!e || n_steps < 0) return fail(FFM_E_INVALID, "bad engine/n_steps");
     hipStream_t s = (hipStream_t)stream;
-    if (e->fused > 1 && e->multi) {
+    if (e->fused > 1 && e->multi && e->cap.n_sel == 0) {
         // k steps per launch, the state of each env pair on chip (core_multi.hip)
         for (int done = 0; done < n_steps;) {
             const int k = std::min(e->fused, n_steps - done);
@@ -380,6 +388,7 @@ int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
         else if (e->lane) HIP_TRY(ffm::launch_core_lane(a, e->d.neighborhood, e->lane_blocks, s));
         else if (e->wave) HIP_TRY(ffm::launch_core_wave(a, e->d.neighborhood, e->mt, e->wave_blocks, s));
         else HIP_TRY(ffm::launch_core_block(a, e->d.neighborhood, e->f64, e->mt, e->block, s));
+        if (e->cap.n_sel) HIP_TRY(ffm::launch_core_capture(a, e->cap, s));
         e->t++;
     }
     return FFM_OK;
@@ -398,7 +407,11 @@ int ffm_engine_reset(ffm_engine* e, void* stream) {
     HIP_TRY(hipMemsetAsync(e->d_dff, 0, E * e->HW * 4, s));
     HIP_TRY(hipMemsetAsync(e->d_cnt, 0, E * 4, s));
     HIP_TRY(hipMemsetAsync(e->d_pos, 0xFF, E * e->d.agent_capacity * 2, s));
-    if (e->mt) return FFM_OK;  // the caller uploads positions drawn from its own MT stream
+    HIP_TRY(hipMemsetAsync(e->d_eps, 0, E * 4, s));   // episodes count from this reset
+    if (e->mt) {   // the caller uploads positions drawn from its own MT stream
+        if (e->cap.n_sel) HIP_TRY(ffm::launch_core_capture_init(make_args(e), e->cap, s));
+        return FFM_OK;
+    }
     // Philox placement, same stream as the in-kernel auto-reset (key: current t).
     if (e->block_reset) {
         ffm::CoreStepArgs a = make_args(e);
@@ -408,6 +421,7 @@ int ffm_engine_reset(ffm_engine* e, void* stream) {
         HIP_TRY(ffm::launch_core_reset(make_args(e), s));
     }
     e->t++;
+    if (e->cap.n_sel) HIP_TRY(ffm::launch_core_capture_init(make_args(e), e->cap, s));
     return FFM_OK;
 }
 
@@ -512,6 +526,68 @@ int ffm_engine_get_mt_state(ffm_engine* e, int64_t env, uint32_t* np_key, int32_
     *np_pos = (int32_t)buf[624];
     std::memcpy(py_key, buf + 625, 624 * 4);
     *py_pos = (int32_t)buf[1249];
+    return FFM_OK;
+}
+
+int ffm_engine_set_trajectory_capture(ffm_engine* e, const int32_t* envs, const int32_t* phases, int32_t n_sel,
+                                      int32_t period, int64_t capacity_rows, void* stream) {
+    if (!e) return fail(FFM_E_INVALID, "null engine");
+    if (n_sel < 0 || (n_sel > 0 && (!envs || period < 1 || capacity_rows < 1)))
+        return fail(FFM_E_INVALID, "trajectory capture: envs, period >= 1 and capacity_rows >= 1 are required");
+    for (int32_t i = 0; i < n_sel; i++) {
+        if (envs[i] < 0 || envs[i] >= e->d.n_envs) return fail(FFM_E_INVALID, "trajectory capture: env out of range");
+        if (phases && phases[i] < 0) return fail(FFM_E_INVALID, "trajectory capture: phase must be >= 0");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipStreamSynchronize(s));        // queued steps may still write the old buffers
+    free_capture(e);
+    if (n_sel == 0) return FFM_OK;
+    ffm::CoreCapture& c = e->cap;
+    const size_t A = (size_t)e->d.agent_capacity;
+    int* de = nullptr; int* dp = nullptr;
+    hipError_t he = hipMalloc((void**)&de, (size_t)n_sel * 4);
+    if (he == hipSuccess && phases) he = hipMalloc((void**)&dp, (size_t)n_sel * 4);
+    c.envs = de; c.phase = dp;
+    if (he == hipSuccess) he = hipMalloc((void**)&c.state, (size_t)n_sel * 12);
+    if (he == hipSuccess) he = hipMalloc((void**)&c.meta, (size_t)capacity_rows * 16);
+    if (he == hipSuccess) he = hipMalloc((void**)&c.cells, (size_t)capacity_rows * A * 2);
+    if (he == hipSuccess) he = hipMalloc((void**)&c.n, 8);
+    if (he != hipSuccess) {
+        free_capture(e);
+        return fail(FFM_E_NOMEM, std::string("trajectory capture: ") + hipGetErrorString(he));
+    }
+    c.cap = capacity_rows; c.period = period;
+    HIP_TRY(hipMemcpyAsync(de, envs, (size_t)n_sel * 4, hipMemcpyHostToDevice, s));
+    if (dp) HIP_TRY(hipMemcpyAsync(dp, phases, (size_t)n_sel * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(c.n, 0, 8, s));
+    c.n_sel = n_sel;
+    HIP_TRY(ffm::launch_core_capture_init(make_args(e), c, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return FFM_OK;
+}
+
+int ffm_engine_drain_trajectory(ffm_engine* e, int32_t* meta, uint16_t* cells, int64_t cap, int64_t* n,
+                                int64_t* dropped, void* stream) {
+    if (!e || !n) return fail(FFM_E_INVALID, "null argument");
+    *n = 0;
+    if (dropped) *dropped = 0;
+    if (e->cap.n_sel == 0) return FFM_OK;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, e->cap.n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const long long have = std::min<long long>((long long)c, e->cap.cap);
+    if (have > cap) {
+        *n = have;
+        return fail(FFM_E_INVALID, "drain_trajectory: buffer too small (*n holds the count)");
+    }
+    const size_t A = (size_t)e->d.agent_capacity;
+    if (have > 0 && meta) HIP_TRY(hipMemcpyAsync(meta, e->cap.meta, (size_t)have * 16, hipMemcpyDeviceToHost, s));
+    if (have > 0 && cells) HIP_TRY(hipMemcpyAsync(cells, e->cap.cells, (size_t)have * A * 2, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemsetAsync(e->cap.n, 0, 8, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n = have;
+    if (dropped) *dropped = (int64_t)c - have;
     return FFM_OK;
 }
 

@@ -35,6 +35,19 @@ struct CoreStepArgs {
     size_t scratch_stride;
 };
 
+// Trajectory capture of the batched ffm_core step (ffm_engine_set_trajectory_capture):
+// rows of {global env, episode, step in episode, count} + agent cells after every step.
+struct CoreCapture {
+    const int* envs;           // [n_sel] local env indices
+    const int* phase;          // [n_sel] or nullptr
+    int* state;                // [n_sel][3]: episode being logged, its steps so far, count after the last step
+    int* meta;                 // [cap][4]
+    uint16_t* cells;           // [cap][A]
+    unsigned long long* n;     // rows appended (may pass cap: dropped)
+    long long cap;
+    int n_sel, period;
+};
+
 size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves);
 size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool mt, bool reset);
 hipError_t launch_core_wave(const CoreStepArgs& a, int nb, bool mt, int blocks, hipStream_t s);
@@ -58,6 +71,8 @@ size_t core_big_scratch_bytes(int H, int W, int A, int F, bool mt);
 hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,
                              float c1, hipStream_t s);
+hipError_t launch_core_capture_init(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s);
+hipError_t launch_core_capture(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s);
 hipError_t launch_np_expf(const float* x, float* y, long long n, hipStream_t s);
 
 }  // namespace ffm

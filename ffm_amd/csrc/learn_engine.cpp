@@ -135,12 +135,17 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     T.t.stride = width == 1 ? 2 : 8;        // 16 B / 64 B records (key + values [+ pad])
     if ((e = hipMalloc((void**)&T.t.rec, T.cap * T.t.stride * 8)) != hipSuccess) return e;
     // hashed tables: copies of the accumulators (LearnTable::reps); FFM_ACC_REPS overrides
+    // (they spread the adds of hot keys over several memory-side atomic units; a large
+    // table has few hot keys per slot, so the copies shrink to keep the accumulators
+    // within kAccRepBytes: 4 copies up to 2^22 V slots / 2^21 H slots)
+    constexpr size_t kAccRepBytes = (size_t)256 << 20;
     uint32_t reps = dense_by ? 1u : 4u;
     if (!dense_by)
         if (const char* ev = getenv("FFM_ACC_REPS")) {
             const long r = strtol(ev, nullptr, 10);
             if (r >= 1 && r <= 8 && (r & (r - 1)) == 0) reps = (uint32_t)r;   // kMaxAccReps
         }
+    while (reps > 1 && T.cap * T.accw * 8 * reps > kAccRepBytes) reps >>= 1;
     T.t.reps = reps;
     T.t.rep_stride = (unsigned long long)(T.cap * T.accw);
     if ((e = hipMalloc((void**)&T.t.acc, T.cap * T.accw * 8 * reps)) != hipSuccess) return e;
@@ -189,6 +194,16 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.mW = magic(d.W);
     a.mBS = magic(a.bs);
     return a;
+}
+
+// Overflow without a host sync: a step queued a copy of the device flag into pinned
+// memory behind itself; whatever of it has landed is reported (every sync point --
+// counters, export, get_state -- reports it exactly through check_overflow).
+static int async_overflow(ffm_learner* l) {
+    const int32_t ov = l->h_overflow ? __atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) : 0;
+    if (ov & 1) return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
+    if (ov & 4) return fail(FFM_E_INVALID, "asynchronous delta export: record buffer too small (raise its capacity)");
+    return FFM_OK;
 }
 
 static int check_overflow(ffm_learner* l, hipStream_t s) {
@@ -456,6 +471,21 @@ static int phase_end(ffm_learner* l, hipStream_t s) {
     return FFM_OK;
 }
 
+// With a sync period K > 1, increments of up to K - 1 steps can be pending between two
+// applies.  Reading, replacing or re-periodising the tables at such a point applies them
+// first (as if the period ended with the last step) and restarts the period, so an
+// export never misses steps and a new period never stretches the current one.
+static int flush_pending(ffm_learner* l, hipStream_t s) {
+    if (l->mt || l->since_apply == 0 || l->phase != 0) return FFM_OK;
+    if (!l->trained) HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
+    if (l->actor) {
+        HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
+        l->hstat_valid = true;
+    }
+    l->since_apply = 0;
+    return FFM_OK;
+}
+
 int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
     if (!l || n_steps < 0) return fail(FFM_E_INVALID, "bad learner/n_steps");
     if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
@@ -463,10 +493,8 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
     // Overflow without a host sync: the previous call queued a copy of the flag
     // into pinned memory behind its steps; whatever of it has landed is reported
     // here (every sync point -- counters, export, get_state -- reports it exactly).
-    if (l->h_overflow && (__atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) & 1))
-        return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
-    if (l->h_overflow && (__atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) & 4))
-        return fail(FFM_E_INVALID, "asynchronous delta export: record buffer too small (raise its capacity)");
+    int rc0 = async_overflow(l);
+    if (rc0) return rc0;
     for (int i = 0; i < n_steps; i++) {
         if (l->mt) {
             HIP_TRY(ffm::launch_learn_exact(make_args(l), s));
@@ -488,6 +516,8 @@ int ffm_learner_step_local(ffm_learner* l, void* stream) {
     if (!l) return fail(FFM_E_INVALID, "null learner");
     if (l->mt) return fail(FFM_E_INVALID, "phased steps are the batched (Philox) step");
     if (l->phase != 0) return fail(FFM_E_INVALID, "step_local: previous step not ended");
+    int rc = async_overflow(l);    // the flag copy queued by an earlier step_end
+    if (rc) return rc;
     return phase_local(l, (hipStream_t)stream);
 }
 
@@ -503,7 +533,12 @@ int ffm_learner_step_apply(ffm_learner* l, int32_t which, void* stream) {
 int ffm_learner_step_end(ffm_learner* l, void* stream) {
     if (!l) return fail(FFM_E_INVALID, "null learner");
     if (l->phase != (l->actor ? 3 : 2)) return fail(FFM_E_INVALID, "step_end before the tables were applied");
-    return phase_end(l, (hipStream_t)stream);
+    int rc = phase_end(l, (hipStream_t)stream);
+    // the overflow flag (a full hash table, an undersized delta record buffer) as of this
+    // step, copied behind it without a host sync: step_local reports it once it has landed
+    if (!rc && l->h_overflow)
+        HIP_TRY(hipMemcpyAsync(l->h_overflow, l->d_overflow, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return rc;
 }
 
 int ffm_learner_delta_export(ffm_learner* l, int32_t which, uint64_t* d_keys, int64_t* d_acc, int64_t cap,
@@ -687,7 +722,8 @@ int ffm_learner_export_table(ffm_learner* l, int32_t which, uint64_t* keys, doub
     DevTable* T = pick(l, which);
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
     hipStream_t s = (hipStream_t)stream;
-    int rc = check_overflow(l, s);
+    int rc = flush_pending(l, s);
+    if (!rc) rc = check_overflow(l, s);
     if (rc) return rc;
     uint32_t cnt = 0;
     HIP_TRY(hipMemcpyAsync(&cnt, T->t.n, 4, hipMemcpyDeviceToHost, s));
@@ -727,6 +763,7 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
         }
     }
     hipStream_t s = (hipStream_t)stream;
+    if (int rc = flush_pending(l, s)) return rc;
     if (which == FFM_TABLE_H) l->hstat_valid = false;
     HIP_TRY(clear_table(l, *T, which == FFM_TABLE_V ? l->L.v_default : 0.0, s));
     if (n > 0) {
@@ -836,6 +873,11 @@ int ffm_learner_set_sync_period(ffm_learner* l, int32_t period) {
     if (!l || period < 1) return fail(FFM_E_INVALID, "sync period must be >= 1");
     if (l->mt && period != 1) return fail(FFM_E_INVALID, "the exact (MT) step applies every step");
     if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    if (l->since_apply != 0) {   // no stream argument: order behind every queued step
+        HIP_TRY(hipDeviceSynchronize());
+        if (int rc = flush_pending(l, nullptr)) return rc;
+        HIP_TRY(hipDeviceSynchronize());
+    }
     l->sync_period = period;
     l->since_apply = 0;
     return FFM_OK;

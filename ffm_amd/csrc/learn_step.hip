@@ -1758,6 +1758,9 @@ __global__ __launch_bounds__(256) void learn_capture_kernel(LearnArgs a, TrajCap
     const int k = a.episodes[e];
     const int ph = c.phase ? c.phase[b] : 0;
     if ((k + ph) % c.period != 0) return;                 // workgroup-uniform
+    // an env that was already empty when the step began has no step to log (auto_reset
+    // off: its episode never advances); the step that emptied it is still written
+    if (a.cnt[e] == 0 && a.nstart[e] == 0) return;
     if (threadIdx.x == 0) row = (long long)atomicAdd(c.n, 1ull);
     __syncthreads();
     if (row >= c.cap) return;                             // counted as dropped by the drain

@@ -163,13 +163,27 @@ class TableSync:
 
 
 def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16, sync_period: int = 1,
-                 dense: bool = False):
+                 dense: bool = False, async_records: bool = False):
     """TableSync's protocol for several shards driven by one process (e.g. one
     Learner per device, or shards of one device): the same phases, with the
     collectives replaced by handing every shard the others' records (or, dense,
-    the summed accumulators and the presence union)."""
+    the summed accumulators and the presence union).
+
+    ``async_records``: the records travel exactly as TableSync moves them, with no
+    host synchronisation: fixed-capacity device buffers filled by
+    ``delta_export_async`` (the record count stays in device memory) and read by
+    ``delta_merge_async`` (min(count, capacity) records); an export that needs more
+    than ``capacity`` is reported at the shard's next sync point."""
     for s in shards:
         s.set_sync_period(sync_period)
+
+    def export_async(s, which):
+        width = 2 if which == "V" else 5
+        k = torch.zeros(capacity, dtype=torch.int64, device=device)
+        a = torch.zeros((capacity, width), dtype=torch.int64, device=device)
+        c = torch.zeros(1, dtype=torch.int64, device=device)
+        s.delta_export_async(which, k.data_ptr(), a.data_ptr(), capacity, c.data_ptr())
+        return k, a, c
 
     def export(s, which):
         width = 2 if which == "V" else 5   # accumulator words (V: sum of td, visits)
@@ -193,6 +207,14 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
                 b[0].copy_(tot)
                 s.dense_adopt(which, uni.data_ptr())
             torch.cuda.synchronize()
+            return
+        if async_records:
+            recs = [export_async(s, which) for s in shards]
+            for i, s in enumerate(shards):
+                for j, (k, a, c) in enumerate(recs):
+                    if j != i:
+                        s.delta_merge_async(which, k.data_ptr(), a.data_ptr(), c.data_ptr(), capacity)
+            torch.cuda.synchronize()      # the record buffers outlive the merges that read them
             return
         recs = [export(s, which) for s in shards]
         for i, s in enumerate(shards):

@@ -28,6 +28,7 @@ EXPORTED = [
     "ffm_engine_get_state", "ffm_engine_set_mt_state", "ffm_engine_get_mt_state",
     "ffm_engine_get_counters", "ffm_engine_device_buffers", "ffm_engine_get_step_index",
     "ffm_engine_set_step_index", "ffm_engine_set_fused_steps", "ffm_np_expf_device",
+    "ffm_engine_set_trajectory_capture", "ffm_engine_drain_trajectory",
     "ffm_learner_create", "ffm_learner_destroy", "ffm_learner_reset", "ffm_learner_step",
     "ffm_learner_set_state", "ffm_learner_get_state", "ffm_learner_get_episodes",
     "ffm_learner_set_mt_state", "ffm_learner_get_mt_state", "ffm_learner_get_counters",
@@ -109,6 +110,8 @@ def load_library():
     L.ffm_engine_get_step_index.argtypes = [P, C.POINTER(C.c_uint32)]
     L.ffm_engine_set_step_index.argtypes = [P, C.c_uint32]
     L.ffm_engine_set_fused_steps.argtypes = [P, i32]
+    L.ffm_engine_set_trajectory_capture.argtypes = [P, P, P, i32, i32, i64, P]
+    L.ffm_engine_drain_trajectory.argtypes = [P, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     L.ffm_np_expf_device.argtypes = [P, P, i64, P]
     L.ffm_learner_create.argtypes = [C.POINTER(EngineDesc), C.POINTER(LearnDesc), C.POINTER(P)]
     L.ffm_learner_destroy.argtypes = [P]
@@ -277,6 +280,49 @@ class Engine:
 
     def update_dff(self, stream=None):
         _check(self._L.ffm_engine_update_dff(self._h, _stream_handle(stream)))
+
+    # -- episode I/O ---------------------------------------------------------
+    def set_trajectory_capture(self, envs, period: int = 1, phases=None, capacity_rows: int | None = None,
+                               stream=None):
+        """Capture `positions` after every step of episode k of env envs[i] (local index)
+        whenever (k + phases[i]) % period == 0 (k counted from the last reset, 0-based):
+        the per-step log of model/ffm_core.py:119-133 / main.py:44-54, batched.
+        drain_trajectories() returns it.  envs=[] turns capture off.  Default capacity:
+        1,024 steps of every selected env between drains."""
+        envs = np.ascontiguousarray(envs, np.int32).reshape(-1)
+        ph = None if phases is None else np.ascontiguousarray(phases, np.int32).reshape(-1)
+        if ph is not None and len(ph) != len(envs):
+            raise ValueError("phases must have one entry per selected env")
+        cap = int(capacity_rows) if capacity_rows else max(1, 1024 * len(envs))
+        self._traj_cap = cap if len(envs) else 0
+        _check(self._L.ffm_engine_set_trajectory_capture(
+            self._h, _ptr(envs) if len(envs) else None, _ptr(ph) if ph is not None and len(ph) else None,
+            len(envs), int(period), cap, _stream_handle(stream)))
+
+    def drain_trajectories(self, stream=None) -> dict:
+        """Rows captured since the last drain, grouped: {(global env, episode k): (steps [T],
+        positions list of T int32 [n_t, 2] arrays)} in step order -- the positions_log of
+        main.py:44-54 (its last entry the empty array of the step that emptied the room)."""
+        cap = getattr(self, "_traj_cap", 0)
+        if not cap:
+            return {}
+        meta = np.empty((cap, 4), np.int32)
+        cells = np.empty((cap, self.A), np.uint16)
+        n, dropped = C.c_int64(), C.c_int64()
+        _check(self._L.ffm_engine_drain_trajectory(self._h, _ptr(meta), _ptr(cells), cap, C.byref(n),
+                                                   C.byref(dropped), _stream_handle(stream)))
+        if dropped.value:
+            raise RuntimeError(f"trajectory buffer overflowed: {dropped.value} rows lost (drain more often)")
+        meta, cells = meta[: n.value], cells[: n.value]
+        order = np.lexsort((meta[:, 2], meta[:, 1], meta[:, 0]))
+        out = {}
+        for r in order.tolist():
+            env, k, st, c = meta[r].tolist()
+            cc = cells[r, :c].astype(np.int32)
+            steps, pos = out.setdefault((env, k), ([], []))
+            steps.append(st)
+            pos.append(np.stack([cc // self.W, cc % self.W], axis=1))
+        return out
 
     # -- state transfer -----------------------------------------------------
     def get_state(self, env0: int = 0, n: int | None = None, stream=None):

@@ -86,7 +86,9 @@ typedef struct {
     int64_t env_base;         /* global id of env 0 (multi-GPU sharding keys RNG by global id) */
     int32_t device;           /* HIP device ordinal */
     int32_t envs_per_block;   /* 0 = auto, > 0 = block kernel with that many envs per workgroup,
-                                 -1 = wave kernel, -2 = packed-bundle kernel (diagnostics, tests) */
+                                 -1 = wave kernel (core_step.hip), -2 = lane kernel (core_lane.hip),
+                                 -3 = group kernel (core_group.hip; 12x12 only, the auto choice there);
+                                 the negative values force a kernel for diagnostics and tests */
 } ffm_engine_desc;
 
 typedef struct {
@@ -110,7 +112,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out);
 int ffm_engine_destroy(ffm_engine* eng);
 
 /* Place n_agents in every env (Philox mode: keyed by the engine step counter,
- * which then advances) and zero the DFF.  MT mode places nothing: the caller
+ * which then advances), zero the DFF and the per-env episode counters.  MT mode places nothing: the caller
  * draws the placement from its own generator (initialize_agents) and uploads it. */
 int ffm_engine_reset(ffm_engine* eng, void* stream);
 
@@ -140,6 +142,24 @@ int ffm_engine_set_mt_state(ffm_engine* eng, int64_t env, const uint32_t* np_key
                             const uint32_t* py_key, int32_t py_pos, void* stream);
 int ffm_engine_get_mt_state(ffm_engine* eng, int64_t env, uint32_t* np_key, int32_t* np_pos,
                             uint32_t* py_key, int32_t* py_pos, void* stream);
+
+/* Trajectory capture of the batched step (replaces the positions log of
+ * model/ffm_core.py:119-133 run() and main.py:44-54, which keep a copy of `positions`
+ * after every step until the room is empty).  For each selected env (local index) its
+ * episode k (0-based, counted from the last ffm_engine_reset; one episode per auto-reset)
+ * is captured iff (k + phases[i]) % period == 0 (phases NULL: 0).  After every step of a
+ * captured episode one row is appended: meta {global env, k, step in the episode
+ * (1-based), count} and the agent_capacity cells (x*W+y, live agents first in the
+ * reference's order, 0xFFFF after); an episode's last row is the empty one of the step
+ * that emptied the room.  An env that is already empty (auto_reset off) logs nothing.
+ * Rows past capacity_rows are dropped and counted.  While capture is on, ffm_engine_step
+ * makes one launch per step (fused steps are off).  n_sel = 0 turns capture off. */
+int ffm_engine_set_trajectory_capture(ffm_engine* eng, const int32_t* envs, const int32_t* phases, int32_t n_sel,
+                                      int32_t period, int64_t capacity_rows, void* stream);
+/* Rows captured since the last drain, in no particular order (sort by env, k, step);
+ * meta [cap][4] int32, cells [cap][agent_capacity] u16, host pointers. */
+int ffm_engine_drain_trajectory(ffm_engine* eng, int32_t* meta, uint16_t* cells, int64_t cap, int64_t* n,
+                                int64_t* dropped, void* stream);
 
 /* counters[4] = {agent_steps, exits, resets, steps} accumulated since create. */
 int ffm_engine_get_counters(ffm_engine* eng, uint64_t* counters, void* stream);
@@ -186,7 +206,9 @@ typedef struct {
     double v_default;         /* value a V read inserts: 0.0 (-1.0 after ffm_ac_core.set_v_table) */
     int32_t block_size;       /* state-key block size (ffm_actor_only: always 5) */
     int32_t max_steps;        /* Philox mode: an episode also ends after this many steps (0 = never) */
-    int32_t log2_v_capacity;  /* hash-table slots (0 = 21) */
+    int32_t log2_v_capacity;  /* hash-table slots (0 = 21); hashed tables also keep up to 4
+                                 copies of their fixed-point accumulators (V 16 B, H 40 B per
+                                 slot and copy), fewer when the copies would pass 256 MiB */
     int32_t log2_h_capacity;
     /* Philox mode, eps_span > 0: each env explores with
      * clip(eps_start + (eps_end - eps_start) * (k + eps_offset) / eps_span, 0, 1) after k ended
@@ -264,7 +286,9 @@ int ffm_learner_delta_merge_async(ffm_learner* l, int32_t which, const uint64_t*
  * increments of K steps accumulate and V / H (and the actor's H statistics) are applied
  * at every K-th step only; a multi-rank run exchanges deltas at those steps only, so
  * sharded == one device at the same K, bit for bit.  apply_due: 1 if the current (or
- * next) step's step_apply applies. */
+ * next) step's step_apply applies.  A table export / import or a new period between two
+ * applies first applies the pending increments (the period ends at the last step) and
+ * restarts the period. */
 int ffm_learner_set_sync_period(ffm_learner* l, int32_t period);
 int ffm_learner_apply_due(ffm_learner* l, int32_t* due);
 /* Dense (ffm_unified rank-key) tables: the device fixed-point accumulators (acc_count

@@ -371,6 +371,70 @@ def test_learner_coupled_shards_equal_one_learner(variant, mode, sync, dense):
         L.close()
 
 
+@pytest.mark.parametrize("variant,mode,sync", [("actor_only", None, 1), ("actor_only", None, 4), ("ac", None, 1),
+                                               ("unified", "actor_only", 3)])
+def test_learner_async_records_equal_one_learner(variant, mode, sync):
+    """TableSync's record path without host syncs, on the GPU kernels: two Learner shards
+    exchange their deltas through delta_export_async (record count left in device
+    memory, fixed-capacity buffers, 4 accumulator copies summed by the export) and
+    delta_merge_async (count read on the device), sync period K; the tables end bit-equal
+    to one Learner holding all envs, and the env states equal."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.dist import shard_range, step_coupled
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    n, N, T = 1500, 32, 45
+    kw = dict(mode=mode, params=p, rng="philox", seed=33, auto_reset=True, max_steps=30)
+    one = _learner(m, s, variant, n_envs=n, n_agents=N, **kw)
+    one.set_sync_period(sync)
+    one.reset()
+    one.step(T)
+    shards = []
+    for r in range(2):
+        b, c = shard_range(n, r, 2)
+        L = _learner(m, s, variant, n_envs=c, n_agents=N, env_base=b, **kw)
+        L.reset()
+        shards.append(L)
+    step_coupled(shards, T, device="cuda", capacity=1 << 17, sync_period=sync, async_records=True)
+    assert one.counters()["agent_steps"] == sum(L.counters()["agent_steps"] for L in shards)
+    op, oc, od = one.get_state()
+    sp = [L.get_state() for L in shards]
+    assert np.array_equal(oc, np.concatenate([x[1] for x in sp]))
+    assert np.array_equal(od.view(np.uint32), np.concatenate([x[2] for x in sp]).view(np.uint32))
+    for which in ["V"] + (["H"] if one.actor else []):
+        k0, v0 = one.export_table(which)
+        o0 = np.argsort(k0)
+        for L in shards:
+            k, v = L.export_table(which)
+            o = np.argsort(k)
+            assert np.array_equal(k[o], k0[o0]), which
+            assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), which
+    for L in shards + [one]:
+        L.close()
+
+
+def test_learner_async_records_too_small_capacity_is_reported():
+    """An asynchronous delta export with more touched entries than its buffer holds drops
+    the surplus records on the device and is reported loudly (ValueError, FFM_E_INVALID)
+    at the shard's next sync point, and by the next step once the flag copy has landed."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.dist import step_coupled
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    kw = dict(params={"epsilon": 0.1}, rng="philox", seed=3, auto_reset=True, max_steps=30)
+    shards = [_learner(m, s, "actor_only", n_envs=256, n_agents=32, env_base=256 * r, **kw) for r in range(2)]
+    for L in shards:
+        L.reset()
+    step_coupled(shards, 2, device="cuda", capacity=16, async_records=True)
+    with pytest.raises(ValueError, match="record buffer too small"):
+        shards[0].counters()
+    with pytest.raises(ValueError, match="record buffer too small"):
+        shards[1].step_local()
+    for L in shards:
+        L.close()
+
+
 @pytest.mark.parametrize("variant,mode,dense", [("unified", "actor_only", True), ("actor_only", None, False)])
 def test_rccl_table_sync_equals_one_learner(variant, mode, dense, tmp_path):
     """The RCCL branch of ffm_amd.dist.TableSync (backend "nccl" = RCCL on ROCm) on the

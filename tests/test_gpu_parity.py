@@ -395,3 +395,87 @@ def test_philox_block_kernel_capped_placement_keys():
     thresholded candidates kept in LDS, identical to the oracle's full sort."""
     cnt, eps = _philox_compare(40, 40, 16, 300, 200, {"neighborhood": "neumann"}, seed=13, envs_per_block=1)
     assert eps.sum() > 0
+
+
+@pytest.mark.parametrize("H,W,N,epb,fused", [(12, 12, 20, 0, 1), (12, 12, 32, 0, 10), (12, 12, 20, -2, 1),
+                                             (20, 24, 60, 2, 1)])
+def test_engine_trajectory_capture_matches_cpu(H, W, N, epb, fused):
+    """Batched positions log (model/ffm_core.py:119-133 run(), main.py:44-54 positions_log):
+    the rows captured after every step of every selected episode equal the CPU
+    restatement's positions after that step, and each episode ends with the empty row of
+    the step that emptied the room (before the auto-reset re-placed it).  Capture turns
+    fused steps off (one launch per step); the group, lane and block kernels."""
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import oracle as O
+    m = make_room(H, W)
+    s = l1_sff(m)
+    p = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"}
+    E, T, seed = 300, 160, 13
+    sel = np.array([0, 7, 100, 298, 299], np.int32)
+    ph = np.array([0, 1, 0, 1, 1], np.int32)
+    eng = _engine(map_array=m, sff=s, n_envs=E, n_agents=N, params=p, rng="philox", seed=seed, auto_reset=True,
+                  envs_per_block=epb)
+    if fused > 1:
+        eng.set_fused_steps(fused)
+    eng.set_trajectory_capture(sel, period=2, phases=ph, capacity_rows=len(sel) * 64)
+    eng.reset()
+    got = {}
+    for _ in range(T // 40):
+        eng.step(40)
+        for key, (st, ps) in eng.drain_trajectories().items():
+            g = got.setdefault(key, ([], []))
+            g[0].extend(st)
+            g[1].extend(ps)
+    core = O.Core(m, s, p)
+    pos = np.stack([core.reset_philox(N, seed, 0, e) for e in range(E)])
+    cnt = np.full(E, N, np.int32)
+    dff = np.zeros((E, H, W), np.float32)
+    eps = np.zeros(E, np.int32)
+    steps = np.zeros(E, np.int32)
+    want = {}
+    for t in range(1, T + 1):
+        k0 = eps.copy()
+        core.step_philox_batch(pos, cnt, dff, eps, seed, t, True, N, 0, 8)
+        for e, q in zip(sel.tolist(), ph.tolist()):
+            k = int(k0[e])
+            steps[e] += 1
+            ended = eps[e] != k0[e]
+            if (k + q) % 2 == 0:
+                c = 0 if ended else int(cnt[e])
+                cells = pos[e, :c].astype(np.int32)
+                w = want.setdefault((e, k), ([], []))
+                w[0].append(int(steps[e]))
+                w[1].append(np.stack([cells // W, cells % W], axis=1))
+            if ended:
+                steps[e] = 0
+    assert sorted(got) == sorted(want)
+    for key, (st, ps) in want.items():
+        assert got[key][0] == st, f"{key}: steps"
+        for a, b in zip(got[key][1], ps):
+            assert np.array_equal(a, b), f"{key}: positions"
+    ended = [v for v in want.values() if len(v[1][-1]) == 0]
+    assert len(ended) >= len(sel), "whole episodes, each ending with its empty row"
+    gp, gc, _ = eng.get_state()
+    assert np.array_equal(gc, cnt)
+    eng.set_trajectory_capture([])
+    eng.step(1)
+    assert eng.drain_trajectories() == {}
+    eng.close()
+
+
+def test_engine_trajectory_capture_stops_when_empty_without_auto_reset():
+    """auto_reset off: an emptied env logs its final empty row once, then nothing (the
+    reference's run() stops there)."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    eng = _engine(map_array=m, sff=l1_sff(m), n_envs=8, n_agents=3, rng="philox", seed=2, auto_reset=False)
+    eng.set_trajectory_capture([0, 5], period=1)
+    eng.reset()
+    eng.step(200)
+    tr = eng.drain_trajectories()
+    _, gc, _ = eng.get_state()
+    assert (gc[[0, 5]] == 0).all()
+    for (env, k), (st, ps) in tr.items():
+        assert k == 0 and st == list(range(1, len(st) + 1))
+        assert len(ps[-1]) == 0 and all(len(q) > 0 for q in ps[:-1])
+    eng.close()

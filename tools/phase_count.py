@@ -9,16 +9,13 @@ import subprocess
 import sys
 
 args = sys.argv[1:]
-pack = "--pack" in args
-args = [x for x in args if x != "--pack"]
-src = args[0] if args else ("ffm_amd/csrc/core_pack.hip" if pack else "ffm_amd/csrc/core_step.hip")
-extra = args[1:] + (["-DFFM_PACK_MARKS"] if pack else [])
+src = args[0] if args else "ffm_amd/csrc/core_step.hip"
+extra = args[1:]
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                 "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only",
                 "-S", "-DFFM_MARKS", *extra, src, "-o", "/tmp/phase.s"], check=True, capture_output=True)
 s = open("/tmp/phase.s").read()
-name = ("_ZN3ffm16core_pack_kernelILi4ELi4ELi12ELi12EEEvNS_12CoreStepArgsE" if pack
-        else "_ZN3ffm16core_wave_kernelILi4ELb0ELi2ELi12ELi12EEEvNS_12CoreStepArgsE")
+name = "_ZN3ffm16core_wave_kernelILi4ELb0ELi2ELi12ELi12EEEvNS_12CoreStepArgsE"
 i = s.index(name + ":")
 body = s[i:s.index(".Lfunc_end", i)].splitlines()
 names = {0: "load/pp", 1: "marks", 2: "decide", 3: "rq write", 4: "resolve", 5: "compaction",
