@@ -326,7 +326,8 @@ def bench_learner(args, world, rank, torch, dist):
     if world > 1:
         # the ranks share V / H: every step exchanges the table deltas over RCCL
         from ffm_amd.dist import TableSync
-        sync = TableSync(L, device="cuda", capacity=1 << 17, sync_period=args.sync_period)
+        # hashed tables: record buffers sized from the measured touched counts
+        sync = TableSync(L, device="cuda", capacity=None, sync_period=args.sync_period)
         run = sync.step
     else:
         L.set_sync_period(args.sync_period)
@@ -334,7 +335,9 @@ def bench_learner(args, world, rank, torch, dist):
     run(args.warmup)
     torch.cuda.synchronize()
     print(f"[bench] config {args.config}: warmup done", file=sys.stderr, flush=True)
+    sent0 = sync.bytes_sent if world > 1 else 0
     reps = timed_repeats(args, world, dist, torch, lambda: run(args.steps), lambda: L.counters(stream))
+    sent_timed = (sync.bytes_sent - sent0) if world > 1 else 0
     elapsed, agent_steps = reps["elapsed"], reps["agent_steps"]
     print(f"[bench] timed regions {reps['summary']['elapsed_s']} s", file=sys.stderr, flush=True)
     nk = min(args.steps, 100)
@@ -377,9 +380,13 @@ def bench_learner(args, world, rank, torch, dist):
             "repeats": reps["summary"],
             "step_ms_events": step_ms,
             "tables": {"V": v_size, "H": h_size},
-            "table_sync": ({"period": args.sync_period, "mode": "dense all-reduce" if sync.dense else "records",
-                            "bytes_per_rank_per_step": sync.bytes_sent / max(1, args.warmup + reps["summary"]["n"]
-                                                                           * args.steps + nk)}
+            "table_sync": (dict({"period": args.sync_period,
+                                 "mode": "dense all-reduce" if sync.dense else "records (adaptive capacity)",
+                                 "bytes_per_rank_per_step": sent_timed / (reps["summary"]["n"] * args.steps),
+                                 "note": "bytes this rank contributes to the collectives per step, over the "
+                                         "timed regions"},
+                                **({} if sync.dense else {"record_capacity": dict(sync.caps),
+                                                          "max_touched_records": dict(sync.max_count)}))
                            if world > 1 else {"period": args.sync_period}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

@@ -162,7 +162,6 @@ void core_wave_kernel(CoreStepArgs a) {
     unsigned char* wbase = smem + wave_shared_bytes(PHW) + (size_t)wv * cv.per_wave;
     GT* grid = reinterpret_cast<GT*>(wbase + cv.grid);
     float* tile = reinterpret_cast<float*>(wbase + cv.dff);
-    uint16_t* sreq = reinterpret_cast<uint16_t*>(wbase + cv.req);
     uint16_t* snxt = reinterpret_cast<uint16_t*>(wbase + cv.nxt);
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
     uint16_t* spos = reinterpret_cast<uint16_t*>(wbase + cv.spos);

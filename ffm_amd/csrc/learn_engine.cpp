@@ -119,6 +119,7 @@ static void release(ffm_learner* l) {
 // dense_by > 0: ffm_unified's rank keys map injectively onto
 // ranks * (cap / 256) + bx * dense_by + by (learn_step.hip dense_slot); the capacity is
 // the next power of two >= 256 * Bx * By and the table can never fill.
+// width: values per record (V 1, H 5; H 9 with the Moore neighbourhood, MT step only).
 static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dense_by = 0, size_t dense_n = 0) {
     T.width = width;
     T.accw = width == 1 ? 2 : width;
@@ -132,7 +133,7 @@ static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dens
     T.t.dense_by = dense_by;
     T.t.limit = (uint32_t)(T.cap - T.cap / 8);
     hipError_t e;
-    T.t.stride = width == 1 ? 2 : 8;        // 16 B / 64 B records (key + values [+ pad])
+    T.t.stride = width == 1 ? 2 : width == 5 ? 8 : 10;   // 16 / 64 / 80 B records (key + values [+ pad])
     if ((e = hipMalloc((void**)&T.t.rec, T.cap * T.t.stride * 8)) != hipSuccess) return e;
     // hashed tables: copies of the accumulators (LearnTable::reps); FFM_ACC_REPS overrides
     // (they spread the adds of hot keys over several memory-side atomic units; a large
@@ -246,9 +247,10 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if ((long long)d.H * d.W == 65536 && (d.map[65535] == 0 || d.map[65535] == 3))
         return fail(FFM_E_UNSUPPORTED, "the last cell of a 65536-cell map must be blocked");
     if (d.neighborhood != 4 &&
-        !(d.neighborhood == 8 && d.variant == FFM_VARIANT_AC && d.rng_mode == FFM_RNG_MT))
-        return fail(FFM_E_UNSUPPORTED, "neighborhood 'moore' is built for ffm_ac_core in MT (reference-exact) mode "
-                                       "only; the other learning variants and the batched step use 'neumann'");
+        !(d.neighborhood == 8 && d.variant != FFM_VARIANT_TRAINED && d.rng_mode == FFM_RNG_MT))
+        return fail(FFM_E_UNSUPPORTED, "neighborhood 'moore' is built for the reference-exact (MT) step of ffm_ac_core, "
+                                       "ffm_unified and ffm_actor_only; the batched step and ffm_trained_core use "
+                                       "'neumann'");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
     // batched: LDS grid codes and placement sorts hold <= 16384 agents; the exact (MT) step
@@ -367,7 +369,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     l->dense_bx = dense_by ? (uint32_t)((H - 1) / learn->block_size + 1) : 0;
     l->V.t.alpha = l->L.alpha_v;   // the visit-averaged V update (learn_step.hip v_visits)
     if ((he = alloc_table(l->V, l->L.log2_v_capacity, 1, dense_by, dense_n)) != hipSuccess ||
-        (he = alloc_table(l->H, l->actor || l->trained ? l->L.log2_h_capacity : 8, 5,
+        (he = alloc_table(l->H, l->actor || l->trained ? l->L.log2_h_capacity : 8, d.neighborhood == 8 ? 9 : 5,
                           l->actor || l->trained ? dense_by : 0, dense_n)) != hipSuccess)
         return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);

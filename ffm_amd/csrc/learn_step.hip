@@ -392,129 +392,104 @@ __device__ __forceinline__ double np_max5(const double* s, int n) {
     return m;
 }
 
-__device__ __forceinline__ double sum_seq(const double* e, int n) {   // NumPy add.reduce, n < 8
-    double s = -0.0;
-    for (int k = 0; k < n; k++) s += e[k];
-    return s;
-}
-__device__ __forceinline__ float sum_seqf(const float* e, int n) {
-    float s = -0.0f;
-    for (int k = 0; k < n; k++) s += e[k];
-    return s;
-}
-
 struct HStat {
     int has, nonfinite;
     double mn, mx;
 };
 
 // Actor policy: model/ffm_unified.py:394-499 (compat = false) and
-// model/ffm_actor_only.py:241-340 (compat = true: invalid -> -inf -> uniform).
+// model/ffm_actor_only.py:241-340 (compat = true: invalid -> -inf -> uniform), over the
+// NA = |neighbours| + 1 moves (stay last; Moore: 9, and add.reduce pairs 8+ terms).
+// The exact (one-lane) kernel's; the batched step uses actor_policy.
 template <class R>
 __device__ int actor_choose(const LearnArgs& a, const double* hrow, const int* coord, const int* valid,
-                            const float* dff, const HStat& hs, bool compat, R& rng) {
-    double h[5], score[5], e[5], p[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = hrow[k];
+                            const float* dff, const HStat& hs, bool compat, int NA, R& rng) {
+    double h[9], score[9], e[9], p[9];
+    for (int k = 0; k < NA; k++) h[k] = hrow[k];
     if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
         const double smin = (double)a.smin, smax = (double)a.smax;
-#pragma unroll
-        for (int k = 0; k < 5; k++) h[k] = ((hs.mx - h[k]) / (hs.mx - hs.mn)) * (smax - smin) + smin;
+        for (int k = 0; k < NA; k++) h[k] = ((hs.mx - h[k]) / (hs.mx - hs.mn)) * (smax - smin) + smin;
     }
     bool bad = false;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const float d = a.kD32 * dff[coord[k]];
         score[k] = a.nkA * h[k] + (double)d;
         if (compat && !valid[k]) score[k] = -__builtin_inf();
         bad = bad || !__builtin_isfinite(score[k]);
     }
-    if (bad) {
-#pragma unroll
-        for (int k = 0; k < 5; k++) score[k] = valid[k] ? 1.0 : 0.0;
-    }
+    if (bad)
+        for (int k = 0; k < NA; k++) score[k] = valid[k] ? 1.0 : 0.0;
     double mx;
     if (compat) {
-        double vs[5];
+        double vs[9];
         int nv = 0;
-        for (int k = 0; k < 5; k++)
+        for (int k = 0; k < NA; k++)
             if (valid[k]) vs[nv++] = score[k];
         mx = nv ? np_max5(vs, nv) : 0.0;
     } else {
-        mx = np_max5(score, 5);
+        mx = np_max5(score, NA);
     }
-    int nvalid = 0, vidx[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
+    int nvalid = 0, vidx[9];
+    for (int k = 0; k < NA; k++) {
         e[k] = valid[k] ? det_exp(score[k] - mx) : 0.0;
         if (valid[k]) vidx[nvalid++] = k;
     }
-    const double sum = sum_seq(e, 5);
+    const double sum = np_sum_n(e, NA);
     if (__builtin_isfinite(sum) && sum > 0) {
-#pragma unroll
-        for (int k = 0; k < 5; k++) p[k] = e[k] / sum;
+        for (int k = 0; k < NA; k++) p[k] = e[k] / sum;
     } else {
-#pragma unroll
-        for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
+        for (int k = 0; k < NA; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
     }
     if (a.epsilon > 0 && rng.coin() < a.epsilon) {
         if (nvalid > 0) return vidx[rng.randint((uint32_t)nvalid)];
-        return 4;
+        return NA - 1;
     }
-    return choice_cdf(p, 5, rng.u());
+    return choice_cdf(p, NA, rng.u());
 }
 
-// Critic-only policy of ffm_unified (:353-392): raw SFF over all five moves.
+// Critic-only policy of ffm_unified (:353-392): raw SFF over all NA moves.
 template <class R>
-__device__ int critic_choose(const LearnArgs& a, const int* coord, const int* valid, const float* dff, R& rng) {
-    double p[5];
+__device__ int critic_choose(const LearnArgs& a, const int* coord, const int* valid, const float* dff, int NA,
+                             R& rng) {
+    double p[9];
     int nvalid = 0;
-#pragma unroll
-    for (int k = 0; k < 5; k++) nvalid += valid[k];
+    for (int k = 0; k < NA; k++) nvalid += valid[k];
     if (a.sff32) {
-        float s[5], e[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
+        float s[9], e[9];
+        for (int k = 0; k < NA; k++) {
             const float x = a.kS32 * a.sff32[coord[k]];
             const float y = a.kD32 * dff[coord[k]];
             s[k] = x + y;
         }
         float mx = s[0];
-        for (int k = 1; k < 5; k++) {
+        for (int k = 1; k < NA; k++) {
             if (s[k] != s[k]) { mx = s[k]; break; }
             mx = s[k] > mx ? s[k] : mx;
         }
-#pragma unroll
-        for (int k = 0; k < 5; k++) e[k] = valid[k] ? np_expf(s[k] - mx) : 0.0f;
-        const float sum = sum_seqf(e, 5);
+        for (int k = 0; k < NA; k++) e[k] = valid[k] ? np_expf(s[k] - mx) : 0.0f;
+        const float sum = np_sum_n(e, NA);
         if (__builtin_isfinite(sum) && sum > 0) {
-#pragma unroll
-            for (int k = 0; k < 5; k++) p[k] = (double)(e[k] / sum);
+            for (int k = 0; k < NA; k++) p[k] = (double)(e[k] / sum);
         } else {
             const float u = (float)(1.0 / (double)nvalid);
-#pragma unroll
-            for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)u : 0.0;
+            for (int k = 0; k < NA; k++) p[k] = valid[k] ? (double)u : 0.0;
         }
     } else {
-        double s[5], e[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
+        double s[9], e[9];
+        for (int k = 0; k < NA; k++) {
             const float y = a.kD32 * dff[coord[k]];
             s[k] = a.kS64 * a.sff64[coord[k]] + (double)y;
         }
-        const double mx = np_max5(s, 5);
-#pragma unroll
-        for (int k = 0; k < 5; k++) e[k] = valid[k] ? det_exp(s[k] - mx) : 0.0;
-        const double sum = sum_seq(e, 5);
+        const double mx = np_max5(s, NA);
+        for (int k = 0; k < NA; k++) e[k] = valid[k] ? det_exp(s[k] - mx) : 0.0;
+        const double sum = np_sum_n(e, NA);
         if (__builtin_isfinite(sum) && sum > 0) {
-#pragma unroll
-            for (int k = 0; k < 5; k++) p[k] = e[k] / sum;
+            for (int k = 0; k < NA; k++) p[k] = e[k] / sum;
         } else {
-#pragma unroll
-            for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
+            for (int k = 0; k < NA; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
         }
     }
-    return choice_cdf(p, 5, rng.u());
+    return choice_cdf(p, NA, rng.u());
 }
 
 // ffm_ac_core decide == ffm_core decide (model/ffm_ac_core.py:126-199).
@@ -580,6 +555,22 @@ __device__ __forceinline__ void moves5(const LearnArgs& a, int x, int y, const O
     valid[4] = 1;
 }
 
+// The exact kernel's moves: the a.nb neighbours in get_neighbors order (Neumann U, D,
+// L, R; Moore row-major, model/ffm_unified.py:173-185), then stay, with the validity mask.
+template <class OCC>
+__device__ void moves_n(const LearnArgs& a, int x, int y, const OCC& occ, int* coord, int* valid, int* inb) {
+    const int nb = a.nb;
+    for (int k = 0; k <= nb; k++) {
+        const int dx = k == nb ? 0 : (nb == 8 ? kMBx[k] : kNBx[k]), dy = k == nb ? 0 : (nb == 8 ? kMBy[k] : kNBy[k]);
+        const int nx = x + dx, ny = y + dy;
+        inb[k] = nx >= 0 && nx < a.H && ny >= 0 && ny < a.W;
+        coord[k] = inb[k] ? nx * a.W + ny : x * a.W + y;
+        const int m = inb[k] ? a.map[coord[k]] : 2;
+        valid[k] = inb[k] && (m == 0 || m == 3) && (k == nb || !occ(coord[k]));
+    }
+    valid[nb] = 1;
+}
+
 __device__ void update_dff_seq(const LearnArgs& a, float* dff, float* B) {
     const int H = a.H, W = a.W, HW = a.HW;
     for (int i = 0; i < HW; i++) B[i] = a.c0 * dff[i];
@@ -602,9 +593,10 @@ __device__ void h_stats_seq(const LearnArgs& a, HStat& hs) {
     hs.nonfinite = 0;
     hs.mn = __builtin_inf();
     hs.mx = -__builtin_inf();
+    const int w = (int)a.Ht.accw;   // H rows: 5 values, 9 with the Moore neighbourhood
     for (uint32_t i = 0; i < n; i++) {
         const double* v = tval(a.Ht, a.Ht.order[i]);
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < w; k++) {
             if (!__builtin_isfinite(v[k])) hs.nonfinite = 1;
             hs.mn = v[k] < hs.mn ? v[k] : hs.mn;
             hs.mx = v[k] > hs.mx ? v[k] : hs.mx;
@@ -884,7 +876,7 @@ __host__ __device__ inline size_t exact_carve(unsigned char* base, int HW, int A
         o += (bytes + 15) & ~(size_t)15;
         return p;
     };
-    const size_t R = (size_t)A * 4 + 1;
+    const size_t R = (size_t)A * 8 + 1;   // requests: ffm_actor_only makes one per neighbour (Moore: 8)
     ExactScratch t;
     t.occ = (int*)take((size_t)HW * 4);
     t.rq_tgt = (int*)take(R * 4);
@@ -942,11 +934,12 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                 if (T >= 0) { S.rq_tgt[nrq] = T; S.rq_agent[nrq++] = i; }
                 continue;
             }
-            int coord[5], valid[5], inb[5];
-            moves5(a, x, y, occ, coord, valid, inb);
+            int coord[9], valid[9], inb[9];
+            const int nb = a.nb, NA = nb + 1;
+            moves_n(a, x, y, occ, coord, valid, inb);
             if (trained) {                                    // model/ffm_trained_core.py:169-258
                 int k = -1;
-                for (int j = 0; j < 4; j++)
+                for (int j = 0; j < nb; j++)
                     if (inb[j] && a.map[coord[j]] == 3) { k = j; break; }
                 if (k < 0) {
                     Policy P;
@@ -960,14 +953,14 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
             }
             if (a.variant == kVarUnified) {
                 int ex = -1;
-                for (int k = 0; k < 4; k++)
+                for (int k = 0; k < nb; k++)
                     if (inb[k] && a.map[coord[k]] == 3) { ex = k; break; }
                 int k;
                 if (ex >= 0) {
                     S.wexit[i] = 1;
                     k = ex;
                 } else if (!actor) {
-                    k = critic_choose(a, coord, valid, dff, rng);
+                    k = critic_choose(a, coord, valid, dff, NA, rng);
                 } else {
                     const uint32_t before = *a.Ht.n;
                     const int hsl = tab_get(a.Ht, S.skey[i], a.overflow);
@@ -977,14 +970,14 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                         hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
                         hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
                     }
-                    k = actor_choose(a, tval(a.Ht, hsl), coord, valid, dff, hs, false, rng);
+                    k = actor_choose(a, tval(a.Ht, hsl), coord, valid, dff, hs, false, NA, rng);
                 }
                 S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
                 S.act[i] = k; S.avalid[i] = valid[k];
             } else {
                 // ffm_actor_only: exit test and decision inside the neighbour loop (:214-355)
                 int ex = -1;
-                for (int j = 0; j < 4; j++) {
+                for (int j = 0; j < nb; j++) {
                     if (ex < 0 && inb[j] && a.map[coord[j]] == 3) ex = j;
                     int k;
                     if (ex >= 0) {
@@ -999,7 +992,7 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                             hs.mn = 0.0 < hs.mn ? 0.0 : hs.mn;
                             hs.mx = 0.0 > hs.mx ? 0.0 : hs.mx;
                         }
-                        k = actor_choose(a, tval(a.Ht, hsl), coord, valid, dff, hs, true, rng);
+                        k = actor_choose(a, tval(a.Ht, hsl), coord, valid, dff, hs, true, NA, rng);
                     }
                     S.rq_tgt[nrq] = coord[k]; S.rq_agent[nrq++] = i;
                     S.act[i] = k; S.avalid[i] = valid[k];

@@ -74,8 +74,17 @@ class TableSync:
     get_h_table -- differs between ranks).
 
     No host synchronisation inside the step loop: the record counts stay on the
-    device (fixed-capacity record buffers, ``capacity`` records per rank and table;
-    a step that touches more is reported as an error at the next sync point).
+    device (fixed-capacity record buffers; a step that touches more entries than the
+    capacity is reported as an error at the next sync point, never silently).
+
+    * record capacity: ``capacity`` records per rank and table; ``capacity=None``
+      sizes it from the touched counts actually measured: every rank copies the
+      all-gathered counts (identical on every rank) to pinned host memory behind the
+      exchange, and every ``adapt_every`` exchanges the capacity becomes
+      ``headroom`` x the largest count of the last window (a power of two in
+      [1,024, ``max_capacity``]).  The window lags ``lag`` exchanges behind the
+      host, whose copies it waits for (a bounded queue depth, not a sync), so
+      every rank decides on the same numbers at the same exchange.
 
     * ``dense`` (default: the shard's tables are dense, i.e. ffm_unified): the whole
       fixed-point accumulator array is all-reduced (SUM; RCCL runs it as
@@ -86,14 +95,24 @@ class TableSync:
       (``Learner.set_sync_period``); K = 1 is the reference's per-step update.
     """
 
-    def __init__(self, shard, group=None, device=None, capacity: int = 1 << 16, sync_period: int = 1,
-                 dense: bool | None = None):
+    def __init__(self, shard, group=None, device=None, capacity: int | None = 1 << 16, sync_period: int = 1,
+                 dense: bool | None = None, max_capacity: int = 1 << 20, headroom: float = 2.0,
+                 adapt_every: int = 16, lag: int = 8):
         self.shard = shard
         self.group = group
         self.device = device
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.capacity = int(capacity)
+        self.adaptive = capacity is None
+        self.max_capacity = int(max_capacity)
+        self.headroom = float(headroom)
+        self.adapt_every, self.lag = int(adapt_every), int(lag)
+        # adaptive: start generous (the first window measures), then follow the counts
+        self.caps = {w: (min(1 << 17, self.max_capacity) if capacity is None else int(capacity)) for w in ("V", "H")}
+        self.capacity = max(self.caps.values())
+        self.seen = {"V": [], "H": []}      # (event, pinned gathered counts) per exchange
+        self.n_ex = {"V": 0, "H": 0}
+        self.max_count = {"V": 0, "H": 0}   # largest touched count observed (reported)
         self.sync_period = int(sync_period)
         shard.set_sync_period(self.sync_period)
         self.dense = bool(getattr(shard, "dense_tables", False)) if dense is None else bool(dense)
@@ -103,8 +122,8 @@ class TableSync:
 
     def _record_buffers(self, which: str):
         b = self.bufs.get(which)
-        if b is None:
-            width, cap, w, dev = (2 if which == "V" else 5), self.capacity, self.world, self.device
+        if b is None or b[0].shape[0] != self.caps[which]:
+            width, cap, w, dev = (2 if which == "V" else 5), self.caps[which], self.world, self.device
             b = (torch.zeros(cap, dtype=torch.int64, device=dev),
                  torch.zeros((cap, width), dtype=torch.int64, device=dev),
                  torch.zeros(1, dtype=torch.int64, device=dev),
@@ -125,6 +144,37 @@ class TableSync:
             if r != self.rank:
                 self.shard.delta_merge_async(which, gk[r].data_ptr(), ga[r].data_ptr(), gc[r:r + 1].data_ptr(), cap)
         self.bytes_sent += 8 + keys.numel() * 8 + acc.numel() * 8
+        if self.adaptive:
+            self._observe(which, gc)
+
+    def _observe(self, which: str, gc):
+        """Queue a copy of the gathered counts; every adapt_every exchanges resize the
+        record buffers from the counts of the window that ended `lag` exchanges ago."""
+        host = torch.empty(gc.shape, dtype=gc.dtype, pin_memory=gc.is_cuda)
+        host.copy_(gc, non_blocking=True)
+        ev = None
+        if gc.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        seen = self.seen[which]
+        seen.append((ev, host))
+        self.n_ex[which] += 1
+        i = self.n_ex[which]
+        if i % self.adapt_every or len(seen) <= self.lag:
+            return
+        window = seen[: len(seen) - self.lag]
+        del seen[: len(seen) - self.lag]
+        m = 0
+        for e, h in window:
+            if e is not None:
+                e.synchronize()             # an exchange `lag` steps back: already done
+            m = max(m, int(h.max()))
+        self.max_count[which] = max(self.max_count[which], m)
+        cap = 1024
+        while cap < self.headroom * m and cap < self.max_capacity:
+            cap *= 2
+        self.caps[which] = cap
+        self.capacity = max(self.caps.values())
 
     def _exchange_dense(self, which: str):
         acc, present = self.shard.dense_buffers(which)

@@ -484,6 +484,8 @@ class Learner:
         d.H, d.W = self.H, self.W
         d.map, d.sff, d.sff_dtype = self.map.ctypes.data, self.sff.ctypes.data, sdt
         d.neighborhood = 4 if p.get("neighborhood", "neumann") == "neumann" else 8
+        # H rows: one value per move (the neighbours, then stay)
+        self.n_actions = d.neighborhood + 1
         d.k_S, d.k_D = float(p.get("k_S", 0.0)), float(p["k_D"])
         d.diffuse, d.decay = float(p["diffuse"]), float(p["decay"])
         d.n_envs, d.agent_capacity, d.n_agents = self.n_envs, self.A, self.n_agents
@@ -692,9 +694,9 @@ class Learner:
         return int(n.value)
 
     def export_table(self, which: str = "V", stream=None):
-        """(keys u64 [n], values f64 [n] or [n, 5]) in insertion order."""
+        """(keys u64 [n], values f64 [n] or [n, n_actions]) in insertion order."""
         w = TABLE_V if which == "V" else TABLE_H
-        width = 1 if w == TABLE_V else 5
+        width = 1 if w == TABLE_V else self.n_actions
         cap = self.table_size(which, stream)
         keys = np.empty(max(cap, 1), np.uint64)
         vals = np.empty((max(cap, 1), width), np.float64)
@@ -706,7 +708,7 @@ class Learner:
 
     def import_table(self, which: str, keys, vals, stream=None):
         w = TABLE_V if which == "V" else TABLE_H
-        width = 1 if w == TABLE_V else 5
+        width = 1 if w == TABLE_V else self.n_actions
         k = np.ascontiguousarray(keys, dtype=np.uint64)
         v = np.ascontiguousarray(vals, dtype=np.float64).reshape(len(k), width)
         _check(self._L.ffm_learner_import_table(self._h, w, _ptr(k), _ptr(v), len(k), _stream_handle(stream)))

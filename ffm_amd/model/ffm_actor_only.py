@@ -87,7 +87,7 @@ class FloorFieldModelActorOnly(LearnModel):
     def get_h_table_size(self):
         """:603-611"""
         n = self._learner.table_size("H")
-        return (n, 5 * n)
+        return (n, self._learner.n_actions * n)
 
     @property
     def V(self):

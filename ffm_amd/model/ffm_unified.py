@@ -126,7 +126,7 @@ class FloorFieldModelUnified(LearnModel):
         """:869-880"""
         if self.learning_mode in ["actor_only", "both"]:
             n = self._learner.table_size("H")
-            return (n, 5 * n)
+            return (n, self._learner.n_actions * n)
         return None
 
     @property

@@ -17,7 +17,6 @@
 
 #define EMPTY_KEY (~(uint64_t)0)
 #define FX_ONE 4294967296.0            /* 2^32: fixed-point scale of batched increments */
-#define MAXR 4                         /* decisions per agent (ffm_actor_only inner loop) */
 
 static const int NB[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};   /* U, D, L, R: model/ffm_unified.py:174-175 */
 /* Moore order of ffm_ac_core.get_neighbors (model/ffm_ac_core.py:51-60) */
@@ -414,7 +413,7 @@ static int choice_cdf(const double* p, int n, double u) {
 
 /* H row of state s, inserting zeros (model/ffm_unified.py:405-410). */
 static int64_t h_row(lctx* L, uint64_t s) {
-    static const double zeros[5] = {0, 0, 0, 0, 0};
+    static const double zeros[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t before = L->Ht->n;
     int64_t slot = tab_get_sync(L->Ht, s, zeros, L->parallel);
     if (!L->jacobi && L->Ht->n > before) {      /* a zero row joins the min/max (:414-423) */
@@ -425,99 +424,100 @@ static int64_t h_row(lctx* L, uint64_t s) {
     return slot;
 }
 
-/* Actor policy (model/ffm_unified.py:394-499, model/ffm_actor_only.py:241-340).
+/* Actor policy (model/ffm_unified.py:394-499, model/ffm_actor_only.py:241-340) over the
+ * NA = |neighbours| + 1 moves (stay last; Moore: 9, add.reduce pairs 8+ terms).
  * compat = ffm_actor_only's masking (invalid -> -inf -> uniform). */
 static int actor_choose(lctx* L, int64_t hslot, const int32_t* coord, const int* valid, const float* dff,
-                        int compat) {
+                        int compat, int NA) {
     const ffo_learn_cfg* c = L->c;
-    double h[5], score[5], e[5], p[5];
-    memcpy(h, L->Ht->vals + hslot * 5, sizeof h);
+    double h[9], score[9], e[9], p[9];
+    memcpy(h, L->Ht->vals + hslot * L->Ht->width, sizeof(double) * (size_t)NA);
     if (L->hs.has && !L->hs.nonfinite && L->hs.mx - L->hs.mn > 1e-6) {
         const double smin = (double)L->smin, smax = (double)L->smax;
-        for (int k = 0; k < 5; k++) h[k] = ((L->hs.mx - h[k]) / (L->hs.mx - L->hs.mn)) * (smax - smin) + smin;
+        for (int k = 0; k < NA; k++) h[k] = ((L->hs.mx - h[k]) / (L->hs.mx - L->hs.mn)) * (smax - smin) + smin;
     }
     const float kD = (float)c->k_D;
     const double nkA = -c->k_A;
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const float d = kD * dff[coord[k]];
         score[k] = nkA * h[k] + (double)d;
     }
     if (compat)
-        for (int k = 0; k < 5; k++)
+        for (int k = 0; k < NA; k++)
             if (!valid[k]) score[k] = -INFINITY;                    /* actor_only.py:291 */
     int bad = 0;
-    for (int k = 0; k < 5; k++) if (!isfinite(score[k])) bad = 1;
+    for (int k = 0; k < NA; k++) if (!isfinite(score[k])) bad = 1;
     if (bad)
-        for (int k = 0; k < 5; k++) score[k] = valid[k] ? 1.0 : 0.0;
+        for (int k = 0; k < NA; k++) score[k] = valid[k] ? 1.0 : 0.0;
     double mx;
     if (compat) {
-        double vs[5]; int nv = 0;
-        for (int k = 0; k < 5; k++) if (valid[k]) vs[nv++] = score[k];
+        double vs[9]; int nv = 0;
+        for (int k = 0; k < NA; k++) if (valid[k]) vs[nv++] = score[k];
         mx = nv ? np_max(vs, nv) : 0.0;
     } else {
-        mx = np_max(score, 5);
+        mx = np_max(score, NA);
     }
-    for (int k = 0; k < 5; k++) e[k] = valid[k] ? ffo_det_exp(score[k] - mx) : 0.0;
-    const double sum = ffo_np_sumd(e, 5);
-    int nvalid = 0, vidx[5];
-    for (int k = 0; k < 5; k++) if (valid[k]) vidx[nvalid++] = k;
+    for (int k = 0; k < NA; k++) e[k] = valid[k] ? ffo_det_exp(score[k] - mx) : 0.0;
+    const double sum = ffo_np_sumd(e, NA);
+    int nvalid = 0, vidx[9];
+    for (int k = 0; k < NA; k++) if (valid[k]) vidx[nvalid++] = k;
     if (isfinite(sum) && sum > 0) {
-        for (int k = 0; k < 5; k++) p[k] = e[k] / sum;
+        for (int k = 0; k < NA; k++) p[k] = e[k] / sum;
     } else {
-        for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
+        for (int k = 0; k < NA; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
     }
     if (L->eps > 0 && dec_coin(&L->rng) < L->eps) {                  /* :478-495 */
         if (nvalid > 0) return vidx[dec_randint(&L->rng, (uint32_t)nvalid)];
-        return 4;
+        return NA - 1;
     }
-    return choice_cdf(p, 5, dec_u53(&L->rng));
+    return choice_cdf(p, NA, dec_u53(&L->rng));
 }
 
-/* Critic-only policy of ffm_unified (:353-392): raw SFF over all 5. */
-static int critic_choose(lctx* L, const int32_t* coord, const int* valid, const float* dff) {
+/* Critic-only policy of ffm_unified (:353-392): raw SFF over all NA moves. */
+static int critic_choose(lctx* L, const int32_t* coord, const int* valid, const float* dff, int NA) {
     const ffo_learn_cfg* c = L->c;
-    double p[5];
+    double p[9];
     int nvalid = 0;
-    for (int k = 0; k < 5; k++) nvalid += valid[k];
+    for (int k = 0; k < NA; k++) nvalid += valid[k];
     if (c->sff32) {
         const float kS = (float)(-c->k_S), kD = (float)c->k_D;
-        float s[5], e[5];
-        for (int k = 0; k < 5; k++) {
+        float s[9], e[9];
+        for (int k = 0; k < NA; k++) {
             const float a = kS * c->sff32[coord[k]];
             const float b = kD * dff[coord[k]];
             s[k] = a + b;
         }
         float mx = s[0];
-        for (int k = 1; k < 5; k++) {
+        for (int k = 1; k < NA; k++) {
             if (s[k] != s[k]) { mx = s[k]; break; }
             mx = s[k] > mx ? s[k] : mx;
         }
-        for (int k = 0; k < 5; k++) e[k] = valid[k] ? ffo_np_expf(s[k] - mx) : 0.0f;
-        const float sum = ffo_np_sumf(e, 5);
+        for (int k = 0; k < NA; k++) e[k] = valid[k] ? ffo_np_expf(s[k] - mx) : 0.0f;
+        const float sum = ffo_np_sumf(e, NA);
         if (isfinite(sum) && sum > 0) {
-            for (int k = 0; k < 5; k++) p[k] = (double)(e[k] / sum);
+            for (int k = 0; k < NA; k++) p[k] = (double)(e[k] / sum);
         } else {
             const float u = (float)(1.0 / (double)nvalid);
-            for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)u : 0.0;
+            for (int k = 0; k < NA; k++) p[k] = valid[k] ? (double)u : 0.0;
         }
     } else {
         const double kS = -c->k_S;
         const float kD = (float)c->k_D;
-        double s[5], e[5];
-        for (int k = 0; k < 5; k++) {
+        double s[9], e[9];
+        for (int k = 0; k < NA; k++) {
             const float b = kD * dff[coord[k]];
             s[k] = kS * c->sff64[coord[k]] + (double)b;
         }
-        const double mx = np_max(s, 5);
-        for (int k = 0; k < 5; k++) e[k] = valid[k] ? ffo_det_exp(s[k] - mx) : 0.0;
-        const double sum = ffo_np_sumd(e, 5);
+        const double mx = np_max(s, NA);
+        for (int k = 0; k < NA; k++) e[k] = valid[k] ? ffo_det_exp(s[k] - mx) : 0.0;
+        const double sum = ffo_np_sumd(e, NA);
         if (isfinite(sum) && sum > 0) {
-            for (int k = 0; k < 5; k++) p[k] = e[k] / sum;
+            for (int k = 0; k < NA; k++) p[k] = e[k] / sum;
         } else {
-            for (int k = 0; k < 5; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
+            for (int k = 0; k < NA; k++) p[k] = valid[k] ? 1.0 / (double)nvalid : 0.0;
         }
     }
-    return choice_cdf(p, 5, dec_u53(&L->rng));
+    return choice_cdf(p, NA, dec_u53(&L->rng));
 }
 
 /* ffm_trained_core policy (model/ffm_trained_core.py:219-300): H row (float32;
@@ -650,7 +650,10 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
     const ffo_learn_cfg* c = L->c;
     const int H = c->H, W = c->W, HW = H * W;
     const int n = *n_io;
-    const int D = c->variant == FFO_VAR_ACTOR_ONLY ? MAXR : 1;
+    const int nb = cfg_nb(c), NA = nb + 1;      /* moves: the neighbours in order, then stay */
+    /* ffm_actor_only's inner-loop quirk: one decision per neighbour (4, Moore 8) */
+    const int D = c->variant == FFO_VAR_ACTOR_ONLY ? nb : 1;
+    const int hw = L->Ht ? L->Ht->width : 5;
     const int actor = c->variant == FFO_VAR_ACTOR_ONLY ||
                       (c->variant == FFO_VAR_UNIFIED && c->mode != FFO_MODE_CRITIC);
     int32_t* rq_tgt = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n * D + 1));
@@ -679,16 +682,16 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
             if (T >= 0) { rq_tgt[nrq] = T; rq_agent[nrq++] = i; }
             continue;
         }
-        int32_t coord[5];
-        int valid[5], inb[5];
-        for (int k = 0; k < 5; k++) {
-            const int nx = k < 4 ? x + NB[k][0] : x, ny = k < 4 ? y + NB[k][1] : y;
+        int32_t coord[9];
+        int valid[9], inb[9];
+        for (int k = 0; k < NA; k++) {
+            const int nx = k < nb ? x + nbx(nb, k) : x, ny = k < nb ? y + nby(nb, k) : y;
             inb[k] = nx >= 0 && nx < H && ny >= 0 && ny < W;
             coord[k] = inb[k] ? nx * W + ny : pos[i];
             const uint8_t m = inb[k] ? c->map[coord[k]] : 2;
-            valid[k] = inb[k] && (m == 0 || m == 3) && (k == 4 || occ[coord[k]] < 0);
+            valid[k] = inb[k] && (m == 0 || m == 3) && (k == nb || occ[coord[k]] < 0);
         }
-        valid[4] = 1;
+        valid[nb] = 1;
         if (c->variant == FFO_VAR_TRAINED) {            /* model/ffm_trained_core.py:169-258 */
             dec_begin(&L->rng, (uint32_t)i);
             int ex = -1;
@@ -703,18 +706,18 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
         if (c->variant == FFO_VAR_UNIFIED) {
             dec_begin(&L->rng, (uint32_t)i);
             int ex = -1;
-            for (int k = 0; k < 4; k++)
+            for (int k = 0; k < nb; k++)
                 if (inb[k] && c->map[coord[k]] == 3) { ex = k; break; }   /* :326-334 */
             int k;
             if (ex >= 0) {
                 wexit[i] = 1;
                 k = ex;
             } else if (!actor) {
-                k = critic_choose(L, coord, valid, dff);
+                k = critic_choose(L, coord, valid, dff, NA);
             } else {
                 const int64_t hs = h_row(L, skey[i]);
                 if (hs < 0) { rc = -1; goto out; }
-                k = actor_choose(L, hs, coord, valid, dff, 0);
+                k = actor_choose(L, hs, coord, valid, dff, 0, NA);
             }
             rq_tgt[nrq] = coord[k]; rq_agent[nrq++] = i;
             act[i] = k; avalid[i] = valid[k];
@@ -723,17 +726,17 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
              * neighbour loop (model/ffm_actor_only.py:214-355): up to four
              * decisions and requests per agent, the last one recorded. */
             int ex = -1;
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < nb; j++) {
                 if (ex < 0 && inb[j] && c->map[coord[j]] == 3) ex = j;
                 int k;
                 if (ex >= 0) {
                     wexit[i] = 1;
                     k = ex;
                 } else {
-                    dec_begin(&L->rng, (uint32_t)(i * MAXR + j));
+                    dec_begin(&L->rng, (uint32_t)(i * D + j));
                     const int64_t hs = h_row(L, skey[i]);
                     if (hs < 0) { rc = -1; goto out; }
-                    k = actor_choose(L, hs, coord, valid, dff, 1);
+                    k = actor_choose(L, hs, coord, valid, dff, 1, NA);
                 }
                 rq_tgt[nrq] = coord[k]; rq_agent[nrq++] = i;
                 act[i] = k; avalid[i] = valid[k];
@@ -754,7 +757,7 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
             /* owner seq for the Philox stream: agent*4 + decision index for
              * ffm_actor_only (every agent makes exactly four requests, so that
              * is q itself), the agent index otherwise */
-            const uint32_t owner_seq = (uint32_t)(D == MAXR ? q : rq_agent[q]);
+            const uint32_t owner_seq = (uint32_t)(c->variant == FFO_VAR_ACTOR_ONLY ? q : rq_agent[q]);
             int w;
             if (m == 1) {
                 w = list[0];
@@ -819,7 +822,7 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
             }
         }
         if (actor) {
-            static const double zeros[5] = {0, 0, 0, 0, 0};
+            static const double zeros[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             for (int i = 0; i < n; i++) {
                 if (act[i] < 0) continue;
                 const int64_t hs = tab_get_sync(L->Ht, skey[i], zeros, L->parallel);   /* :769-773 */
@@ -827,9 +830,9 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
                 if (rec) { rec[i].hslot = (int32_t)hs; rec[i].k = act[i]; rec[i].valid = avalid[i]; }
                 if (!avalid[i]) continue;
                 if (!L->jacobi) {
-                    L->Ht->vals[hs * 5 + act[i]] = L->Ht->vals[hs * 5 + act[i]] + c->alpha_h * td[i];
+                    L->Ht->vals[hs * hw + act[i]] = L->Ht->vals[hs * hw + act[i]] + c->alpha_h * td[i];
                 } else if (!post_update) {
-                    __atomic_fetch_add(&L->Ht->acc[hs * 5 + act[i]], fx(c->alpha_h * td[i]), __ATOMIC_RELAXED);
+                    __atomic_fetch_add(&L->Ht->acc[hs * hw + act[i]], fx(c->alpha_h * td[i]), __ATOMIC_RELAXED);
                 }
             }
         }

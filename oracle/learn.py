@@ -140,7 +140,10 @@ class Learn:
         self.sff64 = None if self.sff32 is not None else np.ascontiguousarray(sff, np.float64)
         self.H, self.W = self.map.shape
         self.V = Table(1, log2_cap)
-        self.Ht = Table(5, log2_cap)
+        # H rows: one value per move (neighbours + stay): 5, or 9 with the Moore neighbourhood
+        moore = p.get("neighborhood", "neumann") == "moore"
+        self.n_actions = 9 if moore and variant in ("unified", "actor_only") else 5
+        self.Ht = Table(self.n_actions, log2_cap)
         self.cfg = LearnCfg(
             self.H, self.W, self.map.ctypes.data,
             self.sff32.ctypes.data if self.sff32 is not None else None,

@@ -125,7 +125,8 @@ def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1, sync_period=1
             cat(lambda x: x.ep_steps), sorted_tables(learns[0])), [sorted_tables(L) for L in learns]
 
 
-def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_period=1, steps=LEARN_STEPS):
+def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_period=1, steps=LEARN_STEPS,
+                 adaptive=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -135,7 +136,10 @@ def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_peri
         base, n = shard_range(n_global, rank, world)
         L = LO.Learn(m, s, variant, mode, learn_params(variant), log2_cap=20)
         shard = LO.Shard(L, n, LEARN_N, LEARN_N, SEED, base, LEARN_MAX)
-        sync = TableSync(shard, device="cpu", capacity=8192, sync_period=sync_period)
+        if adaptive:   # record capacity sized from the measured touched counts
+            sync = TableSync(shard, device="cpu", capacity=None, sync_period=sync_period, adapt_every=4, lag=2)
+        else:
+            sync = TableSync(shard, device="cpu", capacity=8192, sync_period=sync_period)
         sync.step(steps)
         assert sync.exchanges > 0
         parts = {}
@@ -151,6 +155,8 @@ def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_peri
             for r in range(1, world):      # every rank ends with the same tables
                 for k, v in tabs[r].items():
                     summ[f"r{r}_{k}"] = v
+            summ["caps"] = np.array([sync.caps["V"], sync.caps["H"]])
+            summ["max_count"] = np.array([sync.max_count["V"], sync.max_count["H"]])
             np.savez(out_path, **summ)
     finally:
         dist.destroy_process_group()

@@ -115,7 +115,8 @@ def run_case(name, variant, cls, map_array, sff, params, N, seeds, n_ep, max_ste
         nsteps=np.asarray(nsteps, np.int32), counts=np.asarray(counts, cdt),
         cells=np.asarray(cells, cdt), dff_hash=np.asarray(hashes, np.uint64),
         v_keys=np.asarray(vk, np.uint64), v_vals=np.asarray(vv, np.float64), v_n=np.asarray(vn, np.int64),
-        h_keys=np.asarray(hk, np.uint64), h_vals=np.asarray(hv, np.float64).reshape(-1, 5),
+        h_keys=np.asarray(hk, np.uint64),
+        h_vals=np.asarray(hv, np.float64).reshape(-1, 9 if params.get("neighborhood") == "moore" else 5),
         h_n=np.asarray(hn, np.int64), np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
     )
     if pretrained is not None:
@@ -230,6 +231,18 @@ def main():
     run_case("actoronly_12x12_N16", "actor_only", AO, m12, s12, ao_p, 16, [12, 13], 4, 300,
              eps_sched=eps)
     run_case("actoronly_12x12_N32_eps0", "actor_only", AO, m12, s12, ao_p, 32, [14], 2, 300)
+    # the Moore neighbourhood (model/ffm_unified.py:173-185, model/ffm_actor_only.py:87-93):
+    # nine moves, 9-value H rows, 8-term update_dff; ffm_actor_only's inner loop then
+    # makes up to eight decisions per agent
+    mo = {"neighborhood": "moore"}
+    run_case("unified_moore_critic_12x12_N16", "unified", UNI, m12, s12, dict(uni_p, **mo), 16, [23, 24], 3, 300,
+             mode="critic_only")
+    run_case("unified_moore_actor_12x12_N16", "unified", UNI, m12, s12, dict(uni_p, **mo), 16, [25, 26], 4, 300,
+             mode="actor_only", eps_sched=eps)
+    run_case("unified_moore_both_12x12_N20", "unified", UNI, m12, s12, dict(uni_p, block_size=5, **mo), 20, [27], 4,
+             300, mode="both", eps_sched=eps)
+    run_case("actoronly_moore_12x12_N16", "actor_only", AO, m12, s12, dict(ao_p, **mo), 16, [28, 29], 4, 300,
+             eps_sched=eps)
 
     # BASELINE config-5 geometry (256x256 room, 8,192 agents, block 1, the
     # run_unified_actor_training.py parameters), truncated: every reference step

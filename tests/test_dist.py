@@ -126,3 +126,22 @@ def test_gloo_world2_table_sync_equals_single_run(variant, mode, sync_period, tm
         assert np.array_equal(got[k], want[k]), k
         if k.startswith(("V_", "H_")):
             assert np.array_equal(got[f"r1_{k}"], want[k]), f"rank 1 {k}"
+
+
+@pytest.mark.parametrize("variant,mode", [("actor_only", None), ("ac", None)])
+def test_gloo_world2_adaptive_record_capacity(variant, mode, tmp_path):
+    """TableSync(capacity=None): the record buffers follow the measured touched counts
+    (identical on every rank: they come from the all-gathered counts), shrink from the
+    generous start to headroom x the observed maximum, and the result is still the
+    single-process batch bit for bit."""
+    n, steps = 37, 52
+    out = str(tmp_path / "learn.npz")
+    mp.spawn(W.learn_worker, args=(2, _port(), n, variant, mode, out, 1, steps, True), nprocs=2, join=True)
+    got = dict(np.load(out))
+    single, _ = W.run_learn_oracle(variant, mode, 0, n, steps=steps)
+    want = W.learn_summary(single)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), k
+    caps, mx = got["caps"], got["max_count"]
+    assert (mx > 0).all() or variant == "ac"
+    assert caps[0] < (1 << 17) and caps[0] >= 2 * mx[0]

@@ -384,7 +384,7 @@ def test_learner_async_records_equal_one_learner(variant, mode, sync):
     m = make_room(12, 12)
     s = l1_sff(m)
     p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
-    n, N, T = 1500, 32, 45
+    n, N, T = 1500, 32, 48     # a whole number of sync periods: every shard holds every key
     kw = dict(mode=mode, params=p, rng="philox", seed=33, auto_reset=True, max_steps=30)
     one = _learner(m, s, variant, n_envs=n, n_agents=N, **kw)
     one.set_sync_period(sync)
