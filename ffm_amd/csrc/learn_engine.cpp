@@ -84,6 +84,15 @@ struct ffm_learner {
     ffm::TrajCapture traj{};                 // trajectory capture (n_sel = 0: off)
     int sync_period = 1;                     // tables applied every sync_period-th step
     int since_apply = 0;                     // steps since the last apply
+    // tiled step: ffm_unified, dense tables at block size 1, the raster
+    // batch kernel; ffm_learner_step at sync period 1 (the phased multi-rank step keeps
+    // the accumulators, which its exchange sums)
+    bool tiled_ok = false;
+    bool tstats_valid = false;               // d_tstats summarises the current H
+    int NT = 0;
+    ffm::TileRec* d_trecs = nullptr;
+    int* d_tstart = nullptr;
+    double* d_tstats = nullptr;
     DevTable V, H;
 };
 
@@ -107,7 +116,7 @@ static void release(ffm_learner* l) {
     void* bufs[] = {l->d_map, l->d_map2, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
-                    l->d_eplog, l->d_eplog_n};
+                    l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
     free_traj(l);
@@ -194,6 +203,10 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     auto magic = [](int div) { return div <= 1 ? 0u : (uint32_t)(((1ull << 32) + (unsigned)div - 1) / (unsigned)div); };
     a.mW = magic(d.W);
     a.mBS = magic(a.bs);
+    a.trecs = nullptr;       // the accumulator path unless a tiled step sets it
+    a.tstart = l->d_tstart;
+    a.tstats = l->d_tstats;
+    a.NT = l->NT;
     return a;
 }
 
@@ -372,6 +385,18 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         (he = alloc_table(l->H, l->actor || l->trained ? l->L.log2_h_capacity : 8, d.neighborhood == 8 ? 9 : 5,
                           l->actor || l->trained ? dense_by : 0, dense_n)) != hipSuccess)
         return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
+    {
+        const char* ev = getenv("FFM_TILED");
+        l->tiled_ok = !l->mt && d.variant == FFM_VARIANT_UNIFIED && dense_by && learn->block_size == 1 &&
+                      ffm::learn_batch_raster(HW, d.agent_capacity, l->D) && !(ev && ev[0] == '0');
+    }
+    if (l->tiled_ok) {
+        l->NT = (HW + ffm::kTileCells - 1) / ffm::kTileCells;
+        if (hipMalloc((void**)&l->d_trecs, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
+            hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_tstats, (size_t)l->NT * 32) != hipSuccess)
+            return cleanup(fail(FFM_E_NOMEM, "hipMalloc (tiled step)"));
+    }
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
     if (he == hipSuccess) {
         std::vector<uint32_t> m2(((size_t)HW + 15) / 16, 0u);
@@ -458,6 +483,7 @@ static int phase_apply(ffm_learner* l, int32_t which, hipStream_t s) {
     if (due) {
         HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
         l->hstat_valid = true;
+        l->tstats_valid = false;
     }
     l->phase = 3;
     return FFM_OK;
@@ -483,6 +509,7 @@ static int flush_pending(ffm_learner* l, hipStream_t s) {
     if (l->actor) {
         HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
         l->hstat_valid = true;
+        l->tstats_valid = false;
     }
     l->since_apply = 0;
     return FFM_OK;
@@ -501,6 +528,19 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
         if (l->mt) {
             HIP_TRY(ffm::launch_learn_exact(make_args(l), s));
             l->t++;
+            continue;
+        }
+        if (l->tiled_ok && l->sync_period == 1) {
+            // tiled: records -> per-tile sums in LDS -> applied (no accumulators, no full-table pass)
+            if (l->actor && !l->tstats_valid) {
+                HIP_TRY(ffm::launch_learn_tiles(make_args(l), true, s));
+                l->tstats_valid = l->hstat_valid = true;
+            }
+            ffm::LearnArgs a = make_args(l);
+            a.trecs = l->d_trecs;
+            HIP_TRY(ffm::launch_learn_batch(a, s));
+            HIP_TRY(ffm::launch_learn_tiles(a, false, s));
+            if (int rc = phase_end(l, s)) return rc;
             continue;
         }
         int rc = phase_local(l, s);
@@ -766,7 +806,7 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
     }
     hipStream_t s = (hipStream_t)stream;
     if (int rc = flush_pending(l, s)) return rc;
-    if (which == FFM_TABLE_H) l->hstat_valid = false;
+    if (which == FFM_TABLE_H) l->hstat_valid = l->tstats_valid = false;
     HIP_TRY(clear_table(l, *T, which == FFM_TABLE_V ? l->L.v_default : 0.0, s));
     if (n > 0) {
         unsigned long long* dk = nullptr;

@@ -20,6 +20,18 @@ struct LearnRec {
     int32_t k;             // chosen action, -1 = none / invalid
 };
 
+// Tiled learning step: the large-map batch kernel writes one record
+// per agent in cell-raster order instead of adding into the fixed-point accumulators,
+// and two tile kernels sum a tile of cells' records in LDS and apply them.  A tile owns
+// every slot of its cells (rank-major dense slots: p * (cap / 256) + cell at block 1).
+struct TileRec {
+    uint32_t svk;               // V / H slot of s (bits 0-27), action k (28-31; 15 = no H increment)
+    uint32_t snf;               // V slot of s' (bits 0-27; 0x0FFFFFFF = terminal), wexit (28), coll + 1 (29-31)
+    double td;                  // TD error with the step-start V (ffm_unified both: the actor's td)
+};
+constexpr int kTileCells = 8;   // cells per tile: a tile's slots are 256 rank patterns x 8 cells
+constexpr uint32_t kTileNoAct = 15u, kTileTerminal = 0x0FFFFFFFu;
+
 struct LearnTable {
     // [cap][stride] 64-bit words, one record per slot: the key (~0 = empty), then
     // its `width` values (empty slots hold the default).  A lookup's probe and the
@@ -85,6 +97,10 @@ struct LearnArgs {
     double* hstat;              // [4] has, nonfinite, min, max of H (step start)
     double* hpart;              // [2 * kHstatBlocks * 4] partials
     LearnRec* recs;             // [E][A]
+    TileRec* trecs;             // [E][A] tiled step: per-agent records in raster order (nullptr: off)
+    int* tstart;                // [E][NT + 1] tiled step: agents of env e in cells < kTileCells * t
+    double* tstats;             // [NT][4] tiled step: per-tile H summary (present, non-finite, min, max)
+    int NT;                     // tiles: ceil(HW / kTileCells)
     int* overflow;              // [1] table full / reset capacity exceeded
     uint32_t key0, key1, t;
     int auto_reset, max_steps;
@@ -123,6 +139,8 @@ hipError_t launch_learn_exact(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s);
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
+bool learn_batch_raster(int HW, int A, int D);
+hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s);
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_capture(const LearnArgs& a, const TrajCapture& c, hipStream_t s);

@@ -1226,6 +1226,9 @@ void learn_batch_kernel(LearnArgs a) {
     // The agent index (owner priority, Philox keys, order-preserving compaction)
     // is then read back from the grid.
     constexpr bool RASTER = FFM_RASTER && !DL && LPE >= 64 && EPB == 1;
+    // tiled step: records in raster order for the tile kernels, no
+    // accumulator adds; set by the host for single-rank ffm_unified steps at block size 1
+    const bool TILED = RASTER && a.trecs != nullptr;
     int p[APT], ia[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
@@ -1255,8 +1258,15 @@ void learn_batch_kernel(LearnArgs a) {
             const bool f = c < c1 && grid[c] != kNone16;
             const unsigned long long m = __ballot(f);
             if (f) req[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)c;
+            if (a.trecs && lane < 64 / kTileCells) {
+                // tiled step: the raster rank of the first agent of each tile of this 64-cell chunk
+                const int tc = c - lane + kTileCells * lane;
+                if (tc < c1)
+                    a.tstart[e * (a.NT + 1) + tc / kTileCells] = base + __popcll(m & ((1ull << (kTileCells * lane)) - 1ull));
+            }
             base += __popcll(m);
         }
+        if (a.trecs && tid == 0) a.tstart[e * (a.NT + 1) + a.NT] = n;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < APT; j++) {
@@ -1438,6 +1448,8 @@ void learn_batch_kernel(LearnArgs a) {
         const int i = tid + j * LPE;   // recs in lane-rank order: the post kernel inherits the locality
         int vsl = -1;      // this lane's V slot and fixed-point td, added after the block
         long long vq = 0;
+        double tdv = 0.0;  // tiled step: the record's td, s' slot and action
+        int snv = -1, kk = (int)kTileNoAct;
         do {
             if (i >= n || trained || (FFM_LABLATE & 2)) break;
             double r = a.step_penalty;
@@ -1468,10 +1480,16 @@ void learn_batch_kernel(LearnArgs a) {
             const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
             vsl = sv;
             vq = fx(td);
+            tdv = td;
+            snv = sn;
             if (!actor) break;
             if (act[j] < 0) break;
             if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
             if (hsl[j] < 0) break;
+            if (TILED) {            // the tile kernels sum the increments (hsl == sv: one dense layout)
+                kk = avalid[j] ? act[j] : (int)kTileNoAct;
+                break;
+            }
             if (post_update) {
                 LearnRec rc;
                 rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
@@ -1480,7 +1498,18 @@ void learn_batch_kernel(LearnArgs a) {
                 acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + act[j]), fx(a.alpha_h * td));
             }
         } while (false);
-        if (!(FFM_LABLATE & 1)) v_pair_add(a.V, vsl, vq);
+        if (TILED) {
+            if (vsl >= 0) {
+                TileRec rc;
+                rc.svk = (uint32_t)vsl | ((uint32_t)kk << 28);
+                rc.snf = (snv >= 0 ? (uint32_t)snv : kTileTerminal) | ((uint32_t)(wexit[j] ? 1 : 0) << 28) |
+                         ((uint32_t)(coll[j] + 1) << 29);
+                rc.td = tdv;
+                a.trecs[e * A + i] = rc;
+            }
+        } else if (!(FFM_LABLATE & 1)) {
+            v_pair_add(a.V, vsl, vq);
+        }
     }
     LSTAMP(4);
     // ---- exit removal (order preserving), counters ---------------------------------------
@@ -1722,6 +1751,229 @@ __global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
     const double vn = rc.snv >= 0 ? tval(a.V, rc.snv)[0] : 0.0;
     const double td = (rc.r + a.gamma * vn) - tval(a.V, rc.sv)[0];
     acc_add(acc_at(a.Ht, (size_t)rc.hslot * 5 + rc.k), fx(a.alpha_h * td));
+}
+
+// ===========================================================================
+// Tiled learning step (ffm_unified, dense tables, block size 1).
+// Tile t = cells [8 t, 8 t + 8) owns the slots p * Q + c of those cells for every
+// rank pattern p (Q = cap / 256), 2,048 slots.  One workgroup per tile reads the
+// records of every env's agents on those cells (a contiguous raster range per env,
+// learn_batch_kernel's tstart) and sums them in LDS: no atomic leaves the chip, and
+// only touched slots are read and written.  The integer sums are those the
+// accumulators held, so the tables equal the accumulator path's bit for bit.
+// ===========================================================================
+// 1,024 threads per tile, two per env: every env's record range of the tile is
+// split between a thread pair (the LDS of the H pass allows one workgroup per CU).
+constexpr int kTileThreads = 1024, kTileWaves = kTileThreads / 64;
+
+__device__ __forceinline__ int tile_idx(uint32_t slot, int qsh, uint32_t Q, int c0) {
+    return (int)(slot >> qsh) * kTileCells + (int)((slot & (Q - 1u)) - (uint32_t)c0);
+}
+
+// V: visit-averaged TD(0) of every touched state (learn_apply_dense_kernel's update).
+__global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a) {
+    constexpr int NS = 256 * kTileCells;
+    __shared__ long long qs[NS];
+    __shared__ uint32_t ks[NS];
+    const int t = (int)blockIdx.x, tid = (int)threadIdx.x;
+    for (int i = tid; i < NS; i += kTileThreads) { qs[i] = 0; ks[i] = 0u; }
+    __syncthreads();
+    const uint32_t Q = (a.V.mask + 1u) >> 8;
+    const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
+    for (long long w = tid; w < 2 * a.E; w += kTileThreads) {
+        const long long e = w >> 1;
+        const int* ts = a.tstart + e * (a.NT + 1) + t;
+        const int lo = ts[0], hi = ts[1];
+        for (int r = lo + (int)(w & 1); r < hi; r += 2) {
+            const TileRec rc = a.trecs[e * a.A + r];
+            const int idx = tile_idx(rc.svk & 0x0FFFFFFFu, qsh, Q, c0);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(rc.td));
+            atomicAdd(&ks[idx], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < NS; i += kTileThreads) {
+        const uint32_t k = ks[i];
+        if (!k) continue;
+        double* vp = tval(a.V, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+        vp[0] = v_visits(vp[0], qs[i], (long long)k, a.V.alpha);
+    }
+}
+
+// H: the actor increments (actor_only: the TD error with the updated V, like
+// learn_post_kernel; both: the step's td), applied at once, and the tile's summary of
+// the H statistics (present, non-finite, min, max) for the next step.  The summary
+// is updated from the touched rows unless a touched value held the tile's old min or
+// max and moved inward (or was non-finite): then the tile's present rows are rescanned.
+// stats_only: no records, rescan (statistics of an imported / cleared table).
+__global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a, int stats_only) {
+    constexpr int NS = 256 * kTileCells;
+    __shared__ long long hq[NS * 5];
+    __shared__ uint32_t touched[NS / 32];
+    __shared__ double smn[kTileWaves], smx[kTileWaves];
+    __shared__ int sfl[kTileWaves];
+    const int t = (int)blockIdx.x, tid = (int)threadIdx.x;
+    const bool post_update = a.mode == kModeActor;
+    const uint32_t Q = (a.Ht.mask + 1u) >> 8;
+    const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
+    double* ts = a.tstats + 4 * t;
+    const double omn = ts[2], omx = ts[3];
+    const bool onf = ts[1] != 0.0;
+    int flags = 0;                      // 1 non-finite, 2 rescan, 4 any row
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    if (!stats_only) {
+        for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
+        for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
+        __syncthreads();
+        for (long long w = tid; w < 2 * a.E; w += kTileThreads) {
+            const long long e = w >> 1;
+            const int* tsr = a.tstart + e * (a.NT + 1) + t;
+            const int lo = tsr[0], hi = tsr[1];
+            for (int r = lo + (int)(w & 1); r < hi; r += 2) {
+                const TileRec rc = a.trecs[e * a.A + r];
+                const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+                const int idx = tile_idx(sv, qsh, Q, c0);
+                atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+                const int k = (int)(rc.svk >> 28);
+                if (k == (int)kTileNoAct) continue;
+                double td = rc.td;
+                if (post_update) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
+                    double r0 = a.step_penalty;
+                    if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
+                    const int coll = (int)(rc.snf >> 29) - 1;
+                    if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
+                    const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+                    const double vn = sn != kTileTerminal ? tval(a.V, sn)[0] : 0.0;
+                    td = (r0 + a.gamma * vn) - tval(a.V, sv)[0];
+                }
+                atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]),
+                          (unsigned long long)fx(a.alpha_h * td));
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < NS; i += kTileThreads) {
+            if (!((touched[i >> 5] >> (i & 31)) & 1u)) continue;
+            double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+            flags |= 4;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const long long q = hq[i * 5 + k];
+                const double old = vp[k];
+                double v = old;
+                if (q != 0) {
+                    v = v + (double)q * (1.0 / kFxOne);
+                    vp[k] = v;
+                    // a value that held the tile's extreme moved inward (or off / to non-finite)
+                    if ((old == omx && !(v >= old)) || (old == omn && !(v <= old)) || !__builtin_isfinite(old))
+                        flags |= 2;
+                }
+                flags |= __builtin_isfinite(v) ? 0 : 1;
+                mn = v < mn ? v : mn;
+                mx = v > mx ? v : mx;
+            }
+        }
+    }
+    // block reduction of the touched rows' summary
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
+        mn = a2 < mn ? a2 : mn;
+        mx = b2 > mx ? b2 : mx;
+        flags |= __shfl_xor(flags, o);
+    }
+    const int wv = tid >> 6;
+    if ((tid & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sfl[wv] = flags; }
+    __syncthreads();
+    mn = smn[0]; mx = smx[0]; flags = sfl[0];
+    for (int w = 1; w < kTileWaves; w++) {
+        mn = smn[w] < mn ? smn[w] : mn;
+        mx = smx[w] > mx ? smx[w] : mx;
+        flags |= sfl[w];
+    }
+    const bool rescan = stats_only || (flags & 2) || (onf && (flags & 4));
+    if (!rescan) {
+        if (tid == 0) {
+            ts[0] = (ts[0] != 0.0 || (flags & 4)) ? 1.0 : 0.0;
+            ts[1] = (onf || (flags & 1)) ? 1.0 : 0.0;
+            ts[2] = omn < mn ? omn : mn;
+            ts[3] = omx > mx ? omx : mx;
+        }
+        return;
+    }
+    __syncthreads();               // every wave has read the old summary and the shared partials
+    int nf = 0, any = 0;
+    mn = __builtin_inf();
+    mx = -__builtin_inf();
+    for (int i = tid; i < NS; i += kTileThreads) {
+        const size_t slot = (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells);
+        if (!((a.Ht.present[slot >> 5] >> (slot & 31)) & 1u)) continue;
+        any = 1;
+        const double* vp = tval(a.Ht, slot);
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const double v = vp[k];
+            nf |= !__builtin_isfinite(v);
+            mn = v < mn ? v : mn;
+            mx = v > mx ? v : mx;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
+        mn = a2 < mn ? a2 : mn;
+        mx = b2 > mx ? b2 : mx;
+        nf |= __shfl_xor(nf, o);
+        any |= __shfl_xor(any, o);
+    }
+    if ((tid & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sfl[wv] = nf | (any << 1); }
+    __syncthreads();
+    if (tid == 0) {
+        int f = 0;
+        for (int w = 0; w < kTileWaves; w++) {
+            mn = smn[w] < mn ? smn[w] : mn;
+            mx = smx[w] > mx ? smx[w] : mx;
+            f |= sfl[w];
+        }
+        ts[0] = (f & 2) ? 1.0 : 0.0;
+        ts[1] = (f & 1) ? 1.0 : 0.0;
+        ts[2] = mn;
+        ts[3] = mx;
+    }
+}
+
+// The tiles' summaries -> the statistics the next step's actor reads (hstat).
+__global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
+    __shared__ double smn[4], smx[4];
+    __shared__ int snf[4];
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    int nf = 0;
+    for (int t = threadIdx.x; t < a.NT; t += 256) {
+        const double* ts = a.tstats + 4 * t;
+        if (ts[0] == 0.0) continue;
+        nf |= ts[1] != 0.0;
+        mn = ts[2] < mn ? ts[2] : mn;
+        mx = ts[3] > mx ? ts[3] : mx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
+        mn = a2 < mn ? a2 : mn;
+        mx = b2 > mx ? b2 : mx;
+        nf |= __shfl_xor(nf, o);
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smn[wv] = mn; smx[wv] = mx; snf[wv] = nf; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            mn = smn[w] < mn ? smn[w] : mn;
+            mx = smx[w] > mx ? smx[w] : mx;
+            nf |= snf[w];
+        }
+        a.hstat[0] = *a.Ht.n > 0 ? 1.0 : 0.0;
+        a.hstat[1] = nf ? 1.0 : 0.0;
+        a.hstat[2] = mn;
+        a.hstat[3] = mx;
+        *a.Ht.mark = *a.Ht.n;
+        *a.V.mark = *a.V.n;
+    }
 }
 
 __global__ __launch_bounds__(256) void learn_fill_default_kernel(LearnTable T, double v) {
@@ -2137,6 +2389,32 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
         if (a.Ht.dense_by) learn_apply_dense_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
         else learn_apply_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
         learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, nb);
+    }
+    return hipGetLastError();
+}
+
+// Which batch kernel a shape gets (launch_batch_d): does it walk agents in raster order?
+bool learn_batch_raster(int HW, int A, int D) {
+    constexpr size_t kLds = 64 * 1024;
+    if (!FFM_RASTER || A <= 32) return false;       // 32-lane envs: several per workgroup
+    if (A <= 64) return false;                       // one wave per env: LPE = 64, but DL or not --
+    if (A <= 256) return batch_carve(HW, A, D, 1, true).shared > kLds;
+    return true;                                     // 1024-lane workgroups, DFF in global memory
+}
+
+// One tiled step's table work: V, then (actor modes) H and the statistics.  With
+// init_stats, only the per-tile statistics of the current H (no records).
+hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s) {
+    const bool actor = a.mode != kModeCritic;
+    if (init_stats) {
+        learn_tile_h_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a, 1);
+        learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
+        return hipGetLastError();
+    }
+    learn_tile_v_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a);
+    if (actor) {
+        learn_tile_h_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a, 0);
+        learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
     return hipGetLastError();
 }

@@ -223,6 +223,18 @@ def test_learner_philox_large_rooms(variant, mode):
     _philox_compare(variant, mode, p, 64, 64, 600, 16, 25, max_steps=20, seed=4)
 
 
+@pytest.mark.parametrize("mode", ["critic_only", "actor_only", "both"])
+def test_learner_philox_tiled_step_matches_cpu(mode):
+    """The tiled step (ffm_unified at block size 1 on the raster batch kernel, DESIGN.md
+    9.7): per-agent records summed per tile of cells in LDS instead of the fixed-point
+    accumulators, H statistics kept per tile (incremental, rescans when an extreme moves
+    inward).  Positions, DFF, V and H equal the CPU restatement bit for bit."""
+    p = {"epsilon": 0.1, "block_size": 1}
+    _philox_compare("unified", mode, p, 64, 64, 600, 16, 30, max_steps=20, seed=4)
+    _philox_compare("unified", mode, dict(p, k_A=3.0, step_penalty=-1.0), 48, 40, 300, 24, 45, A=320,
+                    max_steps=25, seed=6, env_base=77)
+
+
 def test_learner_philox_config5_geometry():
     """256x256 room, 8,192 agents (BASELINE config 5, ffm_unified actor_only): thresholded
     on-device placement (> 16,384 free cells) and the 8-agents-per-lane kernel."""
