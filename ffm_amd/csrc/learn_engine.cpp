@@ -87,6 +87,7 @@ struct ffm_learner {
     // tiled step: ffm_unified, dense tables at block size 1, the raster
     // batch kernel; ffm_learner_step at sync period 1 (the phased multi-rank step keeps
     // the accumulators, which its exchange sums)
+    int eps_phase = 0;                       // ffm_learner_set_epsilon_phase
     bool tiled_ok = false;
     bool tstats_valid = false;               // d_tstats summarises the current H
     int NT = 0;
@@ -199,6 +200,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.free_cells = l->d_free_cells;
     a.eps_start = l->L.eps_start; a.eps_end = l->L.eps_end;
     a.eps_offset = l->L.eps_offset; a.eps_span = l->L.eps_span;
+    a.eps_phase = l->eps_phase;
     a.eplog = l->d_eplog; a.eplog_n = l->d_eplog_n; a.eplog_cap = l->eplog_cap;
     auto magic = [](int div) { return div <= 1 ? 0u : (uint32_t)(((1ull << 32) + (unsigned)div - 1) / (unsigned)div); };
     a.mW = magic(d.W);
@@ -859,6 +861,12 @@ int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double ep
     if (!l) return fail(FFM_E_INVALID, "null learner");
     l->L.eps_start = eps_start; l->L.eps_end = eps_end;
     l->L.eps_offset = eps_offset; l->L.eps_span = eps_span;
+    return FFM_OK;
+}
+
+int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period) {
+    if (!l || period < 0) return fail(FFM_E_INVALID, "epsilon phase period must be >= 0");
+    l->eps_phase = period;
     return FFM_OK;
 }
 

@@ -110,6 +110,7 @@ struct LearnArgs {
     const uint16_t* free_cells;    // [F] placement candidates: x*W+y of the free cells, row-major
                                    // (np.argwhere(map == 0)), or a radius-limited subset of them
     double eps_start, eps_end, eps_offset, eps_span;   // batched epsilon schedule (eps_span > 0)
+    int eps_phase;              // > 0: global env g adds g % eps_phase to its episode count k
     uint32_t mW, mBS;           // ceil(2^32 / d) for d = W, bs (0 when d = 1): n / d = mulhi(n, m)
     int* eplog;                 // [eplog_cap][4] ended episodes: global env, index, steps, emptied
     unsigned long long* eplog_n;

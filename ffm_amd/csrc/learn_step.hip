@@ -1111,9 +1111,12 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 
 // This env's epsilon: the learner's, or the batched schedule's after k ended
 // episodes (run_actor_only_training.py:190-196, run_unified_actor_training.py:253-259).
-__device__ __forceinline__ double env_epsilon(const LearnArgs& a, int k) {
+// eps_phase spreads envs over the schedule: env g starts at its (g % eps_phase)-th episode,
+// so E >= P envs running one episode each cover a per-configuration schedule of P episodes.
+__device__ __forceinline__ double env_epsilon(const LearnArgs& a, int k, long long genv) {
     if (!(a.eps_span > 0)) return a.epsilon;
-    const double e = a.eps_start + (a.eps_end - a.eps_start) * (((double)k + a.eps_offset) / a.eps_span);
+    const double ph = a.eps_phase > 0 ? (double)(genv % a.eps_phase) : 0.0;
+    const double e = a.eps_start + (a.eps_end - a.eps_start) * (((double)k + a.eps_offset + ph) / a.eps_span);
     return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
 }
 
@@ -1279,7 +1282,7 @@ void learn_batch_kernel(LearnArgs a) {
         __syncthreads();
     }
     const bool trained = a.variant == kVarTrained;
-    const double eps = live && actor ? env_epsilon(a, a.episodes[e]) : 0.0;
+    const double eps = live && actor ? env_epsilon(a, a.episodes[e], a.env_base + e) : 0.0;
     HStat hs{};
     if (actor || trained) {
         hs.has = (int)a.hstat[0];

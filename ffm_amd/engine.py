@@ -36,7 +36,7 @@ EXPORTED = [
     "ffm_learner_export_table", "ffm_learner_import_table", "ffm_learner_get_step_index",
     "ffm_learner_set_step_index", "ffm_learner_step_local", "ffm_learner_step_apply", "ffm_learner_step_end",
     "ffm_learner_delta_export", "ffm_learner_delta_merge", "ffm_learner_set_placement",
-    "ffm_learner_set_epsilon_schedule", "ffm_learner_drain_episodes",
+    "ffm_learner_set_epsilon_schedule", "ffm_learner_set_epsilon_phase", "ffm_learner_drain_episodes",
     "ffm_learner_set_trajectory_capture", "ffm_learner_drain_trajectory",
     "ffm_learner_delta_export_async", "ffm_learner_delta_merge_async", "ffm_learner_set_sync_period",
     "ffm_learner_apply_due", "ffm_learner_dense_buffers", "ffm_learner_dense_adopt",
@@ -137,6 +137,7 @@ def load_library():
     L.ffm_learner_delta_merge.argtypes = [P, i32, P, P, i64, P]
     L.ffm_learner_set_placement.argtypes = [P, P, i32, i32]
     L.ffm_learner_set_epsilon_schedule.argtypes = [P, C.c_double, C.c_double, C.c_double, C.c_double]
+    L.ffm_learner_set_epsilon_phase.argtypes = [P, i32]
     L.ffm_learner_drain_episodes.argtypes = [P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     L.ffm_learner_set_trajectory_capture.argtypes = [P, P, P, i32, i32, i64, P]
     L.ffm_learner_delta_export_async.argtypes = [P, i32, P, P, i64, P, P]
@@ -558,6 +559,10 @@ class Learner:
         """Per-env epsilon clip(start + (end - start) * (k + offset) / span) after k ended episodes."""
         _check(self._L.ffm_learner_set_epsilon_schedule(self._h, float(start), float(end), float(offset),
                                                           float(span)))
+
+    def set_epsilon_phase(self, period: int):
+        """Env g starts the epsilon schedule at its (g % period)-th episode (0 = off)."""
+        _check(self._L.ffm_learner_set_epsilon_phase(self._h, int(period)))
 
     def drain_episodes(self, stream=None) -> np.ndarray:
         """Ended episodes since the last drain: int32 [n, 4] rows {global env, episode index,

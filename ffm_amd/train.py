@@ -82,13 +82,21 @@ def save_trajectory(out_dir: str, N: int, episode: int, total: int, positions: l
 
 def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per_config: int,
                    eps_start: float | None = None, eps_end: float | None = None, out_dir: str | None = None,
-                   log_every: int = 16, verbose: bool = True, trajectory_every: int = 0) -> dict:
+                   log_every: int = 16, verbose: bool = True, trajectory_every: int = 0,
+                   eps_phase: bool = True) -> dict:
     """Run every (radius, N) configuration; return per-configuration statistics and
     (when `out_dir` is given) write the reference's output files there, with the
-    trajectory of every `trajectory_every`-th episode under out_dir/trajectories."""
+    trajectory of every `trajectory_every`-th episode under out_dir/trajectories.
+
+    Epsilon (actor modes) decays linearly over the P = episodes_per_config episodes of a
+    configuration (run_unified_actor_training.py:253-259: episode j of P explores with
+    start + (end - start) * j / P).  With fewer envs than P, env e runs ceil(P / E)
+    episodes and decays over its own; with E >= P (one episode per env) and eps_phase,
+    env g plays episode 1 + g % P of the schedule, so the E episodes cover it."""
     L = learner
     E = L.n_envs
     per_env = max(1, math.ceil(episodes_per_config / E))
+    phased = bool(eps_phase) and per_env == 1 and E >= episodes_per_config > 1
     chunk = max(1, min(int(log_every), 16))      # the episode log holds 16 steps of episode ends
     rows, configs = [], []
     episode_num = 0
@@ -106,7 +114,11 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
             L.set_radius_placement(exit_pos, radius, N)
             if eps_start is not None and L.actor:
                 # local linear decay per configuration (run_unified_actor_training.py:253-259)
-                L.set_epsilon_schedule(eps_start, eps_end, 1, per_env)
+                if phased:
+                    L.set_epsilon_schedule(eps_start, eps_end, 1, episodes_per_config)
+                    L.set_epsilon_phase(episodes_per_config)
+                else:
+                    L.set_epsilon_schedule(eps_start, eps_end, 1, per_env)
             v0 = L.table_size("V")
             L.reset()
             done, trajs = [], {}
@@ -130,7 +142,9 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
             base = episode_num
             for idx, (env, k, steps, emptied) in enumerate(ended.tolist()):
                 episode_num += 1
-                eps = (min(max(eps_start + (eps_end - eps_start) * ((k + 1) / per_env), 0.0), 1.0)
+                j, span = ((k + 1 + env % episodes_per_config, episodes_per_config) if phased   # env: global id
+                           else (k + 1, per_env))
+                eps = (min(max(eps_start + (eps_end - eps_start) * (j / span), 0.0), 1.0)
                        if eps_start is not None and L.actor else 0.0)
                 rows.append([episode_num, len(configs) + 1, radius, N, steps, v1, h1, f"{eps:.6f}"])
                 tr = trajs.get((env, k))
@@ -204,6 +218,8 @@ def main():
     ap.add_argument("--trajectory-every", type=int, default=None,
                     help="save every n-th episode's trajectory (default 100 for actor modes, as "
                          "run_actor_only_training.py; 0 = none)")
+    ap.add_argument("--no-eps-phase", action="store_true",
+                    help="with envs >= episodes: every env at the schedule's first episode (no spread)")
     a = ap.parse_args()
     m = make_room(a.size, a.size)
     # run_unified_*_training.py MODEL_PARAMS
@@ -218,7 +234,7 @@ def main():
     es, ee = (float(x) for x in a.eps.split(","))
     every = a.trajectory_every if a.trajectory_every is not None else (100 if L.actor else 0)
     run_curriculum(L, (0, a.size // 2), [int(x) for x in a.radius.split(",")], n_list, a.episodes, es, ee, a.out,
-                   trajectory_every=every)
+                   trajectory_every=every, eps_phase=not a.no_eps_phase)
 
 
 if __name__ == "__main__":

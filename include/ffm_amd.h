@@ -304,6 +304,11 @@ int ffm_learner_dense_adopt(ffm_learner* l, int32_t which, const uint32_t* d_uni
 int ffm_learner_set_placement(ffm_learner* l, const uint16_t* cells, int32_t count, int32_t n_agents);
 int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double eps_end, double eps_offset,
                                      double eps_span);
+/* period > 0: global env g explores as if g % period more episodes had ended (k + g % period
+ * in the schedule above), so E >= P envs that each run one episode of a configuration cover a
+ * P-episode per-configuration schedule (run_unified_actor_training.py:253-259) between them;
+ * 0 = off (the default). */
+int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period);
 /* Ended episodes since the last drain, in no particular order: records of 4 int32
  * {global env, episode index, steps, 1 = emptied / 0 = truncated at max_steps}
  * (the per-episode rows of run_*_training.py's steps_per_episode.csv).  *dropped counts

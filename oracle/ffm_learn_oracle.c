@@ -904,9 +904,10 @@ void ffo_lbatch_set_placement(ffo_lbatch* b, const uint16_t* cells, int32_t coun
     b->nplace = count;
 }
 
-static double eps_of(const ffo_learn_cfg* c, int32_t k) {
+static double eps_of(const ffo_learn_cfg* c, int32_t k, int64_t genv) {
     if (!(c->eps_span > 0)) return c->epsilon;
-    double e = c->eps_start + (c->eps_end - c->eps_start) * (((double)k + c->eps_offset) / c->eps_span);
+    const double ph = c->eps_phase > 0 ? (double)(genv % c->eps_phase) : 0.0;
+    double e = c->eps_start + (c->eps_end - c->eps_start) * (((double)k + c->eps_offset + ph) / c->eps_span);
     return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
 }
 
@@ -966,7 +967,7 @@ int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, 
             total += (uint64_t)n;
             for (int i = 0; i < n; i++) p32[i] = pe[i];
             L.rng.genv = (uint64_t)(env_base + e);
-            L.eps = eps_of(c, episodes ? episodes[e] : 0);
+            L.eps = eps_of(c, episodes ? episodes[e] : 0, env_base + e);
             if (env_step(&L, p32, &n, dff + e * (int64_t)HW, occ, sm, sm + HW, B, b->recs + e * (int64_t)A_cap))
                 err = 1;
             for (int i = 0; i < n; i++) pe[i] = (uint16_t)p32[i];

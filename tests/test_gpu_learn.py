@@ -484,9 +484,11 @@ def test_learner_curriculum_schedule_and_episode_log(variant, mode):
     ncell = L.set_radius_placement((0, 6), 4, N)
     n = min(N, ncell)
     L.set_epsilon_schedule(0.2, 0.01, 1, 10)
+    L.set_epsilon_phase(7)                      # env g starts the schedule at episode g % 7
     L.reset()
     cpu = LO.Learn(m, s, variant, mode, p, log2_cap=22)
     cpu.set_epsilon_schedule(0.2, 0.01, 1, 10)
+    cpu.set_epsilon_phase(7)
     sh = LO.Shard(cpu, E, N, n, seed, 0, maxs, nthreads=16)
     free = np.argwhere(m == 0)
     r = np.abs(free[:, 0]) + np.abs(free[:, 1] - 6) <= 4
