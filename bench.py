@@ -381,11 +381,12 @@ def bench_learner(args, world, rank, torch, dist):
             "step_ms_events": step_ms,
             "tables": {"V": v_size, "H": h_size},
             "table_sync": (dict({"period": args.sync_period,
-                                 "mode": "dense all-reduce" if sync.dense else "records (adaptive capacity)",
+                                 "mode": ("tiled records all-gather" if sync.tiled else
+                                          "dense all-reduce" if sync.dense else "records (adaptive capacity)"),
                                  "bytes_per_rank_per_step": sent_timed / (reps["summary"]["n"] * args.steps),
                                  "note": "bytes this rank contributes to the collectives per step, over the "
                                          "timed regions"},
-                                **({} if sync.dense else {"record_capacity": dict(sync.caps),
+                                **({} if sync.dense or sync.tiled else {"record_capacity": dict(sync.caps),
                                                           "max_touched_records": dict(sync.max_count)}))
                            if world > 1 else {"period": args.sync_period}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -209,6 +209,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.tstart = l->d_tstart;
     a.tstats = l->d_tstats;
     a.NT = l->NT;
+    a.tile_ensure = 0;
     return a;
 }
 
@@ -862,6 +863,51 @@ int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double ep
     l->L.eps_start = eps_start; l->L.eps_end = eps_end;
     l->L.eps_offset = eps_offset; l->L.eps_span = eps_span;
     return FFM_OK;
+}
+
+// ---- tiled step across ranks ---------------------------------------
+int ffm_learner_tiled_buffers(ffm_learner* l, void** d_recs, int64_t* rec_bytes, int32_t** d_tstart,
+                              int64_t* tstart_count) {
+    if (!l || !d_recs || !rec_bytes || !d_tstart || !tstart_count) return fail(FFM_E_INVALID, "null argument");
+    if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
+    *d_recs = l->d_trecs;
+    *rec_bytes = (int64_t)(l->d.n_envs * l->d.agent_capacity * (int64_t)sizeof(ffm::TileRec));
+    *d_tstart = l->d_tstart;
+    *tstart_count = (int64_t)l->d.n_envs * (l->NT + 1);
+    return FFM_OK;
+}
+
+int ffm_learner_step_tiled_local(ffm_learner* l, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (!l->tiled_ok || l->sync_period != 1) return fail(FFM_E_UNSUPPORTED, "tiled step: tiled learner at sync period 1");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "step_tiled_local: previous step not ended");
+    if (int rc = async_overflow(l)) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (l->actor && !l->tstats_valid) {
+        HIP_TRY(ffm::launch_learn_tiles(make_args(l), true, s));
+        l->tstats_valid = l->hstat_valid = true;
+    }
+    ffm::LearnArgs a = make_args(l);
+    a.trecs = l->d_trecs;
+    HIP_TRY(ffm::launch_learn_batch(a, s));
+    l->phase = 5;
+    return FFM_OK;
+}
+
+int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const int32_t* d_tstart_all,
+                                 int64_t n_envs_all, void* stream) {
+    if (!l || !d_recs_all || !d_tstart_all || n_envs_all < 1) return fail(FFM_E_INVALID, "bad argument");
+    if (l->phase != 5) return fail(FFM_E_INVALID, "step_tiled_apply must follow step_tiled_local");
+    hipStream_t s = (hipStream_t)stream;
+    ffm::LearnArgs a = make_args(l);
+    a.trecs = const_cast<ffm::TileRec*>(reinterpret_cast<const ffm::TileRec*>(d_recs_all));
+    a.tstart = const_cast<int*>(d_tstart_all);
+    a.E = n_envs_all;
+    a.tile_ensure = 1;
+    HIP_TRY(ffm::launch_learn_tiles(a, false, s));
+    int rc = phase_end(l, s);
+    if (!rc && l->h_overflow) HIP_TRY(hipMemcpyAsync(l->h_overflow, l->d_overflow, 4, hipMemcpyDeviceToHost, s));
+    return rc;
 }
 
 int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period) {

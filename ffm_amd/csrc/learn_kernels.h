@@ -101,6 +101,7 @@ struct LearnArgs {
     int* tstart;                // [E][NT + 1] tiled step: agents of env e in cells < kTileCells * t
     double* tstats;             // [NT][4] tiled step: per-tile H summary (present, non-finite, min, max)
     int NT;                     // tiles: ceil(HW / kTileCells)
+    int tile_ensure;            // tile kernels: insert the records' slots (records gathered from other ranks)
     int* overflow;              // [1] table full / reset capacity exceeded
     uint32_t key0, key1, t;
     int auto_reset, max_steps;

@@ -1093,6 +1093,9 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 #ifndef FFM_LABLATE
 #define FFM_LABLATE 0
 #endif
+#ifndef FFM_VEARLY
+#define FFM_VEARLY 0   // ffm_actor_only: probe V(s) at decide (A/B switch)
+#endif
 // FFM_LSTAMP (diagnostic builds): thread 0 of blocks 0 and gridDim/2 prints the
 // wall-clock ticks (100 MHz) of each phase of the batched step.
 #ifndef FFM_LSTAMP
@@ -1298,10 +1301,11 @@ void learn_batch_kernel(LearnArgs a) {
     // ---- decide --------------------------------------------------------------
     unsigned long long skey[APT];
     int act[APT], avalid[APT], wexit[APT], hsl[APT];
+    int vse[APT];        // FFM_VEARLY: the V slot of s, probed at decide beside the H probe
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = ia[j];
-        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
+        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0; vse[j] = -1;
         if (tid + j * LPE >= n) continue;
         const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
         skey[j] = encode(a, smc, x, y);
@@ -1362,6 +1366,9 @@ void learn_batch_kernel(LearnArgs a) {
             // first exit, then the exit for the rest; the last one is the agent's action.
             if (ex != 0) {
                 hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
+                // the learning phase's V(s) probe, independent of the H row: its loads overlap
+                // the H probe and the policy math instead of trailing the resolve
+                if (FFM_VEARLY) vse[j] = tab_get(a.V, skey[j], a.overflow);
                 if (hsl[j] < 0) continue;
                 actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, true, P);
             }
@@ -1477,7 +1484,7 @@ void learn_batch_kernel(LearnArgs a) {
                 sv = (int)dense_slot(skey[j], a.V);
                 dense_ensure(a.V, (uint32_t)sv, skey[j]);
             } else {
-                sv = tab_get(a.V, skey[j], a.overflow);
+                sv = vse[j] >= 0 ? vse[j] : tab_get(a.V, skey[j], a.overflow);
             }
             if (sv < 0) break;
             const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
@@ -1773,6 +1780,13 @@ __device__ __forceinline__ int tile_idx(uint32_t slot, int qsh, uint32_t Q, int 
     return (int)(slot >> qsh) * kTileCells + (int)((slot & (Q - 1u)) - (uint32_t)c0);
 }
 
+// The rank key of a dense slot (inverse of dense_slot): ranks in bits 0-7, bx, by.
+__device__ __forceinline__ unsigned long long dense_key(uint32_t slot, int qsh, uint32_t Q, uint32_t by) {
+    const uint32_t b = slot & (Q - 1u);
+    return (unsigned long long)(slot >> qsh) | ((unsigned long long)(b / by) << 26) |
+           ((unsigned long long)(b % by) << 45);
+}
+
 // V: visit-averaged TD(0) of every touched state (learn_apply_dense_kernel's update).
 __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
@@ -1789,9 +1803,15 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
         const int lo = ts[0], hi = ts[1];
         for (int r = lo + (int)(w & 1); r < hi; r += 2) {
             const TileRec rc = a.trecs[e * a.A + r];
-            const int idx = tile_idx(rc.svk & 0x0FFFFFFFu, qsh, Q, c0);
+            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+            const int idx = tile_idx(sv, qsh, Q, c0);
             atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(rc.td));
             atomicAdd(&ks[idx], 1u);
+            if (a.tile_ensure) {     // another rank's agent: its s and s' join this rank's V
+                dense_ensure(a.V, sv, dense_key(sv, qsh, Q, a.V.dense_by));
+                const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+                if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
+            }
         }
     }
     __syncthreads();
@@ -1837,6 +1857,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a,
                 const uint32_t sv = rc.svk & 0x0FFFFFFFu;
                 const int idx = tile_idx(sv, qsh, Q, c0);
                 atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+                if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
                 const int k = (int)(rc.svk >> 28);
                 if (k == (int)kTileNoAct) continue;
                 double td = rc.td;

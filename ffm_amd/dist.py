@@ -90,6 +90,12 @@ class TableSync:
       fixed-point accumulator array is all-reduced (SUM; RCCL runs it as
       reduce-scatter + all-gather) and the presence bitmaps are OR-ed, instead of
       exporting touched records;
+    * ``tiled`` (default: the shard is a tiled learner -- ffm_unified at block size 1 on a
+      large map -- with equal env counts on every rank, at K = 1): every rank all-gathers
+      the others' per-agent records (16 B each) and tile offsets and sums them per tile of
+      cells into its replicated tables: the exchange is proportional to the
+      agents stepped, not to the table (C5: 84 MB per rank per step instead of 940 MB of
+      accumulators);
     * ``sync_period`` K: the tables are applied (and exchanged) every K-th step only,
       the increments of K steps accumulating in between
       (``Learner.set_sync_period``); K = 1 is the reference's per-step update.
@@ -116,6 +122,13 @@ class TableSync:
         self.sync_period = int(sync_period)
         shard.set_sync_period(self.sync_period)
         self.dense = bool(getattr(shard, "dense_tables", False)) if dense is None else bool(dense)
+        self.tiled = bool(getattr(shard, "tiled", False)) and self.sync_period == 1 and dense is None
+        if self.tiled:      # the gathered records are indexed [rank * E + env]: equal E everywhere
+            n = torch.tensor([int(shard.n_envs)], dtype=torch.int64, device=device)
+            mx = n.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+            dist.all_reduce(n, op=dist.ReduceOp.MIN, group=group)
+            self.tiled = int(n.item()) == int(mx.item())
         self.bufs = {}
         self.bytes_sent = 0          # per rank, summed over exchanges (what this rank contributes)
         self.exchanges = 0
@@ -195,8 +208,27 @@ class TableSync:
         self.exchanges += 1
         (self._exchange_dense if self.dense else self._exchange_records)(which)
 
+    def _step_tiled(self):
+        s = self.shard
+        s.step_tiled_local()
+        recs, tst = s.tiled_buffers()
+        g = self.bufs.get("tiled")
+        if g is None:
+            g = (torch.empty((self.world, recs.numel()), dtype=recs.dtype, device=recs.device),
+                 torch.empty((self.world, tst.numel()), dtype=tst.dtype, device=tst.device))
+            self.bufs["tiled"] = g
+        dist.all_gather([g[0][r] for r in range(self.world)], recs, group=self.group)
+        dist.all_gather([g[1][r] for r in range(self.world)], tst, group=self.group)
+        s.step_tiled_apply(g[0].data_ptr(), g[1].data_ptr(), self.world * s.n_envs)
+        self.exchanges += 1
+        self.bytes_sent += recs.numel() + tst.numel() * 4
+
     def step(self, n_steps: int = 1):
         s = self.shard
+        if self.tiled:
+            for _ in range(int(n_steps)):
+                self._step_tiled()
+            return
         for _ in range(int(n_steps)):
             due = s.apply_due()      # host-side state, no device sync
             s.step_local()
@@ -213,7 +245,7 @@ class TableSync:
 
 
 def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16, sync_period: int = 1,
-                 dense: bool = False, async_records: bool = False):
+                 dense: bool = False, async_records: bool = False, tiled: bool = False):
     """TableSync's protocol for several shards driven by one process (e.g. one
     Learner per device, or shards of one device): the same phases, with the
     collectives replaced by handing every shard the others' records (or, dense,
@@ -226,6 +258,17 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
     than ``capacity`` is reported at the shard's next sync point."""
     for s in shards:
         s.set_sync_period(sync_period)
+    if tiled:      # TableSync's tiled exchange: every shard sums all shards' records (equal E)
+        for _ in range(int(n_steps)):
+            for s in shards:
+                s.step_tiled_local()
+            bufs = [s.tiled_buffers() for s in shards]
+            recs = torch.cat([b[0] for b in bufs])
+            tst = torch.cat([b[1] for b in bufs])
+            for s in shards:
+                s.step_tiled_apply(recs.data_ptr(), tst.data_ptr(), len(shards) * shards[0].n_envs)
+            torch.cuda.synchronize()
+        return
 
     def export_async(s, which):
         width = 2 if which == "V" else 5

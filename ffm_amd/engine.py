@@ -40,6 +40,7 @@ EXPORTED = [
     "ffm_learner_set_trajectory_capture", "ffm_learner_drain_trajectory",
     "ffm_learner_delta_export_async", "ffm_learner_delta_merge_async", "ffm_learner_set_sync_period",
     "ffm_learner_apply_due", "ffm_learner_dense_buffers", "ffm_learner_dense_adopt",
+    "ffm_learner_tiled_buffers", "ffm_learner_step_tiled_local", "ffm_learner_step_tiled_apply",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -146,6 +147,9 @@ def load_library():
     L.ffm_learner_apply_due.argtypes = [P, C.POINTER(i32)]
     L.ffm_learner_dense_buffers.argtypes = [P, i32, C.POINTER(P), C.POINTER(i64), C.POINTER(P), C.POINTER(i64)]
     L.ffm_learner_dense_adopt.argtypes = [P, i32, P, P]
+    L.ffm_learner_tiled_buffers.argtypes = [P, C.POINTER(P), C.POINTER(i64), C.POINTER(P), C.POINTER(i64)]
+    L.ffm_learner_step_tiled_local.argtypes = [P, P]
+    L.ffm_learner_step_tiled_apply.argtypes = [P, P, P, i64, P]
     L.ffm_learner_drain_trajectory.argtypes = [P, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     for name in EXPORTED:
         if name != "ffm_last_error":
@@ -796,6 +800,34 @@ class Learner:
     def dense_adopt(self, which: str, union_ptr: int, stream=None):
         _check(self._L.ffm_learner_dense_adopt(self._h, TABLE_V if which == "V" else TABLE_H, union_ptr,
                                                _stream_handle(stream)))
+
+    # -- the tiled step across ranks -----------------------------------------
+    @property
+    def tiled(self) -> bool:
+        """ffm_unified at block size 1 on a large map: the step sums per-agent records per
+        tile of cells (ffm_learner_step_tiled_*)."""
+        if not hasattr(self, "_tiled"):
+            r, t, nr, nt = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int64()
+            self._tiled = self._L.ffm_learner_tiled_buffers(self._h, C.byref(r), C.byref(nr), C.byref(t),
+                                                            C.byref(nt)) == OK
+        return self._tiled
+
+    def tiled_buffers(self):
+        """(records uint8 [E * A * 16], tile offsets int32 [E * (NT + 1)]) torch views of
+        this learner's device buffers (zero copy), filled by step_tiled_local."""
+        import torch
+        r, t, nr, nt = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int64()
+        _check(self._L.ffm_learner_tiled_buffers(self._h, C.byref(r), C.byref(nr), C.byref(t), C.byref(nt)))
+        dev = torch.device("cuda", self.device)
+        return (torch.as_tensor(_DevArray(r.value, nr.value, "|u1"), device=dev),
+                torch.as_tensor(_DevArray(t.value, nt.value, "<i4"), device=dev))
+
+    def step_tiled_local(self, stream=None):
+        _check(self._L.ffm_learner_step_tiled_local(self._h, _stream_handle(stream)))
+
+    def step_tiled_apply(self, recs_ptr: int, tstart_ptr: int, n_envs_all: int, stream=None):
+        _check(self._L.ffm_learner_step_tiled_apply(self._h, recs_ptr, tstart_ptr, int(n_envs_all),
+                                                    _stream_handle(stream)))
 
     # -- telemetry -----------------------------------------------------------------------
     def counters(self, stream=None) -> dict:

@@ -133,7 +133,7 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
             assert all(isinstance(r, list) and len(r) == z["h_vals"].shape[1] for r in Ht.values())
             assert np.array_equal(np.array(list(Ht.values()), np.float64).view(np.uint64),
                                   z["h_vals"][h_off:h_off + nh].view(np.uint64))
-            assert model.get_h_table_size() == (nh, 5 * nh)
+            assert model.get_h_table_size() == (nh, z["h_vals"].shape[1] * nh)
             h_off += nh
         else:
             assert not Ht

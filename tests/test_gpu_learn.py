@@ -235,6 +235,44 @@ def test_learner_philox_tiled_step_matches_cpu(mode):
                     max_steps=25, seed=6, env_base=77)
 
 
+@pytest.mark.parametrize("mode", ["actor_only", "both"])
+def test_learner_tiled_shards_equal_one_learner(mode):
+    """The tiled step across ranks (TableSync's exchange for tiled learners, coupled in one
+    process): two shards all-gather each other's per-agent records and tile offsets and
+    sum them per tile into their replicated tables; the tables (values, and the key sets
+    including the slots only the other shard created) and the env states equal one
+    learner stepping all envs, bit for bit."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.dist import step_coupled
+    m = make_room(64, 64)
+    s = l1_sff(m)
+    p = {"epsilon": 0.1, "block_size": 1}
+    n, N, T = 16, 600, 30
+    kw = dict(mode=mode, params=p, rng="philox", seed=8, auto_reset=True, max_steps=20)
+    one = _learner(m, s, "unified", n_envs=n, n_agents=N, **kw)
+    assert one.tiled
+    one.reset()
+    one.step(T)
+    shards = [_learner(m, s, "unified", n_envs=n // 2, n_agents=N, env_base=r * (n // 2), **kw) for r in range(2)]
+    for L in shards:
+        L.reset()
+    step_coupled(shards, T, device="cuda", tiled=True)
+    op, oc, od = one.get_state()
+    sp = [L.get_state() for L in shards]
+    assert np.array_equal(oc, np.concatenate([x[1] for x in sp]))
+    assert np.array_equal(od.view(np.uint32), np.concatenate([x[2] for x in sp]).view(np.uint32))
+    for which in ("V", "H"):
+        k0, v0 = one.export_table(which)
+        o0 = np.argsort(k0)
+        for L in shards:
+            k, v = L.export_table(which)
+            o = np.argsort(k)
+            assert np.array_equal(k[o], k0[o0]), which
+            assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), which
+    for L in shards + [one]:
+        L.close()
+
+
 def test_learner_philox_config5_geometry():
     """256x256 room, 8,192 agents (BASELINE config 5, ffm_unified actor_only): thresholded
     on-device placement (> 16,384 free cells) and the 8-agents-per-lane kernel."""

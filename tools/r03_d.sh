@@ -4,7 +4,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-d}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail 10 -v --timeout 600 --timeout-method thread \
   -k "tiled or config5 or trajectory_capture or async_records or moore or dropin or group or config2 or param_points or multi_step" > "$OUT/pytest.log" 2>&1 || { echo "pytest failed"; tail -40 "$OUT/pytest.log"; exit 1; }
 tail -3 "$OUT/pytest.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; tail -30 "$OUT/smoke.log"; exit 1; }
