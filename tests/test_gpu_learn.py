@@ -476,9 +476,13 @@ def test_learner_async_records_too_small_capacity_is_reported():
     shards = [_learner(m, s, "actor_only", n_envs=256, n_agents=32, env_base=256 * r, **kw) for r in range(2)]
     for L in shards:
         L.reset()
-    step_coupled(shards, 2, device="cuda", capacity=16, async_records=True)
     with pytest.raises(ValueError, match="record buffer too small"):
+        # the next step_local raises once the flag copy queued by step_end has landed;
+        # counters() (a sync point) raises in any case
+        step_coupled(shards, 3, device="cuda", capacity=16, async_records=True)
         shards[0].counters()
+    with pytest.raises(ValueError, match="record buffer too small"):
+        shards[1].counters()
     with pytest.raises(ValueError, match="record buffer too small"):
         shards[1].step_local()
     for L in shards:
