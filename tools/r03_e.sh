@@ -11,5 +11,10 @@ timeout -k 10 600 bash tools/rehearse.sh r03_e/rehearse_c4 8 --config 4 --steps 
 tail -1 "$OUT/rehearse_c4.out" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(d['table_sync']), d['value'])"
 timeout -k 10 900 bash tools/actor_pin.sh r03_e/actor_pin 10 512 4096 > "$OUT/actor_pin.out" 2>&1 || { echo "actor pin failed"; tail -20 "$OUT/actor_pin.out"; exit 1; }
 cat "$OUT/actor_pin.out"
-timeout -k 10 600 bash tools/ab.sh "build_ab/libcur.so build_ab/libvearly.so" --config 4 --steps 100 --warmup 30 > "$OUT/ab_c4_vearly.log" 2>&1 || { echo "ab c4 failed"; tail -20 "$OUT/ab_c4_vearly.log"; exit 1; }
-cat "$OUT/ab_c4_vearly.log"
+
+timeout -k 10 600 bash tools/traffic.sh gpurun_out/r03_e/traffic_c5 --config 5 > "$OUT/traffic_c5.out" 2>&1 || { echo "traffic c5 failed"; tail -20 "$OUT/traffic_c5.out"; exit 1; }
+tail -30 "$OUT/traffic_c5.out"
+timeout -k 10 900 bash tools/pmc_kern.sh gpurun_out/r03_e/pmc_c2 "" > "$OUT/pmc_c2.out" 2>&1 || { echo "pmc c2 failed"; tail -20 "$OUT/pmc_c2.out"; exit 1; }
+python3 tools/pmc_summary.py gpurun_out/r03_e/pmc_c2/k1 core_group > "$OUT/pmc_c2_summary.txt"; cat "$OUT/pmc_c2_summary.txt"
+timeout -k 10 600 bash tools/traffic.sh gpurun_out/r03_e/traffic_c2 > "$OUT/traffic_c2.out" 2>&1 || { echo "traffic c2 failed"; tail -20 "$OUT/traffic_c2.out"; exit 1; }
+tail -14 "$OUT/traffic_c2.out"

@@ -57,6 +57,25 @@ res = {
     "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM/rocprofv3 section); WRITE_SIZE as is",
 }
 res["traffic_over_algorithmic"] = res["hbm_bytes_per_launch"] / alg
+if cfg in (4, 5):
+    # the whole learning step: every step kernel's mean bytes per launch (batch, tile / apply /
+    # post passes, stencil, reset), summed -- FETCH x2 + WRITE as above
+    def by_kernel(path, counter):
+        acc = {}
+        for root, _, files in os.walk(path):
+            for fn in files:
+                if fn.endswith("counter_collection.csv"):
+                    with open(os.path.join(root, fn)) as fh:
+                        for r in csv.DictReader(fh):
+                            if r["Counter_Name"] == counter and "learn_" in r["Kernel_Name"]:
+                                name = r["Kernel_Name"].split("(")[0]
+                                acc.setdefault(name, []).append(float(r["Counter_Value"]))
+        return {k: sum(v[10:] or v) / len(v[10:] or v) for k, v in acc.items()}
+    fb, wb = by_kernel(os.path.join(out, "fetch"), "FETCH_SIZE"), by_kernel(os.path.join(out, "write"), "WRITE_SIZE")
+    per = {k: 2 * fb.get(k, 0.0) * 1024 + wb.get(k, 0.0) * 1024 for k in set(fb) | set(wb)}
+    res["per_kernel_bytes_per_launch"] = per
+    res["note"] = ("per-kernel means include kernels that do not run every step (resets); "
+                   "hbm_bytes_per_launch is learn_batch_kernel's")
 print(json.dumps(res, indent=1))
 with open(os.path.join(out, "traffic.json"), "w") as fh:
     json.dump(res, fh, indent=1)
