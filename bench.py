@@ -151,7 +151,7 @@ def main():
     # the engine's state after every single-step launch it ran (the CPU baseline replays
     # all envs through the same steps and compares them bit for bit)
     single_steps = args.burn_in + args.warmup + reps["summary"]["n"] * args.steps + nk
-    snap = eng.get_state() if rank == 0 and not args.no_cpu else None
+    snap = eng.get_state() if rank == 0 and world == 1 and not args.no_cpu else None
 
     # Achievable HBM bandwidth on this box: a device-to-device copy of the same
     # number of bytes one launch moves (read + write), for context beside `peak`.
@@ -223,7 +223,7 @@ def main():
             "cpu_baseline": None,
             "multi_step": multi,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:     # the CPU baseline is an N = 1 measurement
             out["cpu_baseline"] = cpu_baseline(args, m, s, params, snap, single_steps)
         print(json.dumps(out), flush=True)
     eng.close()
@@ -396,7 +396,7 @@ def bench_learner(args, world, rank, torch, dist):
                          "note": "whole learning step (all kernels) timed with HIP events"},
             "cpu_baseline": None,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline_learner(args, cfg, m, s)
         print(json.dumps(out), flush=True)
     L.close()

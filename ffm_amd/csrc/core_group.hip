@@ -42,21 +42,18 @@ namespace ffm {
 
 namespace {
 
-// Auto-reset placements are deferred to the next launch: an env emptied by step t
-// stores its count as N | kPendingPlace, and the wave that steps its group in the next
-// launch (the persistent grid maps groups to waves the same way every launch) places
-// it, keyed by t, as it stages the group -- inside the loop, where the other resident
-// waves hide it, instead of in a tail after the last group that sets the kernel's end.
-// ffm_engine_finalize_placements places what is still pending before the state is read.
-constexpr int kGroupMaxIters = 1 << 20;   // no per-wave mask any more: any grid size
+// Deferred auto-reset placements: 8 bits per group iteration (env s of the wave's
+// i-th group = bit 8 i + s), so a wave steps at most kGroupMaxIters groups.
+constexpr int kGroupMaxIters = 16;
+constexpr int kGroupPendWords = 8 * kGroupMaxIters / 32;
 
 struct GroupCarve {
-    size_t grid, tile, words, posst, kp, keys, per_wave;
+    size_t grid, tile, words, posst, kp, keys, pend, per_wave;
 };
 
 // The staged positions are dead once the agents are marked, so the kept-prefix
-// array reuses them; the placement keys are used only while a group is staged,
-// before its grid is marked, so they reuse the grids (rebuilt after a placement).
+// array reuses them; the placement keys are used only after the step loop, so
+// they reuse the grids and tiles.
 template <int G>
 __host__ __device__ inline GroupCarve group_carve(int PHW, int TS, int F) {
     GroupCarve c;
@@ -69,6 +66,7 @@ __host__ __device__ inline GroupCarve group_carve(int PHW, int TS, int F) {
     c.words = o; o += (size_t)G * 32 * 4;
     c.posst = o;
     c.kp = o;    o += a16((size_t)(G * 32 + 1) * 2);
+    c.pend = o;  o += kGroupPendWords * 4;
     c.per_wave = a16(o);
     return c;
 }
@@ -125,7 +123,7 @@ void core_group_kernel(CoreStepArgs a) {
     const uint16_t* const posst = reinterpret_cast<const uint16_t*>(wbase + cv.posst);
     uint16_t* const kp = reinterpret_cast<uint16_t*>(wbase + cv.kp);
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
-    uint16_t* const posst16 = reinterpret_cast<uint16_t*>(wbase + cv.posst);
+    uint32_t* const pend = reinterpret_cast<uint32_t*>(wbase + cv.pend);
 
     // The lane's DFF float4 slots: q = 64 k + lane of the group's G * HW cells,
     // env q / Q4, cell 4 (q % Q4) of that env.
@@ -178,13 +176,15 @@ void core_group_kernel(CoreStepArgs a) {
     }
     for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
     for (int i = lane; i < G * TS; i += 64) tile[i] = 0.0f;
+    if (lane < kGroupPendWords) pend[lane] = 0u;
     __syncthreads();
     for (int i = lane; i < G * PHW; i += 64) grid[i] = pmap[i % PHW];
     wave_sync();
 
     unsigned c_steps = 0, c_exits = 0, c_resets = 0;
     constexpr uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W, c < 2^16
-    for (; g < ngroups; g += wstride) {
+    const int g_first = g;
+    for (int iter = 0; g < ngroups; g += wstride, iter++) {
         const long long e0 = (long long)g * G;
         const int nenv = (int)min((long long)G, E - e0);
 
@@ -194,21 +194,6 @@ void core_group_kernel(CoreStepArgs a) {
             if (toff[k] >= 0) *reinterpret_cast<float4*>(tile + toff[k]) = cur.d[k];
         if (lane < PWORDS) posst32[lane] = cur.p0;
         if (PWORDS > 64 && 64 + lane < PWORDS) posst32[64 + lane] = cur.p1;
-        {
-            // placements deferred by the previous launch (rare, wave-uniform): the N agents
-            // of an env emptied by step t - 1, keyed by that step, into the staged positions
-            const unsigned long long pm = __ballot(lane < G && cur.c < 0);
-            if (pm) {
-                CoreStepArgs ap = a;
-                ap.t = a.t - 1u;
-                wave_sync();
-                for (int s = 0; s < G; s++)
-                    if ((pm >> s) & 1ull)
-                        wave_reset_env(ap, ebase + (uint32_t)(e0 + s), keys, pfree, posst16 + s * A, lane);
-                for (int i = lane; i < G * PHW; i += 64) grid[i] = pmap[i % PHW];   // the keys overlaid it
-                cur.c = cur.c < 0 ? a.N : cur.c;
-            }
-        }
         int S[G + 1];   // exclusive prefix of the counts (wave-uniform)
         S[0] = 0;
 #pragma unroll
@@ -368,12 +353,12 @@ void core_group_kernel(CoreStepArgs a) {
         const int nk = (int)kp[Sh] - (int)kp[Sl];
         const bool rs = a.auto_reset && lane < nenv && nk == 0;
         const unsigned long long rsm = __ballot(rs);
-        // an emptied env: N agents to place at the next launch's first touch, keyed by this t
-        __builtin_amdgcn_raw_buffer_store_b32(rs ? ((unsigned)a.N | kPendingPlace) : (unsigned)nk,
-                                              pair_rsrc(a.cnt + e0, nenv * 4), lane < G ? lane * 4 : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)(rs ? a.N : nk), pair_rsrc(a.cnt + e0, nenv * 4),
+                                              lane < G ? lane * 4 : kOOB, 0, 0);
         if (rsm) {   // wave-uniform, rare
             c_resets += (unsigned)__popcll(rsm);
             if (a.episodes && rs) a.episodes[e0 + lane] += 1;
+            if (lane == 0) pend[iter >> 2] |= (uint32_t)rsm << (8 * (iter & 3));
         }
 
         // ---- next group's HBM loads, in flight across the stencil, the stores and the
@@ -419,6 +404,20 @@ void core_group_kernel(CoreStepArgs a) {
         cur = nxt;
     }
 
+    // ---- deferred auto-reset placements ------------------------------
+    wave_sync();
+    for (int w = 0; w < kGroupPendWords; w++) {
+        uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend[w]);
+        while (m) {
+            const int bit = w * 32 + __builtin_ctz(m);
+            m &= m - 1u;
+            const long long e = (long long)(g_first + (bit >> 3) * wstride) * G + (bit & 7);
+            wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + e * A, lane);
+            if (FFM_GROUP_ABLATE & 1)   // diagnostic: the same placement again (identical result)
+                wave_reset_env(a, ebase + (uint32_t)e, keys, pfree, a.pos + e * A, lane);
+        }
+    }
+
     if (lane == 0) {
         unsigned long long* ctr = a.counters + 4 * ((size_t)blockIdx.x * 4 + wv);
         if (c_steps) atomicAdd(&ctr[0], (unsigned long long)c_steps);
@@ -455,10 +454,8 @@ static hipError_t group_op(const CoreStepArgs& a, int blocks, hipStream_t s, int
         return hipSuccess;
     }
     const long long groups = (a.E + kGroupG - 1) / kGroupG;
-    // shapes the kernel and its grid assume; the placement keys (F + 1 of 8 B) overlay the grids
-    if (a.H != 12 || a.W != 12 || a.A > 32 || (size_t)(a.F + 1) * 8 > (size_t)kGroupG * 14 * 14 * 2)
-        return hipErrorInvalidConfiguration;
-    (void)groups;
+    if (a.H != 12 || a.W != 12 || a.A > 32 || (groups + (long long)blocks * 4 - 1) / ((long long)blocks * 4) > kGroupMaxIters)
+        return hipErrorInvalidConfiguration;   // shapes the kernel and its grid assume
     core_group_kernel<NB, 12, 12, kGroupG><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
     return hipGetLastError();
 }

@@ -1015,23 +1015,6 @@ __global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
     if (threadIdx.x == 0) a.cnt[e] = a.N;
 }
 
-// Placements the group kernel deferred to the next launch (counts with kPendingPlace):
-// done here, keyed by the step that emptied the env (t - 1), before the state is read
-// or another kernel steps it.
-__global__ __launch_bounds__(64) void core_finalize_kernel(CoreStepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const long long e = blockIdx.x;
-    if (a.cnt[e] >= 0) return;                      // block-uniform
-    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
-    uint16_t* fl = reinterpret_cast<uint16_t*>(smem + align16((size_t)a.F * 8));
-    for (int i = threadIdx.x; i < a.F; i += 64) fl[i] = a.free_padded[i];
-    wave_sync();
-    CoreStepArgs ap = a;
-    ap.t = a.t - 1u;
-    wave_reset_env(ap, (uint32_t)(a.env_base + e), keys, fl, a.pos + e * a.A, threadIdx.x);
-    if (threadIdx.x == 0) a.cnt[e] = a.N;
-}
-
 // Reset every env of a map whose free list does not fit the wave reset's LDS
 // (big maps): one workgroup per env, keys in the env block's global scratch.
 __global__ __launch_bounds__(1024) void core_block_reset_kernel(CoreStepArgs a) {
@@ -1173,7 +1156,7 @@ __global__ __launch_bounds__(64) void core_capture_init_kernel(CoreStepArgs a, C
     const long long e = c.envs[i];
     c.state[3 * i] = a.episodes[e];
     c.state[3 * i + 1] = 0;
-    c.state[3 * i + 2] = a.cnt[e] & 0x7FFFFFFF;
+    c.state[3 * i + 2] = a.cnt[e];
 }
 
 __global__ __launch_bounds__(64) void core_capture_kernel(CoreStepArgs a, CoreCapture c) {
@@ -1181,7 +1164,7 @@ __global__ __launch_bounds__(64) void core_capture_kernel(CoreStepArgs a, CoreCa
     const long long e = c.envs[b];
     int* st = c.state + 3 * b;
     const int k = st[0], steps = st[1] + 1, last = st[2];
-    const int know = a.episodes[e], n = a.cnt[e] & 0x7FFFFFFF;   // a pending placement: N to come
+    const int know = a.episodes[e], n = a.cnt[e];
     const bool ended = know != k;
     const int rc = ended ? 0 : n;
     const int ph = c.phase ? c.phase[b] : 0;
@@ -1207,12 +1190,6 @@ __global__ __launch_bounds__(64) void core_capture_kernel(CoreStepArgs a, CoreCa
         st[1] = ended ? 0 : (rc == 0 && last == 0 ? st[1] : steps);
         st[2] = n;
     }
-}
-
-hipError_t launch_core_finalize(const CoreStepArgs& a, hipStream_t s) {
-    const size_t smem = align16((size_t)a.F * 8) + align16((size_t)a.F * 2);
-    core_finalize_kernel<<<dim3((unsigned)a.E), dim3(64), smem, s>>>(a);
-    return hipGetLastError();
 }
 
 hipError_t launch_core_capture_init(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s) {

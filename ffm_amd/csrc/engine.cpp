@@ -368,19 +368,10 @@ static ffm::CoreStepArgs make_args(ffm_engine* e) {
     return a;
 }
 
-// The group kernel leaves the placements of the envs its last launch emptied to the
-// next launch (counts tagged kPendingPlace); anything else that reads or steps the
-// state places them first.
-static int finalize(ffm_engine* e, hipStream_t s) {
-    if (e->group && e->d.auto_reset && !e->mt && e->t > 0) HIP_TRY(ffm::launch_core_finalize(make_args(e), s));
-    return FFM_OK;
-}
-
 int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     if (!e || n_steps < 0) return fail(FFM_E_INVALID, "bad engine/n_steps");
     hipStream_t s = (hipStream_t)stream;
     if (e->fused > 1 && e->multi && e->cap.n_sel == 0) {
-        if (int rc = finalize(e, s)) return rc;
         // k steps per launch, the state of each env pair on chip (core_multi.hip)
         for (int done = 0; done < n_steps;) {
             const int k = std::min(e->fused, n_steps - done);
@@ -456,7 +447,6 @@ int ffm_engine_set_state(ffm_engine* e, int64_t env0, int64_t n, const uint16_t*
     int rc = check_range(e, env0, n);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = finalize(e, s))) return rc;   // the envs outside [env0, env0 + n) keep their placements
     const int A = e->d.agent_capacity;
     if (counts) {
         for (int64_t i = 0; i < n; i++)
@@ -494,7 +484,6 @@ int ffm_engine_get_state(ffm_engine* e, int64_t env0, int64_t n, uint16_t* posit
     int rc = check_range(e, env0, n);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    if ((rc = finalize(e, s))) return rc;
     const int A = e->d.agent_capacity;
     if (positions)
         HIP_TRY(hipMemcpyAsync(positions, e->d_pos + env0 * A, (size_t)n * A * 2, hipMemcpyDeviceToHost, s));
@@ -616,8 +605,6 @@ int ffm_engine_get_counters(ffm_engine* e, uint64_t* counters, void* stream) {
 
 int ffm_engine_device_buffers(ffm_engine* e, ffm_device_buffers* out) {
     if (!e || !out) return fail(FFM_E_INVALID, "null argument");
-    if (int rc = finalize(e, nullptr)) return rc;   // raw readers see placed envs
-    HIP_TRY(hipDeviceSynchronize());
     out->positions = e->d_pos;
     out->counts = e->d_cnt;
     out->dff = e->d_dff;
@@ -637,8 +624,6 @@ int ffm_engine_get_step_index(ffm_engine* e, uint32_t* t) {
 
 int ffm_engine_set_step_index(ffm_engine* e, uint32_t t) {
     if (!e) return fail(FFM_E_INVALID, "null engine");
-    if (int rc = finalize(e, nullptr)) return rc;   // pending placements are keyed by the old t - 1
-    HIP_TRY(hipDeviceSynchronize());
     e->t = t;
     return FFM_OK;
 }

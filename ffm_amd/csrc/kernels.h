@@ -48,10 +48,6 @@ struct CoreCapture {
     int n_sel, period;
 };
 
-// A count with this bit set (group kernel): the env was emptied by the previous step and
-// its N agents are still to be placed, keyed by that step (core_group.hip).
-constexpr uint32_t kPendingPlace = 0x80000000u;
-
 size_t core_wave_smem_bytes(int H, int W, int A, int F, bool mt, bool reset, int waves);
 size_t core_block_smem_bytes(int H, int W, int A, int K, int F, bool f64, bool mt, bool reset);
 hipError_t launch_core_wave(const CoreStepArgs& a, int nb, bool mt, int blocks, hipStream_t s);
@@ -75,7 +71,6 @@ size_t core_big_scratch_bytes(int H, int W, int A, int F, bool mt);
 hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,
                              float c1, hipStream_t s);
-hipError_t launch_core_finalize(const CoreStepArgs& a, hipStream_t s);
 hipError_t launch_core_capture_init(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s);
 hipError_t launch_core_capture(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s);
 hipError_t launch_np_expf(const float* x, float* y, long long n, hipStream_t s);

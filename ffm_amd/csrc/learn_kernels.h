@@ -29,7 +29,7 @@ struct TileRec {
     uint32_t snf;               // V slot of s' (bits 0-27; 0x0FFFFFFF = terminal), wexit (28), coll + 1 (29-31)
     double td;                  // TD error with the step-start V (ffm_unified both: the actor's td)
 };
-constexpr int kTileCells = 8;   // cells per tile: a tile's slots are 256 rank patterns x 8 cells
+constexpr int kTileCells = 4;   // cells per tile: a tile's slots are 256 rank patterns x 4 cells
 constexpr uint32_t kTileNoAct = 15u, kTileTerminal = 0x0FFFFFFFu;
 
 struct LearnTable {

@@ -1765,16 +1765,17 @@ __global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
 
 // ===========================================================================
 // Tiled learning step (ffm_unified, dense tables, block size 1).
-// Tile t = cells [8 t, 8 t + 8) owns the slots p * Q + c of those cells for every
-// rank pattern p (Q = cap / 256), 2,048 slots.  One workgroup per tile reads the
+// Tile t = cells [4 t, 4 t + 4) owns the slots p * Q + c of those cells for every
+// rank pattern p (Q = cap / 256), 1,024 slots.  One workgroup per tile reads the
 // records of every env's agents on those cells (a contiguous raster range per env,
 // learn_batch_kernel's tstart) and sums them in LDS: no atomic leaves the chip, and
 // only touched slots are read and written.  The integer sums are those the
 // accumulators held, so the tables equal the accumulator path's bit for bit.
 // ===========================================================================
-// 1,024 threads per tile, two per env: every env's record range of the tile is
-// split between a thread pair (the LDS of the H pass allows one workgroup per CU).
-constexpr int kTileThreads = 1024, kTileWaves = kTileThreads / 64;
+// 256 threads per tile, two per env: every env's record range of the tile is split
+// between a thread pair.  Small tiles and workgroups keep several tiles resident per CU
+// (H pass: 40 KB of LDS), so one tile's dependent loads overlap another's.
+constexpr int kTileThreads = 256, kTileWaves = kTileThreads / 64;
 
 __device__ __forceinline__ int tile_idx(uint32_t slot, int qsh, uint32_t Q, int c0) {
     return (int)(slot >> qsh) * kTileCells + (int)((slot & (Q - 1u)) - (uint32_t)c0);

@@ -94,7 +94,7 @@ class TableSync:
       large map -- with equal env counts on every rank, at K = 1): every rank all-gathers
       the others' per-agent records (16 B each) and tile offsets and sums them per tile of
       cells into its replicated tables: the exchange is proportional to the
-      agents stepped, not to the table (C5: 84 MB per rank per step instead of 940 MB of
+      agents stepped, not to the table (C5: about 100 MB per rank per step instead of 940 MB of
       accumulators);
     * ``sync_period`` K: the tables are applied (and exchanged) every K-th step only,
       the increments of K steps accumulating in between
