@@ -94,6 +94,8 @@ struct ffm_learner {
     ffm::TileRec* d_trecs = nullptr;
     int* d_tstart = nullptr;
     double* d_tstats = nullptr;
+    int* d_tdirty = nullptr;
+    int* d_tcand = nullptr;
     DevTable V, H;
 };
 
@@ -117,7 +119,7 @@ static void release(ffm_learner* l) {
     void* bufs[] = {l->d_map, l->d_map2, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
-                    l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats};
+                    l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
     free_traj(l);
@@ -208,6 +210,8 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.trecs = nullptr;       // the accumulator path unless a tiled step sets it
     a.tstart = l->d_tstart;
     a.tstats = l->d_tstats;
+    a.tdirty = l->d_tdirty;
+    a.tcand = l->d_tcand;
     a.NT = l->NT;
     a.tile_ensure = 0;
     return a;
@@ -397,7 +401,10 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         l->NT = (HW + ffm::kTileCells - 1) / ffm::kTileCells;
         if (hipMalloc((void**)&l->d_trecs, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
             hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 4) != hipSuccess ||
-            hipMalloc((void**)&l->d_tstats, (size_t)l->NT * 32) != hipSuccess)
+            hipMalloc((void**)&l->d_tstats, (size_t)l->NT * 32) != hipSuccess ||
+            hipMalloc((void**)&l->d_tdirty, (size_t)l->NT * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_tcand, (size_t)(l->NT + 1) * 4) != hipSuccess ||
+            hipMemset(l->d_tdirty, 0, (size_t)l->NT * 4) != hipSuccess)
             return cleanup(fail(FFM_E_NOMEM, "hipMalloc (tiled step)"));
     }
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);

@@ -100,6 +100,8 @@ struct LearnArgs {
     TileRec* trecs;             // [E][A] tiled step: per-agent records in raster order (nullptr: off)
     int* tstart;                // [E][NT + 1] tiled step: agents of env e in cells < kTileCells * t
     double* tstats;             // [NT][4] tiled step: per-tile H summary (present, non-finite, min, max)
+    int* tdirty;                // [NT] tiled step: bit 0 max, 1 min, 2 non-finite flag only a bound (stale)
+    int* tcand;                 // [NT + 1] tiled step: tiles to rescan ([0] = count, then the tiles)
     int NT;                     // tiles: ceil(HW / kTileCells)
     int tile_ensure;            // tile kernels: insert the records' slots (records gathered from other ranks)
     int* overflow;              // [1] table full / reset capacity exceeded

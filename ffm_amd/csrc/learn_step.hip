@@ -1093,9 +1093,6 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 #ifndef FFM_LABLATE
 #define FFM_LABLATE 0
 #endif
-#ifndef FFM_VEARLY
-#define FFM_VEARLY 0   // ffm_actor_only: probe V(s) at decide (A/B switch)
-#endif
 // FFM_LSTAMP (diagnostic builds): thread 0 of blocks 0 and gridDim/2 prints the
 // wall-clock ticks (100 MHz) of each phase of the batched step.
 #ifndef FFM_LSTAMP
@@ -1301,11 +1298,10 @@ void learn_batch_kernel(LearnArgs a) {
     // ---- decide --------------------------------------------------------------
     unsigned long long skey[APT];
     int act[APT], avalid[APT], wexit[APT], hsl[APT];
-    int vse[APT];        // FFM_VEARLY: the V slot of s, probed at decide beside the H probe
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = ia[j];
-        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0; vse[j] = -1;
+        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
         if (tid + j * LPE >= n) continue;
         const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
         skey[j] = encode(a, smc, x, y);
@@ -1366,9 +1362,6 @@ void learn_batch_kernel(LearnArgs a) {
             // first exit, then the exit for the rest; the last one is the agent's action.
             if (ex != 0) {
                 hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
-                // the learning phase's V(s) probe, independent of the H row: its loads overlap
-                // the H probe and the policy math instead of trailing the resolve
-                if (FFM_VEARLY) vse[j] = tab_get(a.V, skey[j], a.overflow);
                 if (hsl[j] < 0) continue;
                 actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, true, P);
             }
@@ -1484,7 +1477,7 @@ void learn_batch_kernel(LearnArgs a) {
                 sv = (int)dense_slot(skey[j], a.V);
                 dense_ensure(a.V, (uint32_t)sv, skey[j]);
             } else {
-                sv = vse[j] >= 0 ? vse[j] : tab_get(a.V, skey[j], a.overflow);
+                sv = tab_get(a.V, skey[j], a.overflow);
             }
             if (sv < 0) break;
             const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
@@ -1824,110 +1817,14 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     }
 }
 
-// H: the actor increments (actor_only: the TD error with the updated V, like
-// learn_post_kernel; both: the step's td), applied at once, and the tile's summary of
-// the H statistics (present, non-finite, min, max) for the next step.  The summary
-// is updated from the touched rows unless a touched value held the tile's old min or
-// max and moved inward (or was non-finite): then the tile's present rows are rescanned.
-// stats_only: no records, rescan (statistics of an imported / cleared table).
-__global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a, int stats_only) {
+// Exact min / max / non-finite of one tile's present H rows (a block-wide scan).
+__device__ void tile_rescan(const LearnArgs& a, int t, double* smn, double* smx, int* sfl) {
     constexpr int NS = 256 * kTileCells;
-    __shared__ long long hq[NS * 5];
-    __shared__ uint32_t touched[NS / 32];
-    __shared__ double smn[kTileWaves], smx[kTileWaves];
-    __shared__ int sfl[kTileWaves];
-    const int t = (int)blockIdx.x, tid = (int)threadIdx.x;
-    const bool post_update = a.mode == kModeActor;
+    const int tid = (int)threadIdx.x, wv = tid >> 6;
     const uint32_t Q = (a.Ht.mask + 1u) >> 8;
-    const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
-    double* ts = a.tstats + 4 * t;
-    const double omn = ts[2], omx = ts[3];
-    const bool onf = ts[1] != 0.0;
-    int flags = 0;                      // 1 non-finite, 2 rescan, 4 any row
-    double mn = __builtin_inf(), mx = -__builtin_inf();
-    if (!stats_only) {
-        for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
-        for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
-        __syncthreads();
-        for (long long w = tid; w < 2 * a.E; w += kTileThreads) {
-            const long long e = w >> 1;
-            const int* tsr = a.tstart + e * (a.NT + 1) + t;
-            const int lo = tsr[0], hi = tsr[1];
-            for (int r = lo + (int)(w & 1); r < hi; r += 2) {
-                const TileRec rc = a.trecs[e * a.A + r];
-                const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-                const int idx = tile_idx(sv, qsh, Q, c0);
-                atomicOr(&touched[idx >> 5], 1u << (idx & 31));
-                if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
-                const int k = (int)(rc.svk >> 28);
-                if (k == (int)kTileNoAct) continue;
-                double td = rc.td;
-                if (post_update) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
-                    double r0 = a.step_penalty;
-                    if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
-                    const int coll = (int)(rc.snf >> 29) - 1;
-                    if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
-                    const uint32_t sn = rc.snf & 0x0FFFFFFFu;
-                    const double vn = sn != kTileTerminal ? tval(a.V, sn)[0] : 0.0;
-                    td = (r0 + a.gamma * vn) - tval(a.V, sv)[0];
-                }
-                atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]),
-                          (unsigned long long)fx(a.alpha_h * td));
-            }
-        }
-        __syncthreads();
-        for (int i = tid; i < NS; i += kTileThreads) {
-            if (!((touched[i >> 5] >> (i & 31)) & 1u)) continue;
-            double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
-            flags |= 4;
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-                const long long q = hq[i * 5 + k];
-                const double old = vp[k];
-                double v = old;
-                if (q != 0) {
-                    v = v + (double)q * (1.0 / kFxOne);
-                    vp[k] = v;
-                    // a value that held the tile's extreme moved inward (or off / to non-finite)
-                    if ((old == omx && !(v >= old)) || (old == omn && !(v <= old)) || !__builtin_isfinite(old))
-                        flags |= 2;
-                }
-                flags |= __builtin_isfinite(v) ? 0 : 1;
-                mn = v < mn ? v : mn;
-                mx = v > mx ? v : mx;
-            }
-        }
-    }
-    // block reduction of the touched rows' summary
-    for (int o = 32; o > 0; o >>= 1) {
-        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
-        mn = a2 < mn ? a2 : mn;
-        mx = b2 > mx ? b2 : mx;
-        flags |= __shfl_xor(flags, o);
-    }
-    const int wv = tid >> 6;
-    if ((tid & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sfl[wv] = flags; }
-    __syncthreads();
-    mn = smn[0]; mx = smx[0]; flags = sfl[0];
-    for (int w = 1; w < kTileWaves; w++) {
-        mn = smn[w] < mn ? smn[w] : mn;
-        mx = smx[w] > mx ? smx[w] : mx;
-        flags |= sfl[w];
-    }
-    const bool rescan = stats_only || (flags & 2) || (onf && (flags & 4));
-    if (!rescan) {
-        if (tid == 0) {
-            ts[0] = (ts[0] != 0.0 || (flags & 4)) ? 1.0 : 0.0;
-            ts[1] = (onf || (flags & 1)) ? 1.0 : 0.0;
-            ts[2] = omn < mn ? omn : mn;
-            ts[3] = omx > mx ? omx : mx;
-        }
-        return;
-    }
-    __syncthreads();               // every wave has read the old summary and the shared partials
+    const int c0 = t * kTileCells;
     int nf = 0, any = 0;
-    mn = __builtin_inf();
-    mx = -__builtin_inf();
+    double mn = __builtin_inf(), mx = -__builtin_inf();
     for (int i = tid; i < NS; i += kTileThreads) {
         const size_t slot = (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells);
         if (!((a.Ht.present[slot >> 5] >> (slot & 31)) & 1u)) continue;
@@ -1948,6 +1845,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a,
         nf |= __shfl_xor(nf, o);
         any |= __shfl_xor(any, o);
     }
+    __syncthreads();
     if ((tid & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sfl[wv] = nf | (any << 1); }
     __syncthreads();
     if (tid == 0) {
@@ -1957,14 +1855,162 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a,
             mx = smx[w] > mx ? smx[w] : mx;
             f |= sfl[w];
         }
+        double* ts = a.tstats + 4 * t;
         ts[0] = (f & 2) ? 1.0 : 0.0;
         ts[1] = (f & 1) ? 1.0 : 0.0;
         ts[2] = mn;
         ts[3] = mx;
+        a.tdirty[t] = 0;
     }
 }
 
-// The tiles' summaries -> the statistics the next step's actor reads (hstat).
+// H: the actor increments (actor_only: the TD error with the updated V, like
+// learn_post_kernel; both: the step's td), applied at once, and the tile's summary of
+// the H statistics (present, non-finite, min, max) for the next step.  The summary is
+// widened by the touched rows' new values; when a touched value held the tile's min or
+// max and moved inward, the old extreme stays as a bound and the tile is marked stale
+// (tdirty): learn_tile_cand_kernel rescans only the stale tiles whose bound could
+// decide the table's min or max.
+__global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a) {
+    constexpr int NS = 256 * kTileCells;
+    __shared__ long long hq[NS * 5];
+    __shared__ uint32_t touched[NS / 32];
+    __shared__ double smn[kTileWaves], smx[kTileWaves];
+    __shared__ int sfl[kTileWaves];
+    const int t = (int)blockIdx.x, tid = (int)threadIdx.x;
+    const bool post_update = a.mode == kModeActor;
+    const uint32_t Q = (a.Ht.mask + 1u) >> 8;
+    const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
+    double* ts = a.tstats + 4 * t;
+    const double omn = ts[2], omx = ts[3];
+    const bool onf = ts[1] != 0.0;
+    int flags = 0;                      // 1 non-finite, 2 max stale, 4 any row, 8 min stale, 16 nf stale
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
+    for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
+    __syncthreads();
+    for (long long w = tid; w < 2 * a.E; w += kTileThreads) {
+        const long long e = w >> 1;
+        const int* tsr = a.tstart + e * (a.NT + 1) + t;
+        const int lo = tsr[0], hi = tsr[1];
+        for (int r = lo + (int)(w & 1); r < hi; r += 2) {
+            const TileRec rc = a.trecs[e * a.A + r];
+            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+            const int idx = tile_idx(sv, qsh, Q, c0);
+            atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+            if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
+            const int k = (int)(rc.svk >> 28);
+            if (k == (int)kTileNoAct) continue;
+            double td = rc.td;
+            if (post_update) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
+                double r0 = a.step_penalty;
+                if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
+                const int coll = (int)(rc.snf >> 29) - 1;
+                if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
+                const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+                const double vn = sn != kTileTerminal ? tval(a.V, sn)[0] : 0.0;
+                td = (r0 + a.gamma * vn) - tval(a.V, sv)[0];
+            }
+            atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]),
+                      (unsigned long long)fx(a.alpha_h * td));
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < NS; i += kTileThreads) {
+        if (!((touched[i >> 5] >> (i & 31)) & 1u)) continue;
+        double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+        flags |= 4;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const long long q = hq[i * 5 + k];
+            const double old = vp[k];
+            double v = old;
+            if (q != 0) {
+                v = v + (double)q * (1.0 / kFxOne);
+                vp[k] = v;
+                if (old == omx && !(v >= old)) flags |= 2;    // the max moved inward (or to NaN)
+                if (old == omn && !(v <= old)) flags |= 8;
+                if (!__builtin_isfinite(old)) flags |= 16;
+            }
+            flags |= __builtin_isfinite(v) ? 0 : 1;
+            mn = v < mn ? v : mn;
+            mx = v > mx ? v : mx;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
+        mn = a2 < mn ? a2 : mn;
+        mx = b2 > mx ? b2 : mx;
+        flags |= __shfl_xor(flags, o);
+    }
+    const int wv = tid >> 6;
+    if ((tid & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sfl[wv] = flags; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kTileWaves; w++) {
+            mn = smn[w] < mn ? smn[w] : mn;
+            mx = smx[w] > mx ? smx[w] : mx;
+            flags |= sfl[w];
+        }
+        // the old extremes stay as bounds (a value that left them is only inward)
+        ts[0] = (ts[0] != 0.0 || (flags & 4)) ? 1.0 : 0.0;
+        ts[1] = (onf || (flags & 1)) ? 1.0 : 0.0;
+        ts[2] = omn < mn ? omn : mn;
+        ts[3] = omx > mx ? omx : mx;
+        a.tdirty[t] |= ((flags & 2) ? 1 : 0) | ((flags & 8) ? 2 : 0) | ((flags & 16) ? 4 : 0);
+    }
+}
+
+// The tiles to rescan: a stale tile matters only if its bound could be the table's
+// extreme -- its max bound above every exact tile max (or its min bound below every
+// exact min), or a non-finite flag that may be stale.  all: every tile (statistics of
+// an imported / cleared table).
+__global__ __launch_bounds__(1024) void learn_tile_cand_kernel(LearnArgs a, int all) {
+    __shared__ double smn[16], smx[16];
+    __shared__ int ncand;
+    const int tid = (int)threadIdx.x;
+    if (tid == 0) ncand = 0;
+    double cmn = __builtin_inf(), cmx = -__builtin_inf();   // over exact (clean) tiles
+    if (!all) {
+        for (int t = tid; t < a.NT; t += 1024) {
+            const double* ts = a.tstats + 4 * t;
+            const int d = a.tdirty[t];
+            if (ts[0] == 0.0) continue;
+            if (!(d & 1)) cmx = ts[3] > cmx ? ts[3] : cmx;
+            if (!(d & 2)) cmn = ts[2] < cmn ? ts[2] : cmn;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(cmn, o), b2 = __shfl_xor(cmx, o);
+        cmn = a2 < cmn ? a2 : cmn;
+        cmx = b2 > cmx ? b2 : cmx;
+    }
+    if ((tid & 63) == 0) { smn[tid >> 6] = cmn; smx[tid >> 6] = cmx; }
+    __syncthreads();
+    for (int w = 0; w < 16; w++) {
+        cmn = smn[w] < cmn ? smn[w] : cmn;
+        cmx = smx[w] > cmx ? smx[w] : cmx;
+    }
+    for (int t = tid; t < a.NT; t += 1024) {
+        const double* ts = a.tstats + 4 * t;
+        const int d = a.tdirty[t];
+        const bool c = all || (ts[0] != 0.0 && (((d & 1) && ts[3] >= cmx) || ((d & 2) && ts[2] <= cmn) ||
+                                                ((d & 4) && ts[1] != 0.0)));
+        if (c) a.tcand[1 + atomicAdd(&ncand, 1)] = t;
+    }
+    __syncthreads();
+    if (tid == 0) a.tcand[0] = ncand;
+}
+
+__global__ __launch_bounds__(kTileThreads) void learn_tile_rescan_kernel(LearnArgs a) {
+    __shared__ double smn[kTileWaves], smx[kTileWaves];
+    __shared__ int sfl[kTileWaves];
+    const int n = a.tcand[0];
+    for (int c = (int)blockIdx.x; c < n; c += (int)gridDim.x) tile_rescan(a, a.tcand[1 + c], smn, smx, sfl);
+}
+
+// The tiles' summaries -> the statistics the next step's actor reads (hstat).  After
+// learn_tile_rescan_kernel, a stale tile's bound is never the table's extreme.
 __global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
     __shared__ double smn[4], smx[4];
     __shared__ int snf[4];
@@ -2431,14 +2477,18 @@ bool learn_batch_raster(int HW, int A, int D) {
 // init_stats, only the per-tile statistics of the current H (no records).
 hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s) {
     const bool actor = a.mode != kModeCritic;
+    const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
     if (init_stats) {
-        learn_tile_h_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a, 1);
+        learn_tile_cand_kernel<<<dim3(1), dim3(1024), 0, s>>>(a, 1);
+        learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
         return hipGetLastError();
     }
     learn_tile_v_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a);
     if (actor) {
-        learn_tile_h_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a, 0);
+        learn_tile_h_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a);
+        learn_tile_cand_kernel<<<dim3(1), dim3(1024), 0, s>>>(a, 0);
+        learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
     return hipGetLastError();

@@ -7,7 +7,7 @@ from collections import defaultdict
 skip = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 d = defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
-    name = r["Kernel_Name"].split("(")[0].replace("ffm::(anonymous namespace)::", "").replace("void ", "")
+    name = r["Kernel_Name"].replace("ffm::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
     d[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
 for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
     w = v[skip:] if len(v) > skip else v
