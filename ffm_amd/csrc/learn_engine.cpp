@@ -395,7 +395,8 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     {
         const char* ev = getenv("FFM_TILED");
         l->tiled_ok = !l->mt && d.variant == FFM_VARIANT_UNIFIED && dense_by && learn->block_size == 1 &&
-                      ffm::learn_batch_raster(HW, d.agent_capacity, l->D) && !(ev && ev[0] == '0');
+                      ffm::learn_batch_raster(HW, d.agent_capacity, l->D) && !(ev && ev[0] == '0') &&
+                      (unsigned long long)E * (unsigned long long)A < (1ull << 31);
     }
     if (l->tiled_ok) {
         l->NT = (HW + ffm::kTileCells - 1) / ffm::kTileCells;
@@ -904,6 +905,8 @@ int ffm_learner_step_tiled_local(ffm_learner* l, void* stream) {
 int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const int32_t* d_tstart_all,
                                  int64_t n_envs_all, void* stream) {
     if (!l || !d_recs_all || !d_tstart_all || n_envs_all < 1) return fail(FFM_E_INVALID, "bad argument");
+    if ((unsigned long long)n_envs_all * (unsigned long long)l->d.agent_capacity >= (1ull << 32))   // 32-bit record indices
+        return fail(FFM_E_INVALID, "tiled step: n_envs_all * agent_capacity >= 2^32");
     if (l->phase != 5) return fail(FFM_E_INVALID, "step_tiled_apply must follow step_tiled_local");
     hipStream_t s = (hipStream_t)stream;
     ffm::LearnArgs a = make_args(l);

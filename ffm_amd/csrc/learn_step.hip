@@ -1774,6 +1774,71 @@ __device__ __forceinline__ int tile_idx(uint32_t slot, int qsh, uint32_t Q, int 
     return (int)(slot >> qsh) * kTileCells + (int)((slot & (Q - 1u)) - (uint32_t)c0);
 }
 
+// XCD-aware tile order: blocks b and b + 8 share an XCD (dealt round-robin), so block b
+// takes tile (b % 8) * per + b / 8 and each XCD walks its own contiguous run of tiles.
+// Adjacent tiles share the lines of tstart rows, record ranges and table rows; in one
+// L2 those lines are fetched once instead of once per XCD.  Grid: 8 * per blocks.
+__device__ __forceinline__ int tile_of_block(int NT) {
+    const int per = (NT + 7) >> 3, b = (int)blockIdx.x;
+    return (b & 7) * per + (b >> 3);
+}
+
+constexpr int kTileEnvChunk = 2 * kTileThreads;   // envs whose ranges one pass gathers
+constexpr int kTileList = 4 * kTileThreads;       // record indices per window
+
+// Calls f(g) for every record g (an index into trecs) of tile t's cells.  The record
+// ranges of 512 envs at a time (tstart) are loaded together, a block scan places them in
+// one flat list, and the records are dealt evenly over the threads: one dependent chain
+// (range, record, table reads) per record instead of one per env in turn.  A cell holds
+// at most one agent, so a pass holds <= 4 * 512 records: two windows at most.
+template <typename F>
+__device__ __forceinline__ void tile_records(const LearnArgs& a, int t, uint32_t* list, int* wsum, F f) {
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (long long e0 = 0; e0 < a.E; e0 += kTileEnvChunk) {
+        int lo[2], n[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const long long e = e0 + tid + j * kTileThreads;
+            lo[j] = 0;
+            n[j] = 0;
+            if (e < a.E) {
+                const int* ts = a.tstart + e * (a.NT + 1) + t;
+                lo[j] = ts[0];
+                n[j] = ts[1] - lo[j];
+            }
+        }
+        const int c = n[0] + n[1];
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int off = incl - c, total = 0;
+#pragma unroll
+        for (int w = 0; w < kTileWaves; w++) {
+            off += w < wv ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        for (int b = 0; b < total; b += kTileList) {
+            int o = off - b;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const uint32_t g0 = (uint32_t)((e0 + tid + j * kTileThreads) * a.A + lo[j]);
+                for (int i = 0; i < n[j]; i++, o++)
+                    if (o >= 0 && o < kTileList) list[o] = g0 + (uint32_t)i;
+            }
+            __syncthreads();
+            const int m = total - b < kTileList ? total - b : kTileList;
+            for (int i = tid; i < m; i += kTileThreads) f(list[i]);
+            __syncthreads();
+        }
+        __syncthreads();    // wsum is rewritten by the next pass
+    }
+}
+
 // The rank key of a dense slot (inverse of dense_slot): ranks in bits 0-7, bx, by.
 __device__ __forceinline__ unsigned long long dense_key(uint32_t slot, int qsh, uint32_t Q, uint32_t by) {
     const uint32_t b = slot & (Q - 1u);
@@ -1786,34 +1851,40 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     constexpr int NS = 256 * kTileCells;
     __shared__ long long qs[NS];
     __shared__ uint32_t ks[NS];
-    const int t = (int)blockIdx.x, tid = (int)threadIdx.x;
+    __shared__ uint32_t list[kTileList];
+    __shared__ int wsum[kTileWaves];
+    const int t = tile_of_block(a.NT), tid = (int)threadIdx.x;
+    if (t >= a.NT) return;
     for (int i = tid; i < NS; i += kTileThreads) { qs[i] = 0; ks[i] = 0u; }
     __syncthreads();
     const uint32_t Q = (a.V.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
-    for (long long w = tid; w < 2 * a.E; w += kTileThreads) {
-        const long long e = w >> 1;
-        const int* ts = a.tstart + e * (a.NT + 1) + t;
-        const int lo = ts[0], hi = ts[1];
-        for (int r = lo + (int)(w & 1); r < hi; r += 2) {
-            const TileRec rc = a.trecs[e * a.A + r];
-            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-            const int idx = tile_idx(sv, qsh, Q, c0);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(rc.td));
-            atomicAdd(&ks[idx], 1u);
-            if (a.tile_ensure) {     // another rank's agent: its s and s' join this rank's V
-                dense_ensure(a.V, sv, dense_key(sv, qsh, Q, a.V.dense_by));
-                const uint32_t sn = rc.snf & 0x0FFFFFFFu;
-                if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
-            }
+    tile_records(a, t, list, wsum, [&](uint32_t g) {
+        const TileRec rc = a.trecs[g];
+        const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+        const int idx = tile_idx(sv, qsh, Q, c0);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(rc.td));
+        atomicAdd(&ks[idx], 1u);
+        if (a.tile_ensure) {     // another rank's agent: its s and s' join this rank's V
+            dense_ensure(a.V, sv, dense_key(sv, qsh, Q, a.V.dense_by));
+            const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+            if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
         }
+    });
+    constexpr int kPer = NS / kTileThreads;
+    double vv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {    // the loads first (one latency, not four)
+        const int i = tid + j * kTileThreads;
+        if (ks[i]) vv[j] = tval(a.V, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells))[0];
     }
-    __syncthreads();
-    for (int i = tid; i < NS; i += kTileThreads) {
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * kTileThreads;
         const uint32_t k = ks[i];
         if (!k) continue;
         double* vp = tval(a.V, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
-        vp[0] = v_visits(vp[0], qs[i], (long long)k, a.V.alpha);
+        vp[0] = v_visits(vv[j], qs[i], (long long)k, a.V.alpha);
     }
 }
 
@@ -1877,7 +1948,10 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     __shared__ uint32_t touched[NS / 32];
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
-    const int t = (int)blockIdx.x, tid = (int)threadIdx.x;
+    __shared__ uint32_t list[kTileList];
+    __shared__ int wsum[kTileWaves];
+    const int t = tile_of_block(a.NT), tid = (int)threadIdx.x;
+    if (t >= a.NT) return;
     const bool post_update = a.mode == kModeActor;
     const uint32_t Q = (a.Ht.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
@@ -1889,41 +1963,50 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
     for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
     __syncthreads();
-    for (long long w = tid; w < 2 * a.E; w += kTileThreads) {
-        const long long e = w >> 1;
-        const int* tsr = a.tstart + e * (a.NT + 1) + t;
-        const int lo = tsr[0], hi = tsr[1];
-        for (int r = lo + (int)(w & 1); r < hi; r += 2) {
-            const TileRec rc = a.trecs[e * a.A + r];
-            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-            const int idx = tile_idx(sv, qsh, Q, c0);
-            atomicOr(&touched[idx >> 5], 1u << (idx & 31));
-            if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
-            const int k = (int)(rc.svk >> 28);
-            if (k == (int)kTileNoAct) continue;
-            double td = rc.td;
-            if (post_update) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
-                double r0 = a.step_penalty;
-                if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
-                const int coll = (int)(rc.snf >> 29) - 1;
-                if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
-                const uint32_t sn = rc.snf & 0x0FFFFFFFu;
-                const double vn = sn != kTileTerminal ? tval(a.V, sn)[0] : 0.0;
-                td = (r0 + a.gamma * vn) - tval(a.V, sv)[0];
-            }
-            atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]),
-                      (unsigned long long)fx(a.alpha_h * td));
+    tile_records(a, t, list, wsum, [&](uint32_t g) {
+        const TileRec rc = a.trecs[g];
+        const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+        const int idx = tile_idx(sv, qsh, Q, c0);
+        atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+        if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
+        const int k = (int)(rc.svk >> 28);
+        if (k == (int)kTileNoAct) return;
+        double td = rc.td;
+        if (post_update) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
+            double r0 = a.step_penalty;
+            if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
+            const int coll = (int)(rc.snf >> 29) - 1;
+            if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
+            const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+            const double vn = sn != kTileTerminal ? tval(a.V, sn)[0] : 0.0;
+            td = (r0 + a.gamma * vn) - tval(a.V, sv)[0];
+        }
+        atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]), (unsigned long long)fx(a.alpha_h * td));
+    });
+    // every touched row's loads are issued before the first is used (one latency, not four)
+    constexpr int kPer = NS / kTileThreads;
+    double hv[kPer][5];
+    bool tch[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * kTileThreads;
+        tch[j] = (touched[i >> 5] >> (i & 31)) & 1u;
+        if (tch[j]) {
+            const double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+#pragma unroll
+            for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
         }
     }
-    __syncthreads();
-    for (int i = tid; i < NS; i += kTileThreads) {
-        if (!((touched[i >> 5] >> (i & 31)) & 1u)) continue;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        if (!tch[j]) continue;
+        const int i = tid + j * kTileThreads;
         double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
         flags |= 4;
 #pragma unroll
         for (int k = 0; k < 5; k++) {
             const long long q = hq[i * 5 + k];
-            const double old = vp[k];
+            const double old = hv[j][k];
             double v = old;
             if (q != 0) {
                 v = v + (double)q * (1.0 / kFxOne);
@@ -1964,20 +2047,41 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
 // The tiles to rescan: a stale tile matters only if its bound could be the table's
 // extreme -- its max bound above every exact tile max (or its min bound below every
 // exact min), or a non-finite flag that may be stale.  all: every tile (statistics of
-// an imported / cleared table).
-__global__ __launch_bounds__(1024) void learn_tile_cand_kernel(LearnArgs a, int all) {
-    __shared__ double smn[16], smx[16];
+// an imported / cleared table).  hpart[0..2] keeps the exact extremes and the
+// non-finite flag of the tiles not rescanned for learn_tile_final_kernel.
+constexpr int kCandThreads = 1024, kCandUnroll = 4;
+
+__device__ __forceinline__ void tile_summary(const LearnArgs& a, int t, double4& ts, int& d) {
+    const double2* p = reinterpret_cast<const double2*>(a.tstats + 4 * (size_t)t);
+    const double2 x = p[0], y = p[1];
+    ts = make_double4(x.x, x.y, y.x, y.y);
+    d = a.tdirty[t];
+}
+
+__global__ __launch_bounds__(kCandThreads) void learn_tile_cand_kernel(LearnArgs a, int all) {
+    constexpr int NW = kCandThreads / 64;
+    __shared__ double smn[NW], smx[NW];
+    __shared__ int sfl[NW];
     __shared__ int ncand;
     const int tid = (int)threadIdx.x;
     if (tid == 0) ncand = 0;
     double cmn = __builtin_inf(), cmx = -__builtin_inf();   // over exact (clean) tiles
     if (!all) {
-        for (int t = tid; t < a.NT; t += 1024) {
-            const double* ts = a.tstats + 4 * t;
-            const int d = a.tdirty[t];
-            if (ts[0] == 0.0) continue;
-            if (!(d & 1)) cmx = ts[3] > cmx ? ts[3] : cmx;
-            if (!(d & 2)) cmn = ts[2] < cmn ? ts[2] : cmn;
+        for (int t0 = tid; t0 < a.NT; t0 += kCandUnroll * kCandThreads) {
+            double4 ts[kCandUnroll];
+            int d[kCandUnroll];
+#pragma unroll
+            for (int u = 0; u < kCandUnroll; u++) {     // the loads first
+                const int t = t0 + u * kCandThreads;
+                d[u] = 3;
+                if (t < a.NT) tile_summary(a, t, ts[u], d[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < kCandUnroll; u++) {
+                if (d[u] == 3 || ts[u].x == 0.0) continue;
+                if (!(d[u] & 1)) cmx = ts[u].w > cmx ? ts[u].w : cmx;
+                if (!(d[u] & 2)) cmn = ts[u].z < cmn ? ts[u].z : cmn;
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -1987,19 +2091,43 @@ __global__ __launch_bounds__(1024) void learn_tile_cand_kernel(LearnArgs a, int 
     }
     if ((tid & 63) == 0) { smn[tid >> 6] = cmn; smx[tid >> 6] = cmx; }
     __syncthreads();
-    for (int w = 0; w < 16; w++) {
+    for (int w = 0; w < NW; w++) {
         cmn = smn[w] < cmn ? smn[w] : cmn;
         cmx = smx[w] > cmx ? smx[w] : cmx;
     }
-    for (int t = tid; t < a.NT; t += 1024) {
-        const double* ts = a.tstats + 4 * t;
-        const int d = a.tdirty[t];
-        const bool c = all || (ts[0] != 0.0 && (((d & 1) && ts[3] >= cmx) || ((d & 2) && ts[2] <= cmn) ||
-                                                ((d & 4) && ts[1] != 0.0)));
-        if (c) a.tcand[1 + atomicAdd(&ncand, 1)] = t;
+    int nf = 0;     // non-finite flags of the tiles not rescanned
+    for (int t0 = tid; t0 < a.NT; t0 += kCandUnroll * kCandThreads) {
+        double4 ts[kCandUnroll];
+        int d[kCandUnroll];
+#pragma unroll
+        for (int u = 0; u < kCandUnroll; u++) {
+            const int t = t0 + u * kCandThreads;
+            d[u] = -1;
+            if (t < a.NT) {
+                if (all) d[u] = 0;
+                else tile_summary(a, t, ts[u], d[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCandUnroll; u++) {
+            if (d[u] < 0) continue;
+            const bool c = all || (ts[u].x != 0.0 && (((d[u] & 1) && ts[u].w >= cmx) ||
+                                                       ((d[u] & 2) && ts[u].z <= cmn) ||
+                                                       ((d[u] & 4) && ts[u].y != 0.0)));
+            if (c) a.tcand[1 + atomicAdd(&ncand, 1)] = t0 + u * kCandThreads;
+            else nf |= ts[u].x != 0.0 && ts[u].y != 0.0;
+        }
     }
+    for (int o = 32; o > 0; o >>= 1) nf |= __shfl_xor(nf, o);
+    if ((tid & 63) == 0) sfl[tid >> 6] = nf;
     __syncthreads();
-    if (tid == 0) a.tcand[0] = ncand;
+    if (tid == 0) {
+        for (int w = 0; w < NW; w++) nf |= sfl[w];
+        a.tcand[0] = ncand;
+        a.hpart[0] = cmn;
+        a.hpart[1] = cmx;
+        a.hpart[2] = nf ? 1.0 : 0.0;
+    }
 }
 
 __global__ __launch_bounds__(kTileThreads) void learn_tile_rescan_kernel(LearnArgs a) {
@@ -2009,15 +2137,17 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_rescan_kernel(LearnAr
     for (int c = (int)blockIdx.x; c < n; c += (int)gridDim.x) tile_rescan(a, a.tcand[1 + c], smn, smx, sfl);
 }
 
-// The tiles' summaries -> the statistics the next step's actor reads (hstat).  After
-// learn_tile_rescan_kernel, a stale tile's bound is never the table's extreme.
+// The tiles' summaries -> the statistics the next step's actor reads (hstat): the
+// exact extremes of the tiles learn_tile_cand_kernel kept (hpart) and the rescanned
+// tiles'.  After learn_tile_rescan_kernel a stale tile's bound is never the extreme.
 __global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
     __shared__ double smn[4], smx[4];
     __shared__ int snf[4];
-    double mn = __builtin_inf(), mx = -__builtin_inf();
-    int nf = 0;
-    for (int t = threadIdx.x; t < a.NT; t += 256) {
-        const double* ts = a.tstats + 4 * t;
+    double mn = a.hpart[0], mx = a.hpart[1];
+    int nf = a.hpart[2] != 0.0;
+    const int n = a.tcand[0];
+    for (int c = threadIdx.x; c < n; c += 256) {
+        const double* ts = a.tstats + 4 * (size_t)a.tcand[1 + c];
         if (ts[0] == 0.0) continue;
         nf |= ts[1] != 0.0;
         mn = ts[2] < mn ? ts[2] : mn;
@@ -2479,15 +2609,16 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
     const bool actor = a.mode != kModeCritic;
     const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
     if (init_stats) {
-        learn_tile_cand_kernel<<<dim3(1), dim3(1024), 0, s>>>(a, 1);
+        learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 1);
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
         return hipGetLastError();
     }
-    learn_tile_v_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a);
+    const unsigned tgrid = 8u * (unsigned)((a.NT + 7) / 8);
+    learn_tile_v_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
     if (actor) {
-        learn_tile_h_kernel<<<dim3((unsigned)a.NT), dim3(kTileThreads), 0, s>>>(a);
-        learn_tile_cand_kernel<<<dim3(1), dim3(1024), 0, s>>>(a, 0);
+        learn_tile_h_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+        learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
