@@ -92,7 +92,7 @@ struct ffm_learner {
     bool tstats_valid = false;               // d_tstats summarises the current H
     int NT = 0;
     ffm::TileRec* d_trecs = nullptr;
-    int* d_tstart = nullptr;
+    uint16_t* d_tstart = nullptr;
     double* d_tstats = nullptr;
     int* d_tdirty = nullptr;
     int* d_tcand = nullptr;
@@ -401,7 +401,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (l->tiled_ok) {
         l->NT = (HW + ffm::kTileCells - 1) / ffm::kTileCells;
         if (hipMalloc((void**)&l->d_trecs, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
-            hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 2) != hipSuccess ||
             hipMalloc((void**)&l->d_tstats, (size_t)l->NT * 32) != hipSuccess ||
             hipMalloc((void**)&l->d_tdirty, (size_t)l->NT * 4) != hipSuccess ||
             hipMalloc((void**)&l->d_tcand, (size_t)(l->NT + 1) * 4) != hipSuccess ||
@@ -874,7 +874,7 @@ int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double ep
 }
 
 // ---- tiled step across ranks ---------------------------------------
-int ffm_learner_tiled_buffers(ffm_learner* l, void** d_recs, int64_t* rec_bytes, int32_t** d_tstart,
+int ffm_learner_tiled_buffers(ffm_learner* l, void** d_recs, int64_t* rec_bytes, uint16_t** d_tstart,
                               int64_t* tstart_count) {
     if (!l || !d_recs || !rec_bytes || !d_tstart || !tstart_count) return fail(FFM_E_INVALID, "null argument");
     if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
@@ -902,7 +902,7 @@ int ffm_learner_step_tiled_local(ffm_learner* l, void* stream) {
     return FFM_OK;
 }
 
-int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const int32_t* d_tstart_all,
+int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const uint16_t* d_tstart_all,
                                  int64_t n_envs_all, void* stream) {
     if (!l || !d_recs_all || !d_tstart_all || n_envs_all < 1) return fail(FFM_E_INVALID, "bad argument");
     if ((unsigned long long)n_envs_all * (unsigned long long)l->d.agent_capacity >= (1ull << 32))   // 32-bit record indices
@@ -911,7 +911,7 @@ int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const i
     hipStream_t s = (hipStream_t)stream;
     ffm::LearnArgs a = make_args(l);
     a.trecs = const_cast<ffm::TileRec*>(reinterpret_cast<const ffm::TileRec*>(d_recs_all));
-    a.tstart = const_cast<int*>(d_tstart_all);
+    a.tstart = const_cast<uint16_t*>(d_tstart_all);
     a.E = n_envs_all;
     a.tile_ensure = 1;
     HIP_TRY(ffm::launch_learn_tiles(a, false, s));

@@ -98,7 +98,7 @@ struct LearnArgs {
     double* hpart;              // [2 * kHstatBlocks * 4] partials
     LearnRec* recs;             // [E][A]
     TileRec* trecs;             // [E][A] tiled step: per-agent records in raster order (nullptr: off)
-    int* tstart;                // [E][NT + 1] tiled step: agents of env e in cells < kTileCells * t
+    uint16_t* tstart;           // [E][NT + 1] tiled step: agents of env e in cells < kTileCells * t (A <= 16384)
     double* tstats;             // [NT][4] tiled step: per-tile H summary (present, non-finite, min, max)
     int* tdirty;                // [NT] tiled step: bit 0 max, 1 min, 2 non-finite flag only a bound (stale)
     int* tcand;                 // [NT + 1] tiled step: tiles to rescan ([0] = count, then the tiles)

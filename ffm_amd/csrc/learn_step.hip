@@ -1265,11 +1265,12 @@ void learn_batch_kernel(LearnArgs a) {
                 // tiled step: the raster rank of the first agent of each tile of this 64-cell chunk
                 const int tc = c - lane + kTileCells * lane;
                 if (tc < c1)
-                    a.tstart[e * (a.NT + 1) + tc / kTileCells] = base + __popcll(m & ((1ull << (kTileCells * lane)) - 1ull));
+                    a.tstart[e * (a.NT + 1) + tc / kTileCells] =
+                        (uint16_t)(base + __popcll(m & ((1ull << (kTileCells * lane)) - 1ull)));
             }
             base += __popcll(m);
         }
-        if (a.trecs && tid == 0) a.tstart[e * (a.NT + 1) + a.NT] = n;
+        if (a.trecs && tid == 0) a.tstart[e * (a.NT + 1) + a.NT] = (uint16_t)n;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < APT; j++) {
@@ -1786,57 +1787,96 @@ __device__ __forceinline__ int tile_of_block(int NT) {
 constexpr int kTileEnvChunk = 2 * kTileThreads;   // envs whose ranges one pass gathers
 constexpr int kTileList = 4 * kTileThreads;       // record indices per window
 
-// Calls f(g) for every record g (an index into trecs) of tile t's cells.  The record
-// ranges of 512 envs at a time (tstart) are loaded together, a block scan places them in
-// one flat list, and the records are dealt evenly over the threads: one dependent chain
-// (range, record, table reads) per record instead of one per env in turn.  A cell holds
-// at most one agent, so a pass holds <= 4 * 512 records: two windows at most.
+// Tile t's record ranges of envs [e0, e0 + 512): loaded together (two envs per thread),
+// and a block scan gives each thread the offset of its records in one flat list and the
+// block the total.  Ends with a barrier (wsum read); the caller syncs before reusing wsum.
+struct TileRanges {
+    int lo[2], n[2], off, total;
+};
+
+__device__ __forceinline__ TileRanges tile_ranges(const LearnArgs& a, int t, long long e0, int* wsum) {
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    TileRanges r;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const long long e = e0 + tid + j * kTileThreads;
+        r.lo[j] = 0;
+        r.n[j] = 0;
+        if (e < a.E) {
+            const uint16_t* ts = a.tstart + e * (a.NT + 1) + t;
+            r.lo[j] = ts[0];
+            r.n[j] = ts[1] - r.lo[j];
+        }
+    }
+    const int c = r.n[0] + r.n[1];
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    r.off = incl - c;
+    r.total = 0;
+#pragma unroll
+    for (int w = 0; w < kTileWaves; w++) {
+        r.off += w < wv ? wsum[w] : 0;
+        r.total += wsum[w];
+    }
+    return r;
+}
+
+// Window [b, b + kTileList) of the flat list: the record indices (into trecs).
+__device__ __forceinline__ void tile_fill(const LearnArgs& a, long long e0, const TileRanges& r, int b,
+                                          uint32_t* list) {
+    const int tid = (int)threadIdx.x;
+    int o = r.off - b;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint32_t g0 = (uint32_t)((e0 + tid + j * kTileThreads) * a.A + r.lo[j]);
+        for (int i = 0; i < r.n[j]; i++, o++)
+            if (o >= 0 && o < kTileList) list[o] = g0 + (uint32_t)i;
+    }
+}
+
+// Calls f(g) for every record g of tile t's cells, dealt evenly over the threads: one
+// dependent chain (range, record, table reads) per record instead of one per env in turn.
 template <typename F>
 __device__ __forceinline__ void tile_records(const LearnArgs& a, int t, uint32_t* list, int* wsum, F f) {
-    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = (int)threadIdx.x;
     for (long long e0 = 0; e0 < a.E; e0 += kTileEnvChunk) {
-        int lo[2], n[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const long long e = e0 + tid + j * kTileThreads;
-            lo[j] = 0;
-            n[j] = 0;
-            if (e < a.E) {
-                const int* ts = a.tstart + e * (a.NT + 1) + t;
-                lo[j] = ts[0];
-                n[j] = ts[1] - lo[j];
-            }
-        }
-        const int c = n[0] + n[1];
-        int incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        int off = incl - c, total = 0;
-#pragma unroll
-        for (int w = 0; w < kTileWaves; w++) {
-            off += w < wv ? wsum[w] : 0;
-            total += wsum[w];
-        }
-        for (int b = 0; b < total; b += kTileList) {
-            int o = off - b;
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                const uint32_t g0 = (uint32_t)((e0 + tid + j * kTileThreads) * a.A + lo[j]);
-                for (int i = 0; i < n[j]; i++, o++)
-                    if (o >= 0 && o < kTileList) list[o] = g0 + (uint32_t)i;
-            }
+        const TileRanges r = tile_ranges(a, t, e0, wsum);
+        for (int b = 0; b < r.total; b += kTileList) {
+            tile_fill(a, e0, r, b, list);
             __syncthreads();
-            const int m = total - b < kTileList ? total - b : kTileList;
+            const int m = r.total - b < kTileList ? r.total - b : kTileList;
             for (int i = tid; i < m; i += kTileThreads) f(list[i]);
             __syncthreads();
         }
         __syncthreads();    // wsum is rewritten by the next pass
     }
+}
+
+// The fast form of a tile pass: every record of the tile in one window (at most 512 envs,
+// at most kTileList records, the common case).  Each thread then holds up to J records
+// at once; the first record of a slot (its "owner", elected by an LDS atomic) loads the
+// slot's table row together with the others' table reads, and applies it after the
+// barrier from registers: range, record, (table reads), apply -- three dependent steps.
+// Returns the window's record count, or -1 (the caller takes tile_records; no barrier
+// owed).
+constexpr int kTileJ = kTileList / kTileThreads;
+
+__device__ __forceinline__ int tile_window(const LearnArgs& a, int t, uint32_t* list, int* wsum) {
+    if (a.E > kTileEnvChunk) return -1;
+    const TileRanges r = tile_ranges(a, t, 0, wsum);
+    if (r.total > kTileList) {
+        __syncthreads();
+        return -1;
+    }
+    tile_fill(a, 0, r, 0, list);
+    __syncthreads();
+    return r.total;
 }
 
 // The rank key of a dense slot (inverse of dense_slot): ranks in bits 0-7, bx, by.
@@ -1859,17 +1899,48 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     __syncthreads();
     const uint32_t Q = (a.V.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
-    tile_records(a, t, list, wsum, [&](uint32_t g) {
-        const TileRec rc = a.trecs[g];
-        const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-        const int idx = tile_idx(sv, qsh, Q, c0);
+    auto add = [&](const TileRec& rc, uint32_t sv, int idx) {
         atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(rc.td));
-        atomicAdd(&ks[idx], 1u);
         if (a.tile_ensure) {     // another rank's agent: its s and s' join this rank's V
             dense_ensure(a.V, sv, dense_key(sv, qsh, Q, a.V.dense_by));
             const uint32_t sn = rc.snf & 0x0FFFFFFFu;
             if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
         }
+    };
+    const int m = tile_window(a, t, list, wsum);
+    if (m >= 0) {
+        TileRec rc[kTileJ];
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++)
+            if (tid + j * kTileThreads < m) rc[j] = a.trecs[list[tid + j * kTileThreads]];
+        bool own[kTileJ];
+        double vv[kTileJ];
+        int ix[kTileJ];
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++) {
+            own[j] = false;
+            if (tid + j * kTileThreads >= m) continue;
+            const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+            ix[j] = tile_idx(sv, qsh, Q, c0);
+            own[j] = atomicAdd(&ks[ix[j]], 1u) == 0u;
+            if (own[j]) vv[j] = tval(a.V, sv)[0];
+            add(rc[j], sv, ix[j]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++) {
+            if (!own[j]) continue;
+            double* vp = tval(a.V, rc[j].svk & 0x0FFFFFFFu);
+            vp[0] = v_visits(vv[j], qs[ix[j]], (long long)ks[ix[j]], a.V.alpha);
+        }
+        return;
+    }
+    tile_records(a, t, list, wsum, [&](uint32_t g) {
+        const TileRec rc = a.trecs[g];
+        const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+        const int idx = tile_idx(sv, qsh, Q, c0);
+        atomicAdd(&ks[idx], 1u);
+        add(rc, sv, idx);
     });
     constexpr int kPer = NS / kTileThreads;
     double vv[kPer];
@@ -1963,11 +2034,8 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
     for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
     __syncthreads();
-    tile_records(a, t, list, wsum, [&](uint32_t g) {
-        const TileRec rc = a.trecs[g];
-        const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-        const int idx = tile_idx(sv, qsh, Q, c0);
-        atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+    // the increment of one record (the row's ensure included)
+    auto add = [&](const TileRec& rc, uint32_t sv, int idx, double vn, double vs) {
         if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
         const int k = (int)(rc.svk >> 28);
         if (k == (int)kTileNoAct) return;
@@ -1977,36 +2045,26 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
             if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
             const int coll = (int)(rc.snf >> 29) - 1;
             if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
-            const uint32_t sn = rc.snf & 0x0FFFFFFFu;
-            const double vn = sn != kTileTerminal ? tval(a.V, sn)[0] : 0.0;
-            td = (r0 + a.gamma * vn) - tval(a.V, sv)[0];
+            td = (r0 + a.gamma * vn) - vs;
         }
         atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]), (unsigned long long)fx(a.alpha_h * td));
-    });
-    // every touched row's loads are issued before the first is used (one latency, not four)
-    constexpr int kPer = NS / kTileThreads;
-    double hv[kPer][5];
-    bool tch[kPer];
-#pragma unroll
-    for (int j = 0; j < kPer; j++) {
-        const int i = tid + j * kTileThreads;
-        tch[j] = (touched[i >> 5] >> (i & 31)) & 1u;
-        if (tch[j]) {
-            const double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
-#pragma unroll
-            for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < kPer; j++) {
-        if (!tch[j]) continue;
-        const int i = tid + j * kTileThreads;
-        double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+    };
+    // the V values the actor's td reads (actor_only: updated by learn_tile_v_kernel)
+    auto vpair = [&](const TileRec& rc, uint32_t sv, double& vn, double& vs) {
+        vn = 0.0;
+        vs = 0.0;
+        if (!post_update || (rc.svk >> 28) == kTileNoAct) return;
+        const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+        if (sn != kTileTerminal) vn = tval(a.V, sn)[0];
+        vs = tval(a.V, sv)[0];
+    };
+    // a touched row: new values, the summary's bounds and staleness
+    auto apply = [&](double* vp, int idx, const double* old5) {
         flags |= 4;
 #pragma unroll
         for (int k = 0; k < 5; k++) {
-            const long long q = hq[i * 5 + k];
-            const double old = hv[j][k];
+            const long long q = hq[idx * 5 + k];
+            const double old = old5[k];
             double v = old;
             if (q != 0) {
                 v = v + (double)q * (1.0 / kFxOne);
@@ -2018,6 +2076,67 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
             flags |= __builtin_isfinite(v) ? 0 : 1;
             mn = v < mn ? v : mn;
             mx = v > mx ? v : mx;
+        }
+    };
+    const int m = tile_window(a, t, list, wsum);
+    if (m >= 0) {
+        TileRec rc[kTileJ];
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++)
+            if (tid + j * kTileThreads < m) rc[j] = a.trecs[list[tid + j * kTileThreads]];
+        bool own[kTileJ];
+        int ix[kTileJ];
+        double hv[kTileJ][5], vn[kTileJ], vs[kTileJ];
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++) {     // owners' rows and the V reads, all in flight
+            own[j] = false;
+            if (tid + j * kTileThreads >= m) continue;
+            const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+            ix[j] = tile_idx(sv, qsh, Q, c0);
+            const uint32_t bit = 1u << (ix[j] & 31);
+            own[j] = !(atomicOr(&touched[ix[j] >> 5], bit) & bit);
+            if (own[j]) {
+                const double* vp = tval(a.Ht, sv);
+#pragma unroll
+                for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
+            }
+            vpair(rc[j], sv, vn[j], vs[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++)
+            if (tid + j * kTileThreads < m) add(rc[j], rc[j].svk & 0x0FFFFFFFu, ix[j], vn[j], vs[j]);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kTileJ; j++)
+            if (own[j]) apply(tval(a.Ht, rc[j].svk & 0x0FFFFFFFu), ix[j], hv[j]);
+    } else {
+        tile_records(a, t, list, wsum, [&](uint32_t g) {
+            const TileRec rc = a.trecs[g];
+            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+            const int idx = tile_idx(sv, qsh, Q, c0);
+            atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+            double vn, vs;
+            vpair(rc, sv, vn, vs);
+            add(rc, sv, idx, vn, vs);
+        });
+        // every touched row's loads are issued before the first is used (one latency, not four)
+        constexpr int kPer = NS / kTileThreads;
+        double hv[kPer][5];
+        bool tch[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const int i = tid + j * kTileThreads;
+            tch[j] = (touched[i >> 5] >> (i & 31)) & 1u;
+            if (tch[j]) {
+                const double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+#pragma unroll
+                for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const int i = tid + j * kTileThreads;
+            if (tch[j]) apply(tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells)), i, hv[j]);
         }
     }
     for (int o = 32; o > 0; o >>= 1) {

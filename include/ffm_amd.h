@@ -285,15 +285,16 @@ int ffm_learner_delta_merge_async(ffm_learner* l, int32_t which, const uint64_t*
 /* The tiled step across ranks (ffm_unified, dense tables at block size 1 on large maps,
  * sync period 1): step_tiled_local runs the step and leaves one 16-B record
  * per agent (raster order) and per-env tile offsets in this learner's DEVICE buffers
- * (tiled_buffers: rec_bytes bytes of records, tstart_count int32 offsets); the ranks
+ * (tiled_buffers: rec_bytes bytes of records, tstart_count uint16 offsets: agent ranks
+ * below agent_capacity <= 16384); the ranks
  * all-gather both, rank-major; step_tiled_apply sums every rank's records per tile of
  * cells into the replicated tables (inserting the slots other ranks created) and ends the
  * step.  Every rank holds, bit for bit, the tables one device stepping all envs would hold.
  * Learners of other kinds return FFM_E_UNSUPPORTED. */
-int ffm_learner_tiled_buffers(ffm_learner* l, void** d_recs, int64_t* rec_bytes, int32_t** d_tstart,
+int ffm_learner_tiled_buffers(ffm_learner* l, void** d_recs, int64_t* rec_bytes, uint16_t** d_tstart,
                               int64_t* tstart_count);
 int ffm_learner_step_tiled_local(ffm_learner* l, void* stream);
-int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const int32_t* d_tstart_all,
+int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const uint16_t* d_tstart_all,
                                  int64_t n_envs_all, void* stream);
 /* Table sync period K >= 1 (default 1 = the reference's per-step updates): the fixed-point
  * increments of K steps accumulate and V / H (and the actor's H statistics) are applied
