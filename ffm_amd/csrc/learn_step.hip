@@ -1894,6 +1894,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     __shared__ uint32_t list[kTileList];
     __shared__ int wsum[kTileWaves];
     const int t = tile_of_block(a.NT), tid = (int)threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0) a.tcand[0] = 0;    // the H pass's queue of wide tiles
     if (t >= a.NT) return;
     for (int i = tid; i < NS; i += kTileThreads) { qs[i] = 0; ks[i] = 0u; }
     __syncthreads();
@@ -2013,7 +2014,205 @@ __device__ void tile_rescan(const LearnArgs& a, int t, double* smn, double* smx,
 // max and moved inward, the old extreme stays as a bound and the tile is marked stale
 // (tdirty): learn_tile_cand_kernel rescans only the stale tiles whose bound could
 // decide the table's min or max.
+//
+// Pieces shared by the two forms of the H pass:
+struct TileHCtx {
+    double omn, omx;                    // the tile's summary at step start
+    bool onf;
+    int flags;                          // 1 non-finite, 2 max stale, 4 any row, 8 min stale, 16 nf stale
+    double mn, mx;                      // over the touched rows' new values
+};
+
+// The V values the actor's td reads (actor_only: updated by learn_tile_v_kernel).
+__device__ __forceinline__ void tile_h_vpair(const LearnArgs& a, const TileRec& rc, uint32_t sv, double& vn,
+                                             double& vs) {
+    vn = 0.0;
+    vs = 0.0;
+    if (a.mode != kModeActor || (rc.svk >> 28) == kTileNoAct) return;
+    const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+    if (sn != kTileTerminal) vn = tval(a.V, sn)[0];
+    vs = tval(a.V, sv)[0];
+}
+
+// The fixed-point increment alpha_h * td of one record (an action taken).
+__device__ __forceinline__ long long tile_h_q(const LearnArgs& a, const TileRec& rc, double vn, double vs) {
+    double td = rc.td;
+    if (a.mode == kModeActor) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
+        double r0 = a.step_penalty;
+        if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
+        const int coll = (int)(rc.snf >> 29) - 1;
+        if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
+        td = (r0 + a.gamma * vn) - vs;
+    }
+    return fx(a.alpha_h * td);
+}
+
+// A touched row: new values, the summary's bounds and staleness.
+__device__ __forceinline__ void tile_h_apply(double* vp, const long long (&q)[5], const double* old5, TileHCtx& c) {
+    c.flags |= 4;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const double old = old5[k];
+        double v = old;
+        if (q[k] != 0) {
+            v = v + (double)q[k] * (1.0 / kFxOne);
+            vp[k] = v;
+            if (old == c.omx && !(v >= old)) c.flags |= 2;    // the max moved inward (or to NaN)
+            if (old == c.omn && !(v <= old)) c.flags |= 8;
+            if (!__builtin_isfinite(old)) c.flags |= 16;
+        }
+        c.flags |= __builtin_isfinite(v) ? 0 : 1;
+        c.mn = v < c.mn ? v : c.mn;
+        c.mx = v > c.mx ? v : c.mx;
+    }
+}
+
+__device__ __forceinline__ TileHCtx tile_h_begin(const LearnArgs& a, int t) {
+    const double* ts = a.tstats + 4 * t;
+    TileHCtx c;
+    c.omn = ts[2];
+    c.omx = ts[3];
+    c.onf = ts[1] != 0.0;
+    c.flags = 0;
+    c.mn = __builtin_inf();
+    c.mx = -__builtin_inf();
+    return c;
+}
+
+// The block's summary of tile t (ends with a barrier: smn / smx / sfl are free again).
+__device__ __forceinline__ void tile_h_end(const LearnArgs& a, int t, TileHCtx& c, double* smn, double* smx,
+                                           int* sfl) {
+    const int tid = (int)threadIdx.x;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(c.mn, o), b2 = __shfl_xor(c.mx, o);
+        c.mn = a2 < c.mn ? a2 : c.mn;
+        c.mx = b2 > c.mx ? b2 : c.mx;
+        c.flags |= __shfl_xor(c.flags, o);
+    }
+    const int wv = tid >> 6;
+    if ((tid & 63) == 0) { smn[wv] = c.mn; smx[wv] = c.mx; sfl[wv] = c.flags; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kTileWaves; w++) {
+            c.mn = smn[w] < c.mn ? smn[w] : c.mn;
+            c.mx = smx[w] > c.mx ? smx[w] : c.mx;
+            c.flags |= sfl[w];
+        }
+        // the old extremes stay as bounds (a value that left them is only inward)
+        double* ts = a.tstats + 4 * t;
+        ts[0] = (ts[0] != 0.0 || (c.flags & 4)) ? 1.0 : 0.0;
+        ts[1] = (c.onf || (c.flags & 1)) ? 1.0 : 0.0;
+        ts[2] = c.omn < c.mn ? c.omn : c.mn;
+        ts[3] = c.omx > c.mx ? c.omx : c.mx;
+        a.tdirty[t] |= ((c.flags & 2) ? 1 : 0) | ((c.flags & 8) ? 2 : 0) | ((c.flags & 16) ? 4 : 0);
+    }
+    __syncthreads();
+}
+
+// The fast form: every record of the tile in one window (tile_window), at most
+// kTileList records, so at most kTileList (slot, action) pairs are touched.  The sums
+// live in one fixed-point word per touched pair, found through a pair -> index map:
+// 22 KB of LDS instead of 40 KB for every pair of the tile, so five workgroups share a
+// CU (the register limit) instead of three, and their dependent loads overlap.
+//   1. per record: the slot's first record (its owner, an LDS bit) loads the H row, the
+//      pair's first record takes an index (wave-aggregated counter), V reads in flight;
+//   2. (barrier) every record adds its increment into its pair's word;
+//   3. (barrier) owners apply their rows from registers.
+// A tile whose records need more than one window is queued (tcand, count reset by
+// learn_tile_v_kernel) for learn_tile_h_wide_kernel.
+constexpr int kTilePairs = 256 * kTileCells * 5;
+
 __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a) {
+    constexpr int NS = 256 * kTileCells;
+    __shared__ long long hq[kTileList];             // per touched (slot, action) pair
+    __shared__ uint16_t pid[kTilePairs];            // pair -> index into hq (valid where pbit is set)
+    __shared__ uint32_t pbit[kTilePairs / 32];
+    __shared__ uint32_t touched[NS / 32];
+    __shared__ double smn[kTileWaves], smx[kTileWaves];
+    __shared__ int sfl[kTileWaves];
+    __shared__ uint32_t list[kTileList];
+    __shared__ int wsum[kTileWaves];
+    __shared__ int npair;
+    const int t = tile_of_block(a.NT), tid = (int)threadIdx.x, lane = tid & 63;
+    if (t >= a.NT) return;
+    const uint32_t Q = (a.Ht.mask + 1u) >> 8;
+    const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
+    for (int i = tid; i < kTileList; i += kTileThreads) hq[i] = 0;
+    for (int i = tid; i < kTilePairs / 32; i += kTileThreads) pbit[i] = 0u;
+    if (tid < NS / 32) touched[tid] = 0u;
+    if (tid == 0) npair = 0;
+    // (tile_window's barriers order these stores before any use)
+    const int m = tile_window(a, t, list, wsum);
+    if (m < 0) {
+        if (tid == 0) a.tcand[1 + atomicAdd(&a.tcand[0], 1)] = t;
+        return;
+    }
+    TileHCtx c = tile_h_begin(a, t);
+    TileRec rc[kTileJ];
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++)
+        if (tid + j * kTileThreads < m) rc[j] = a.trecs[list[tid + j * kTileThreads]];
+    bool own[kTileJ], pown[kTileJ];
+    int ix[kTileJ], pr[kTileJ];
+    double hv[kTileJ][5], vn[kTileJ], vs[kTileJ];
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++) {     // owners' rows and the V reads, all in flight
+        own[j] = false;
+        pown[j] = false;
+        pr[j] = -1;
+        if (tid + j * kTileThreads >= m) continue;
+        const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+        ix[j] = tile_idx(sv, qsh, Q, c0);
+        const uint32_t bit = 1u << (ix[j] & 31);
+        own[j] = !(atomicOr(&touched[ix[j] >> 5], bit) & bit);
+        if (own[j]) {
+            const double* vp = tval(a.Ht, sv);
+#pragma unroll
+            for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
+        }
+        tile_h_vpair(a, rc[j], sv, vn[j], vs[j]);
+        if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
+        const int k = (int)(rc[j].svk >> 28);
+        if (k != (int)kTileNoAct) {
+            pr[j] = ix[j] * 5 + k;
+            const uint32_t pb = 1u << (pr[j] & 31);
+            pown[j] = !(atomicOr(&pbit[pr[j] >> 5], pb) & pb);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++) {     // pair owners take consecutive indices, one atomic per wave
+        const unsigned long long bm = __ballot(pown[j]);
+        if (!bm) continue;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&npair, __popcll(bm));
+        base = __shfl(base, 0);
+        if (pown[j]) pid[pr[j]] = (uint16_t)(base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++)
+        if (pr[j] >= 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&hq[pid[pr[j]]]),
+                      (unsigned long long)tile_h_q(a, rc[j], vn[j], vs[j]));
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++) {
+        if (!own[j]) continue;
+        long long q[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int p = ix[j] * 5 + k;
+            q[k] = ((pbit[p >> 5] >> (p & 31)) & 1u) ? hq[pid[p]] : 0;
+        }
+        tile_h_apply(tval(a.Ht, rc[j].svk & 0x0FFFFFFFu), q, hv[j], c);
+    }
+    tile_h_end(a, t, c, smn, smx, sfl);
+}
+
+// The general form, for the tiles the fast form queued (more than one window of
+// records: a crowded tile, or more than 512 envs): every (slot, action) pair of the
+// tile has its word (40 KB), records stream through windows, then the touched rows.
+__global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
     __shared__ long long hq[NS * 5];
     __shared__ uint32_t touched[NS / 32];
@@ -2021,103 +2220,28 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     __shared__ int sfl[kTileWaves];
     __shared__ uint32_t list[kTileList];
     __shared__ int wsum[kTileWaves];
-    const int t = tile_of_block(a.NT), tid = (int)threadIdx.x;
-    if (t >= a.NT) return;
-    const bool post_update = a.mode == kModeActor;
+    const int tid = (int)threadIdx.x;
     const uint32_t Q = (a.Ht.mask + 1u) >> 8;
-    const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
-    double* ts = a.tstats + 4 * t;
-    const double omn = ts[2], omx = ts[3];
-    const bool onf = ts[1] != 0.0;
-    int flags = 0;                      // 1 non-finite, 2 max stale, 4 any row, 8 min stale, 16 nf stale
-    double mn = __builtin_inf(), mx = -__builtin_inf();
-    for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
-    for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
-    __syncthreads();
-    // the increment of one record (the row's ensure included)
-    auto add = [&](const TileRec& rc, uint32_t sv, int idx, double vn, double vs) {
-        if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
-        const int k = (int)(rc.svk >> 28);
-        if (k == (int)kTileNoAct) return;
-        double td = rc.td;
-        if (post_update) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
-            double r0 = a.step_penalty;
-            if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
-            const int coll = (int)(rc.snf >> 29) - 1;
-            if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
-            td = (r0 + a.gamma * vn) - vs;
-        }
-        atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]), (unsigned long long)fx(a.alpha_h * td));
-    };
-    // the V values the actor's td reads (actor_only: updated by learn_tile_v_kernel)
-    auto vpair = [&](const TileRec& rc, uint32_t sv, double& vn, double& vs) {
-        vn = 0.0;
-        vs = 0.0;
-        if (!post_update || (rc.svk >> 28) == kTileNoAct) return;
-        const uint32_t sn = rc.snf & 0x0FFFFFFFu;
-        if (sn != kTileTerminal) vn = tval(a.V, sn)[0];
-        vs = tval(a.V, sv)[0];
-    };
-    // a touched row: new values, the summary's bounds and staleness
-    auto apply = [&](double* vp, int idx, const double* old5) {
-        flags |= 4;
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const long long q = hq[idx * 5 + k];
-            const double old = old5[k];
-            double v = old;
-            if (q != 0) {
-                v = v + (double)q * (1.0 / kFxOne);
-                vp[k] = v;
-                if (old == omx && !(v >= old)) flags |= 2;    // the max moved inward (or to NaN)
-                if (old == omn && !(v <= old)) flags |= 8;
-                if (!__builtin_isfinite(old)) flags |= 16;
-            }
-            flags |= __builtin_isfinite(v) ? 0 : 1;
-            mn = v < mn ? v : mn;
-            mx = v > mx ? v : mx;
-        }
-    };
-    const int m = tile_window(a, t, list, wsum);
-    if (m >= 0) {
-        TileRec rc[kTileJ];
-#pragma unroll
-        for (int j = 0; j < kTileJ; j++)
-            if (tid + j * kTileThreads < m) rc[j] = a.trecs[list[tid + j * kTileThreads]];
-        bool own[kTileJ];
-        int ix[kTileJ];
-        double hv[kTileJ][5], vn[kTileJ], vs[kTileJ];
-#pragma unroll
-        for (int j = 0; j < kTileJ; j++) {     // owners' rows and the V reads, all in flight
-            own[j] = false;
-            if (tid + j * kTileThreads >= m) continue;
-            const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
-            ix[j] = tile_idx(sv, qsh, Q, c0);
-            const uint32_t bit = 1u << (ix[j] & 31);
-            own[j] = !(atomicOr(&touched[ix[j] >> 5], bit) & bit);
-            if (own[j]) {
-                const double* vp = tval(a.Ht, sv);
-#pragma unroll
-                for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
-            }
-            vpair(rc[j], sv, vn[j], vs[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < kTileJ; j++)
-            if (tid + j * kTileThreads < m) add(rc[j], rc[j].svk & 0x0FFFFFFFu, ix[j], vn[j], vs[j]);
+    const int qsh = __builtin_ctz(Q);
+    const int n = a.tcand[0];
+    for (int ci = (int)blockIdx.x; ci < n; ci += (int)gridDim.x) {
+        const int t = a.tcand[1 + ci], c0 = t * kTileCells;
+        for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
+        for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
         __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kTileJ; j++)
-            if (own[j]) apply(tval(a.Ht, rc[j].svk & 0x0FFFFFFFu), ix[j], hv[j]);
-    } else {
+        TileHCtx c = tile_h_begin(a, t);
         tile_records(a, t, list, wsum, [&](uint32_t g) {
             const TileRec rc = a.trecs[g];
             const uint32_t sv = rc.svk & 0x0FFFFFFFu;
             const int idx = tile_idx(sv, qsh, Q, c0);
             atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+            if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
+            const int k = (int)(rc.svk >> 28);
+            if (k == (int)kTileNoAct) return;
             double vn, vs;
-            vpair(rc, sv, vn, vs);
-            add(rc, sv, idx, vn, vs);
+            tile_h_vpair(a, rc, sv, vn, vs);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]),
+                      (unsigned long long)tile_h_q(a, rc, vn, vs));
         });
         // every touched row's loads are issued before the first is used (one latency, not four)
         constexpr int kPer = NS / kTileThreads;
@@ -2136,32 +2260,16 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const int i = tid + j * kTileThreads;
-            if (tch[j]) apply(tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells)), i, hv[j]);
+            if (!tch[j]) continue;
+            long long q[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) q[k] = hq[i * 5 + k];
+            tile_h_apply(tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells)), q, hv[j], c);
         }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        const double a2 = __shfl_xor(mn, o), b2 = __shfl_xor(mx, o);
-        mn = a2 < mn ? a2 : mn;
-        mx = b2 > mx ? b2 : mx;
-        flags |= __shfl_xor(flags, o);
-    }
-    const int wv = tid >> 6;
-    if ((tid & 63) == 0) { smn[wv] = mn; smx[wv] = mx; sfl[wv] = flags; }
-    __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < kTileWaves; w++) {
-            mn = smn[w] < mn ? smn[w] : mn;
-            mx = smx[w] > mx ? smx[w] : mx;
-            flags |= sfl[w];
-        }
-        // the old extremes stay as bounds (a value that left them is only inward)
-        ts[0] = (ts[0] != 0.0 || (flags & 4)) ? 1.0 : 0.0;
-        ts[1] = (onf || (flags & 1)) ? 1.0 : 0.0;
-        ts[2] = omn < mn ? omn : mn;
-        ts[3] = omx > mx ? omx : mx;
-        a.tdirty[t] |= ((flags & 2) ? 1 : 0) | ((flags & 8) ? 2 : 0) | ((flags & 16) ? 4 : 0);
+        tile_h_end(a, t, c, smn, smx, sfl);
     }
 }
+
 
 // The tiles to rescan: a stale tile matters only if its bound could be the table's
 // extreme -- its max bound above every exact tile max (or its min bound below every
@@ -2611,6 +2719,72 @@ __global__ __launch_bounds__(256) void learn_stencil4_kernel(LearnArgs a, int ti
     *reinterpret_cast<float4*>(a.dff_out + e * (long long)a.HW + c) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// The same stencil for rows of whole waves (W % 256 == 0; C5's 256x256): a wave owns a
+// 256-cell row segment over kColRows consecutive rows, four cells per lane, and keeps the
+// quads of the rows above, at and below in registers, so each row is loaded once per
+// strip (plus one halo row above and below) instead of three times; the left and right
+// neighbours come from the adjacent lanes (a scalar load only at a segment's inner
+// edges).  A workgroup's four waves take consecutive strips.  Per cell the identical
+// operation sequence (U, D, L, R).
+constexpr int kColRows = 8;
+
+__global__ __launch_bounds__(256) void learn_stencil_col_kernel(LearnArgs a, int strips, int segs) {
+    const unsigned B = gridDim.x, b = blockIdx.x;
+    const unsigned lt = (B & 7u) ? b : (b & 7u) * (B >> 3) + (b >> 3);
+    const int per_env = strips * segs;
+    const long long e = lt / (unsigned)per_env;
+    const int r = (int)(lt - (unsigned)e * (unsigned)per_env);
+    const int sg = r % segs, st = r / segs;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const int H = a.H, W = a.W;
+    const int x0 = (st * 4 + wv) * kColRows;
+    if (x0 >= H) return;
+    const int y = sg * 256 + 4 * lane;
+    const float* dff = a.dff_in + e * (long long)a.HW;
+    float* out = a.dff_out + e * (long long)a.HW;
+    const float c0 = a.c0, c1 = a.c1;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 q[kColRows + 2];                 // rows x0 - 1 .. x0 + kColRows
+#pragma unroll
+    for (int i = 0; i < kColRows + 2; i++) {
+        const int x = x0 - 1 + i;
+        q[i] = (x >= 0 && x < H) ? *reinterpret_cast<const float4*>(dff + (long long)x * W + y) : z4;
+    }
+    const bool eL = lane == 0 && y > 0, eR = lane == 63 && y + 4 < W;    // segment edges inside the row
+    float le[kColRows], re[kColRows];
+#pragma unroll
+    for (int i = 0; i < kColRows; i++) {
+        const int x = x0 + i;
+        le[i] = (eL && x < H) ? dff[(long long)x * W + y - 1] : 0.f;
+        re[i] = (eR && x < H) ? dff[(long long)x * W + y + 4] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < kColRows; i++) {
+        const int x = x0 + i;
+        if (x >= H) break;
+        const float4 m = q[i + 1], u = q[i], d = q[i + 2];
+        float l = __shfl_up(m.w, 1), rr = __shfl_down(m.x, 1);
+        l = lane == 0 ? le[i] : l;
+        rr = lane == 63 ? re[i] : rr;
+        const float mv[4] = {m.x, m.y, m.z, m.w}, uv[4] = {u.x, u.y, u.z, u.w}, dv[4] = {d.x, d.y, d.z, d.w};
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float acc = c0 * mv[k];
+            const float nb[4] = {uv[k], dv[k], k > 0 ? mv[k - 1] : l, k < 3 ? mv[k + 1] : rr};
+            const bool in[4] = {x > 0, x < H - 1, k > 0 || y > 0, k < 3 || y + 4 < W};
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {             // U, D, L, R as kNBx / kNBy
+                const float v = in[qq] ? c0 * nb[qq] : 0.0f;
+                const float t = c1 * v;
+                acc = acc + t;
+            }
+            o[k] = acc < 1e-4f ? 0.0f : acc;
+        }
+        *reinterpret_cast<float4*>(out + (long long)x * W + y) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 constexpr int kSepStencilHW = 16384;
 
 template <int BS, int EPB, int APT, int D, bool DL>
@@ -2629,7 +2803,10 @@ hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     learn_batch_kernel<BS, EPB, APT, D, DL><<<dim3(blocks), dim3(BS), smem, s>>>(a);
     if (a.sep_stencil) {
         const int tiles = (a.HW + 255) / 256;
-        if (a.W % 4 == 0) {
+        if (a.W % 256 == 0 && !(FFM_LABLATE & 16)) {
+            const int segs = a.W / 256, strips = (a.H + 4 * kColRows - 1) / (4 * kColRows);
+            learn_stencil_col_kernel<<<dim3((unsigned)(strips * segs * a.E)), dim3(256), 0, s>>>(a, strips, segs);
+        } else if (a.W % 4 == 0) {
             const int tiles4 = (a.HW / 4 + 255) / 256;
             learn_stencil4_kernel<<<dim3((unsigned)(tiles4 * a.E)), dim3(256), 0, s>>>(a, tiles4);
         } else {
@@ -2737,6 +2914,7 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
     learn_tile_v_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
     if (actor) {
         learn_tile_h_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+        learn_tile_h_wide_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);

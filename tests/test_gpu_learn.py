@@ -235,6 +235,15 @@ def test_learner_philox_tiled_step_matches_cpu(mode):
                     max_steps=25, seed=6, env_base=77)
 
 
+@pytest.mark.parametrize("H,W", [(70, 256), (40, 512)])
+def test_learner_philox_column_stencil_shapes(H, W):
+    """The separate DFF stencil in row-segment strips (learn_stencil_col_kernel, W % 256 ==
+    0): a last strip of 6 rows (70 = 2 x 32 + 6) and two 256-cell segments per row (the
+    neighbours across a segment edge); the DFF equals the CPU restatement bit for bit."""
+    p = {"epsilon": 0.1, "block_size": 1}
+    _philox_compare("unified", "actor_only", p, H, W, 300, 6, 20, max_steps=15, seed=5)
+
+
 @pytest.mark.parametrize("n,N,T", [(520, 600, 8), (300, 3000, 6)])
 def test_learner_tiled_general_tile_pass_equals_accumulators(monkeypatch, n, N, T):
     """The tile passes' general form (records beyond one window: more than 512 envs, or a
