@@ -273,9 +273,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
                                        "'neumann'");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
-    // batched: LDS grid codes and placement sorts hold <= 16384 agents; the exact (MT) step
+    // batched: LDS grid codes hold 14-bit agent indices (<= 16383 agents); the exact (MT) step
     // keeps int scratch and u16 cells, so the drop-in classes can hold every free cell
-    if (d.agent_capacity < 1 || d.agent_capacity > (d.rng_mode == FFM_RNG_MT ? 65535 : 16384))
+    if (d.agent_capacity < 1 || d.agent_capacity > (d.rng_mode == FFM_RNG_MT ? 65535 : 16383))
         return fail(FFM_E_INVALID, "agent_capacity");
     if (d.n_agents < 0 || d.n_agents > d.agent_capacity) return fail(FFM_E_INVALID, "n_agents > agent_capacity");
     if (d.rng_mode != FFM_RNG_PHILOX && d.rng_mode != FFM_RNG_MT) return fail(FFM_E_INVALID, "rng_mode");

@@ -241,6 +241,29 @@ struct SmBits {                  // batch kernel, next positions (exit cells exc
     }
 };
 
+// Batch kernel: the LDS grid carries the static map class of every cell (bits 14-15:
+// 0 free, 1 / 2 blocked, 3 exit) beside the index of the agent standing there (bits
+// 0-13, kGIdx = none; batched learners hold at most 16383 agents), so the state
+// encoder, the move candidates and the exit tests read one LDS word per cell instead of
+// an LDS word and the global 2-bit map.
+constexpr uint16_t kGIdx = 0x3FFF;
+struct SmGridC {                 // current positions
+    const uint16_t* grid;
+    __device__ int operator()(int c) const {
+        const uint32_t g = grid[c];
+        return (g & kGIdx) != kGIdx ? 1 : (int)(g >> 14);
+    }
+};
+struct SmBitsC {                 // next positions (exit cells excluded)
+    const uint16_t* grid;
+    const uint32_t* bits;
+    __device__ int operator()(int c) const {
+        const uint32_t b = bits[c >> 5];
+        const int m = (int)(grid[c] >> 14);
+        return ((b >> (c & 31)) & 1u) ? 1 : m;
+    }
+};
+
 // n / d for 0 <= n < 65536 through m = ceil(2^32 / d): (n * m) >> 32 (checked
 // exhaustively for every 2 <= d <= 65536; m = 0 encodes d = 1).  One v_mul_hi_u32
 // instead of a ~30-instruction integer divide.
@@ -557,6 +580,21 @@ __device__ __forceinline__ void moves5(const LearnArgs& a, int x, int y, const O
 
 // The exact kernel's moves: the a.nb neighbours in get_neighbors order (Neumann U, D,
 // L, R; Moore row-major, model/ffm_unified.py:173-185), then stay, with the validity mask.
+// moves5 on the class-carrying grid; cls[k] = the candidate's map class (2 off the map).
+__device__ __forceinline__ void moves5_grid(const LearnArgs& a, int x, int y, const uint16_t* grid, int* coord,
+                                            int* valid, int* inb, int* cls) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const int nx = k < 4 ? x + kNBx[k] : x, ny = k < 4 ? y + kNBy[k] : y;
+        inb[k] = nx >= 0 && nx < a.H && ny >= 0 && ny < a.W;
+        coord[k] = inb[k] ? nx * a.W + ny : x * a.W + y;
+        const uint32_t g = grid[coord[k]];
+        cls[k] = inb[k] ? (int)(g >> 14) : 2;
+        valid[k] = inb[k] && (cls[k] == 0 || cls[k] == 3) && (k == 4 || (g & kGIdx) == kGIdx);
+    }
+    valid[4] = 1;
+}
+
 template <class OCC>
 __device__ void moves_n(const LearnArgs& a, int x, int y, const OCC& occ, int* coord, int* valid, int* inb) {
     const int nb = a.nb;
@@ -1213,7 +1251,7 @@ void learn_batch_kernel(LearnArgs a) {
 #endif
     LSTAMP(0);
 
-    for (int c = tid; c < HW; c += LPE) grid[c] = kNone16;
+    for (int c = tid; c < HW; c += LPE) grid[c] = (uint16_t)((map2_at(a.map2, c) << 14) | kGIdx);
     if (DL) {
         const float* src = a.dff_in + (live ? e : 0) * (long long)HW;
         for (int c = tid; c < HW; c += LPE) dff[c] = src[c];
@@ -1238,7 +1276,7 @@ void learn_batch_kernel(LearnArgs a) {
         const int i = tid + j * LPE;
         p[j] = i < n ? a.pos[e * A + i] : 0;
         ia[j] = i;
-        if (i < n) grid[p[j]] = (uint16_t)i;
+        if (i < n) grid[p[j]] = (uint16_t)((grid[p[j]] & ~kGIdx) | (uint32_t)i);
     }
     if (RASTER) {
         __syncthreads();
@@ -1251,14 +1289,14 @@ void learn_batch_kernel(LearnArgs a) {
         const int c0 = w * cpw, c1 = min(c0 + cpw, HW);
         int cnt = 0;
         for (int c = c0 + lane; c - lane < c1; c += 64)
-            cnt += __popcll(__ballot(c < c1 && grid[c] != kNone16));
+            cnt += __popcll(__ballot(c < c1 && (grid[c] & kGIdx) != kGIdx));
         if (lane == 0) ws[w] = cnt;
         __syncthreads();
         int base = 0;
 #pragma unroll
         for (int q = 0; q < NW; q++) base += q < w ? ws[q] : 0;
         for (int c = c0 + lane; c - lane < c1; c += 64) {
-            const bool f = c < c1 && grid[c] != kNone16;
+            const bool f = c < c1 && (grid[c] & kGIdx) != kGIdx;
             const unsigned long long m = __ballot(f);
             if (f) req[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)c;
             if (a.trecs && lane < 64 / kTileCells) {
@@ -1276,7 +1314,7 @@ void learn_batch_kernel(LearnArgs a) {
         for (int j = 0; j < APT; j++) {
             const int r = tid + j * LPE;
             p[j] = r < n ? req[r] : 0;
-            ia[j] = r < n ? grid[p[j]] : r;
+            ia[j] = r < n ? (grid[p[j]] & kGIdx) : r;
         }
         __syncthreads();   // the list is read: decide may write req
         for (int c = tid; c < n; c += LPE) req[c] = kNone16;
@@ -1292,8 +1330,7 @@ void learn_batch_kernel(LearnArgs a) {
         hs.mx = a.hstat[3];
     }
     __syncthreads();
-    const SmGrid smc{a.map2, grid};
-    auto occ = [&](int c) { return grid[c] != kNone16; };
+    const SmGridC smc{grid};
     LSTAMP(1);
 
     // ---- decide --------------------------------------------------------------
@@ -1307,10 +1344,11 @@ void learn_batch_kernel(LearnArgs a) {
         const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
         skey[j] = encode(a, smc, x, y);
         int coord[5], valid[5], inb[5];
-        moves5(a, x, y, occ, coord, valid, inb);
+        int cls[5];
+        moves5_grid(a, x, y, grid, coord, valid, inb, cls);
         int ex = -1;                               // first exit among the neighbours
 #pragma unroll
-        for (int k = 3; k >= 0; k--) ex = inb[k] && map2_at(a.map2, coord[k]) == 3 ? k : ex;
+        for (int k = 3; k >= 0; k--) ex = inb[k] && cls[k] == 3 ? k : ex;
         Policy P;
         if (FFM_LABLATE & 4) {
             req[i * D] = (uint16_t)p[j];
@@ -1322,7 +1360,7 @@ void learn_batch_kernel(LearnArgs a) {
             if ((valid[0] | valid[1] | valid[2] | valid[3]) == 0) continue;
             int exv = -1;
 #pragma unroll
-            for (int k = 3; k >= 0; k--) exv = valid[k] && map2_at(a.map2, coord[k]) == 3 ? k : exv;
+            for (int k = 3; k >= 0; k--) exv = valid[k] && cls[k] == 3 ? k : exv;
             if (exv >= 0) {
                 wexit[j] = 1;
                 req[i] = (uint16_t)coord[exv];
@@ -1406,8 +1444,8 @@ void learn_batch_kernel(LearnArgs a) {
             for (int c5 = 0; c5 < 5; c5++) {
                 const int cx = c5 < 4 ? tx + kNBx[c5] : tx, cy = c5 < 4 ? ty + kNBy[c5] : ty;
                 if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
-                const int b = grid[cx * W + cy];
-                if (b == kNone16) continue;
+                const int b = grid[cx * W + cy] & kGIdx;
+                if (b == (int)kGIdx) continue;
 #pragma unroll
                 for (int d2 = 0; d2 < D; d2++) {
                     const int sq = b * D + d2;
@@ -1440,13 +1478,13 @@ void learn_batch_kernel(LearnArgs a) {
             for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
             *c = v;
         }
-        if (map2_at(a.map2, nxt[j]) != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
+        if ((grid[nxt[j]] >> 14) != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
     }
     __syncthreads();
     LSTAMP(3);
 
     // ---- learning (TD(0) critic, actor) --------------------------------------------------
-    const SmBits smn{a.map2, bits};
+    const SmBitsC smn{grid, bits};
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;   // recs in lane-rank order: the post kernel inherits the locality
@@ -1523,7 +1561,7 @@ void learn_batch_kernel(LearnArgs a) {
         // index through req (resolve's last read of it is behind the barrier above)
 #pragma unroll
         for (int j = 0; j < APT; j++)
-            if (tid + j * LPE < n) req[ia[j]] = map2_at(a.map2, nxt[j]) != 3 ? (uint16_t)nxt[j] : kNone16;
+            if (tid + j * LPE < n) req[ia[j]] = (grid[nxt[j]] >> 14) != 3 ? (uint16_t)nxt[j] : kNone16;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < APT; j++) {
@@ -1539,7 +1577,7 @@ void learn_batch_kernel(LearnArgs a) {
 #pragma unroll
         for (int j = 0; j < APT; j++) {
             const int i = tid + j * LPE;
-            const bool keep = i < n && map2_at(a.map2, nxt[j]) != 3;
+            const bool keep = i < n && (grid[nxt[j]] >> 14) != 3;
             int tot;
             const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
             if (keep) a.pos[e * A + base_ + off] = (uint16_t)nxt[j];
@@ -2856,7 +2894,7 @@ int learn_batch_block_size(int A) { return A <= 64 ? 64 : A <= 256 ? 256 : 1024;
 size_t learn_batch_smem_bytes(int HW, int A, int D) { return batch_carve(HW, A, D, 1).shared; }
 
 bool learn_batch_supported(int HW, int A, int D) {
-    return A <= 16384 && learn_batch_smem_bytes(HW, A, D) <= 160 * 1024;
+    return A <= 16383 && learn_batch_smem_bytes(HW, A, D) <= 160 * 1024;
 }
 
 hipError_t launch_learn_hstat(const LearnArgs& a, hipStream_t s) {

@@ -77,7 +77,7 @@ typedef struct {
     int32_t neighborhood;     /* 4 = "neumann", 8 = "moore" (model/ffm_core.py:28-34) */
     double k_S, k_D, diffuse, decay;   /* params, model/ffm_core.py:8-15 */
     int64_t n_envs;           /* E: independent environments on this device */
-    int32_t agent_capacity;   /* A: slots per env (>= n_agents; learners: <= 16384 batched, <= 65535 MT) */
+    int32_t agent_capacity;   /* A: slots per env (>= n_agents; learners: <= 16383 batched, <= 65535 MT) */
     int32_t n_agents;         /* N placed by reset / auto-reset */
     int32_t rng_mode;         /* FFM_RNG_* */
     int32_t auto_reset;       /* 1: an env emptied by a step is re-placed (Philox, keyed by that
@@ -286,7 +286,7 @@ int ffm_learner_delta_merge_async(ffm_learner* l, int32_t which, const uint64_t*
  * sync period 1): step_tiled_local runs the step and leaves one 16-B record
  * per agent (raster order) and per-env tile offsets in this learner's DEVICE buffers
  * (tiled_buffers: rec_bytes bytes of records, tstart_count uint16 offsets: agent ranks
- * below agent_capacity <= 16384); the ranks
+ * below agent_capacity <= 16383); the ranks
  * all-gather both, rank-major; step_tiled_apply sums every rank's records per tile of
  * cells into the replicated tables (inserting the slots other ranks created) and ends the
  * step.  Every rank holds, bit for bit, the tables one device stepping all envs would hold.
