@@ -48,12 +48,12 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
-    ap.add_argument("--steps", type=int, default=None, help="default 500 (configs 2-4), 50 (config 5)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 50 (configs 2-4), 5 (config 5)")
+    ap.add_argument("--steps", type=int, default=None, help="default 500 (config 2), 1500 (config 3: one episode), 300 (config 4), 50 (config 5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 50 (config 2), 20 (config 3), 30 (config 4), 5 (config 5)")
     ap.add_argument("--burn-in", type=int, default=None,
                     help="untimed steps after reset before the warmup, so the timed envs are desynchronised "
                          "(steady state) instead of all starting their first episode together; default 1000 "
-                         "(config 2), 400 (config 3), 0 (learner configs)")
+                         "(config 2), else 0")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
     ap.add_argument("--size", type=int, default=None)
     ap.add_argument("--agents", type=int, default=None)
@@ -79,14 +79,16 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (default: profiles/traffic_<H>x<W>_A<A>_E<E>.json)")
     a = ap.parse_args()
-    size, agents, envs, steps, warmup = {2: (12, 32, 65536, 500, 50), 3: (64, 512, 8192, 200, 20),
+    # config 3: an episode takes 1,491 +- 31 steps (oracle, 64 envs), so its envs stay in
+    # phase; every timed window spans one episode and averages a whole evacuation
+    size, agents, envs, steps, warmup = {2: (12, 32, 65536, 500, 50), 3: (64, 512, 8192, 1500, 20),
                                          4: (12, 32, 65536, 300, 30), 5: (256, 8192, 512, 50, 5)}[a.config]
     a.size = a.size or size
     a.agents = a.agents or agents
     a.envs = a.envs or envs
     a.steps = a.steps if a.steps is not None else steps
     a.warmup = a.warmup if a.warmup is not None else warmup
-    a.burn_in = a.burn_in if a.burn_in is not None else {2: 1000, 3: 400}.get(a.config, 0)
+    a.burn_in = a.burn_in if a.burn_in is not None else {2: 1000}.get(a.config, 0)
     return a
 
 
@@ -203,7 +205,10 @@ def main():
                              f"{args.neighborhood}, Philox seed {args.seed}, on-device auto-reset, "
                              + (f"steady state (envs desynchronised by a {args.burn_in}-step untimed burn-in "
                                 f"after reset)" if args.burn_in else
-                                "all envs start their first episode in phase (no burn-in)")),
+                                "all envs start their first episode in phase (no burn-in)"
+                                + (f"; {args.steps}-step timed windows, about one episode (1,491 +- 31 steps) "
+                                   f"each, so every window averages a whole evacuation"
+                                   if H == 64 and args.steps >= 1400 else ""))),
                 "burn_in_steps": args.burn_in,
                 "map": f"{H}x{W}", "agents_per_env": A, "envs_per_gpu": E,
                 "global_envs": E * world, "parallelism": f"env-sharded x{world}",
