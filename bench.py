@@ -142,7 +142,9 @@ def main():
     # Kernel time for the roofline: HIP events on the launch stream bracketing
     # nk back-to-back launches (a separate pass, so events do not perturb
     # `value`); per-launch event pairs would add their own gaps to each launch.
-    nk = min(args.steps, 200)
+    # nk = the window length, so the pass averages the same phases as a timed window
+    # (config 3: one episode, its in-phase reset burst included).
+    nk = min(args.steps, 2000)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
