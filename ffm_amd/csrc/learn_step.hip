@@ -1270,13 +1270,26 @@ void learn_batch_kernel(LearnArgs a) {
     // tiled step: records in raster order for the tile kernels, no
     // accumulator adds; set by the host for single-rank ffm_unified steps at block size 1
     const bool TILED = RASTER && a.trecs != nullptr;
-    int p[APT], ia[APT];
+    // Per-agent state, packed so the APT slots of a lane stay in registers (APT = 8 at
+    // C5: unpacked, the kernel spilled to scratch).  pa: cell (bits 0-15) | agent index
+    // (16-29).  sa, from decide on: act + 1 (0-2), avalid (3), wexit (4), and from
+    // resolve: coll + 1 (5-9), wins (10-13), next cell (16-31).
+    uint32_t pa[APT], sa[APT];
+#define BK_P(j) ((int)(pa[j] & 0xFFFFu))
+#define BK_IA(j) ((int)(pa[j] >> 16))
+#define BK_ACT(j) ((int)(sa[j] & 7u) - 1)
+#define BK_AVALID(j) ((int)((sa[j] >> 3) & 1u))
+#define BK_WEXIT(j) ((int)((sa[j] >> 4) & 1u))
+#define BK_COLL(j) ((int)((sa[j] >> 5) & 31u) - 1)
+#define BK_WINS(j) ((int)((sa[j] >> 10) & 15u))
+#define BK_NXT(j) ((int)(sa[j] >> 16))
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;
-        p[j] = i < n ? a.pos[e * A + i] : 0;
-        ia[j] = i;
-        if (i < n) grid[p[j]] = (uint16_t)((grid[p[j]] & ~kGIdx) | (uint32_t)i);
+        const int pj = i < n ? a.pos[e * A + i] : 0;
+        pa[j] = (uint32_t)pj | ((uint32_t)i << 16);
+        sa[j] = 0u;
+        if (i < n) grid[pj] = (uint16_t)((grid[pj] & ~kGIdx) | (uint32_t)i);
     }
     if (RASTER) {
         __syncthreads();
@@ -1313,8 +1326,8 @@ void learn_batch_kernel(LearnArgs a) {
 #pragma unroll
         for (int j = 0; j < APT; j++) {
             const int r = tid + j * LPE;
-            p[j] = r < n ? req[r] : 0;
-            ia[j] = r < n ? (grid[p[j]] & kGIdx) : r;
+            const int pj = r < n ? req[r] : 0;
+            pa[j] = (uint32_t)pj | ((uint32_t)(r < n ? (grid[pj] & kGIdx) : r) << 16);
         }
         __syncthreads();   // the list is read: decide may write req
         for (int c = tid; c < n; c += LPE) req[c] = kNone16;
@@ -1335,13 +1348,13 @@ void learn_batch_kernel(LearnArgs a) {
 
     // ---- decide --------------------------------------------------------------
     unsigned long long skey[APT];
-    int act[APT], avalid[APT], wexit[APT], hsl[APT];
+    int hsl[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = ia[j];
-        act[j] = -1; avalid[j] = 0; wexit[j] = 0; hsl[j] = -1; skey[j] = 0;
+        const int i = BK_IA(j);
+        sa[j] = 0u; hsl[j] = -1; skey[j] = 0;
         if (tid + j * LPE >= n) continue;
-        const int x = fdiv(p[j], a.mW), y = p[j] - x * W;
+        const int x = fdiv(BK_P(j), a.mW), y = BK_P(j) - x * W;
         skey[j] = encode(a, smc, x, y);
         int coord[5], valid[5], inb[5];
         int cls[5];
@@ -1351,8 +1364,8 @@ void learn_batch_kernel(LearnArgs a) {
         for (int k = 3; k >= 0; k--) ex = inb[k] && cls[k] == 3 ? k : ex;
         Policy P;
         if (FFM_LABLATE & 4) {
-            req[i * D] = (uint16_t)p[j];
-            act[j] = 4; avalid[j] = 1;
+            req[i * D] = (uint16_t)BK_P(j);
+            sa[j] = 5u | 8u;
             continue;
         }
         if (a.variant == kVarAC) {
@@ -1362,7 +1375,7 @@ void learn_batch_kernel(LearnArgs a) {
 #pragma unroll
             for (int k = 3; k >= 0; k--) exv = valid[k] && cls[k] == 3 ? k : exv;
             if (exv >= 0) {
-                wexit[j] = 1;
+                sa[j] |= 16u;
                 req[i] = (uint16_t)coord[exv];
                 continue;
             }
@@ -1375,7 +1388,7 @@ void learn_batch_kernel(LearnArgs a) {
         if (D == 1) {
             int k;
             if (ex >= 0) {
-                wexit[j] = 1;
+                sa[j] |= 16u;
                 k = ex;
             } else {
                 if (trained) {
@@ -1395,7 +1408,7 @@ void learn_batch_kernel(LearnArgs a) {
                 k = policy_draw(P, eps, rng);
             }
             req[i] = (uint16_t)coord[k];
-            act[j] = k; avalid[j] = valid[k];
+            sa[j] = (sa[j] & ~15u) | (uint32_t)(k + 1) | ((uint32_t)valid[k] << 3);
         } else {
             // model/ffm_actor_only.py:214-355: decisions for the neighbours before the
             // first exit, then the exit for the rest; the last one is the agent's action.
@@ -1415,8 +1428,7 @@ void learn_batch_kernel(LearnArgs a) {
                 }
                 req[i * 4 + d] = (uint16_t)coord[k];
             }
-            wexit[j] = ex >= 0;
-            act[j] = k; avalid[j] = valid[k];
+            sa[j] = (uint32_t)(k + 1) | ((uint32_t)valid[k] << 3) | ((ex >= 0 ? 1u : 0u) << 4);
         }
     }
     __syncthreads();
@@ -1426,12 +1438,11 @@ void learn_batch_kernel(LearnArgs a) {
     // Requesters of a target stand on it or next to it; a target's owner is its
     // smallest request seq (= the reference's dict order); every member draws
     // the winner rank from the owner's stream itself.
-    int nxt[APT], coll[APT], wins[APT];
 #pragma unroll
     for (int j = 0; j < APT; j++) {
-        const int i = ia[j];
-        nxt[j] = p[j]; coll[j] = -1; wins[j] = 0;
-        if (tid + j * LPE >= n) continue;
+        const int i = BK_IA(j);
+        int nxj = BK_P(j), clj = -1, wnj = 0;
+        if (tid + j * LPE < n) {
         int best_owner = -1, best_won_owner = -1;
 #pragma unroll
         for (int d = 0; d < D; d++) {
@@ -1460,25 +1471,27 @@ void learn_batch_kernel(LearnArgs a) {
                 PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)owner, kPurFriction);
                 w = (int)ps.randbelow((uint32_t)m);
             }
-            if (owner > best_owner) { best_owner = owner; coll[j] = m == 1 ? 0 : m - 1; }
+            if (owner > best_owner) { best_owner = owner; clj = m == 1 ? 0 : m - 1; }
             if (rank == w) {
-                wins[j]++;
-                if (owner > best_won_owner) { best_won_owner = owner; nxt[j] = T; }
+                wnj++;
+                if (owner > best_won_owner) { best_won_owner = owner; nxj = T; }
             }
         }
+        }
+        sa[j] = (sa[j] & 0x1Fu) | ((uint32_t)(clj + 1) << 5) | ((uint32_t)wnj << 10) | ((uint32_t)nxj << 16);
     }
     // deposits at the winners' own cells (distinct per agent: no races); every
     // agent's next cell joins the next state map unless it is an exit
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         if (tid + j * LPE >= n) continue;
-        if (wins[j]) {
-            float* c = dff + p[j];
+        if (BK_WINS(j)) {
+            float* c = dff + BK_P(j);
             float v = *c;
-            for (int q = 0; q < wins[j]; q++) v = v + 1.0f;
+            for (int q = 0; q < BK_WINS(j); q++) v = v + 1.0f;
             *c = v;
         }
-        if ((grid[nxt[j]] >> 14) != 3) atomicOr(&bits[nxt[j] >> 5], 1u << (nxt[j] & 31));
+        if ((grid[BK_NXT(j)] >> 14) != 3) atomicOr(&bits[BK_NXT(j) >> 5], 1u << (BK_NXT(j) & 31));
     }
     __syncthreads();
     LSTAMP(3);
@@ -1495,12 +1508,12 @@ void learn_batch_kernel(LearnArgs a) {
         do {
             if (i >= n || trained || (FFM_LABLATE & 2)) break;
             double r = a.step_penalty;
-            if (wexit[j]) r = r + a.exit_reward;
-            if (coll[j] >= 0) r = r + (double)coll[j] * a.collision_penalty;
+            if (BK_WEXIT(j)) r = r + a.exit_reward;
+            if (BK_COLL(j) >= 0) r = r + (double)BK_COLL(j) * a.collision_penalty;
             int sn = -1;
             double vn = 0.0;
-            if (!wexit[j]) {
-                const int nx = fdiv(nxt[j], a.mW), ny = nxt[j] - nx * W;
+            if (!BK_WEXIT(j)) {
+                const int nx = fdiv(BK_NXT(j), a.mW), ny = BK_NXT(j) - nx * W;
                 const unsigned long long nk = encode(a, smn, nx, ny);
                 if (a.V.dense_by) {
                     sn = (int)dense_slot(nk, a.V);
@@ -1525,27 +1538,27 @@ void learn_batch_kernel(LearnArgs a) {
             tdv = td;
             snv = sn;
             if (!actor) break;
-            if (act[j] < 0) break;
+            if (BK_ACT(j) < 0) break;
             if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
             if (hsl[j] < 0) break;
             if (TILED) {            // the tile kernels sum the increments (hsl == sv: one dense layout)
-                kk = avalid[j] ? act[j] : (int)kTileNoAct;
+                kk = BK_AVALID(j) ? BK_ACT(j) : (int)kTileNoAct;
                 break;
             }
             if (post_update) {
                 LearnRec rc;
-                rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = avalid[j] ? act[j] : -1;
+                rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = BK_AVALID(j) ? BK_ACT(j) : -1;
                 a.recs[e * A + i] = rc;
-            } else if (avalid[j] && !(FFM_LABLATE & 1)) {
-                acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + act[j]), fx(a.alpha_h * td));
+            } else if (BK_AVALID(j) && !(FFM_LABLATE & 1)) {
+                acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + BK_ACT(j)), fx(a.alpha_h * td));
             }
         } while (false);
         if (TILED) {
             if (vsl >= 0) {
                 TileRec rc;
                 rc.svk = (uint32_t)vsl | ((uint32_t)kk << 28);
-                rc.snf = (snv >= 0 ? (uint32_t)snv : kTileTerminal) | ((uint32_t)(wexit[j] ? 1 : 0) << 28) |
-                         ((uint32_t)(coll[j] + 1) << 29);
+                rc.snf = (snv >= 0 ? (uint32_t)snv : kTileTerminal) | ((uint32_t)BK_WEXIT(j) << 28) |
+                         ((uint32_t)(BK_COLL(j) + 1) << 29);
                 rc.td = tdv;
                 a.trecs[e * A + i] = rc;
             }
@@ -1561,7 +1574,7 @@ void learn_batch_kernel(LearnArgs a) {
         // index through req (resolve's last read of it is behind the barrier above)
 #pragma unroll
         for (int j = 0; j < APT; j++)
-            if (tid + j * LPE < n) req[ia[j]] = (grid[nxt[j]] >> 14) != 3 ? (uint16_t)nxt[j] : kNone16;
+            if (tid + j * LPE < n) req[BK_IA(j)] = (grid[BK_NXT(j)] >> 14) != 3 ? (uint16_t)BK_NXT(j) : kNone16;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < APT; j++) {
@@ -1577,10 +1590,10 @@ void learn_batch_kernel(LearnArgs a) {
 #pragma unroll
         for (int j = 0; j < APT; j++) {
             const int i = tid + j * LPE;
-            const bool keep = i < n && (grid[nxt[j]] >> 14) != 3;
+            const bool keep = i < n && (grid[BK_NXT(j)] >> 14) != 3;
             int tot;
             const int off = env_scan_flag<BS, LPE>(keep, ws, tot);
-            if (keep) a.pos[e * A + base_ + off] = (uint16_t)nxt[j];
+            if (keep) a.pos[e * A + base_ + off] = (uint16_t)BK_NXT(j);
             base_ += tot;
         }
     }
@@ -1610,6 +1623,14 @@ void learn_batch_kernel(LearnArgs a) {
                ts_[1] - ts_[0], ts_[2] - ts_[1], ts_[3] - ts_[2], ts_[4] - ts_[3], ts_[5] - ts_[4], ts_[6] - ts_[5]);
 
 #endif
+#undef BK_P
+#undef BK_IA
+#undef BK_ACT
+#undef BK_AVALID
+#undef BK_WEXIT
+#undef BK_COLL
+#undef BK_WINS
+#undef BK_NXT
     if (live && tid == 0) {
         a.cnt[e] = base_;
         a.nstart[e] = n;
