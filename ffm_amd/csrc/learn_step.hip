@@ -1347,15 +1347,21 @@ void learn_batch_kernel(LearnArgs a) {
     LSTAMP(1);
 
     // ---- decide --------------------------------------------------------------
-    unsigned long long skey[APT];
-    int hsl[APT];
+    // state keys: kept per slot when a lane walks few agents; with APT >= 4 (1,024-lane
+    // workgroups on large maps) the learn phase re-encodes them from the unchanged grid
+    // instead (twelve LDS reads), which keeps the slots' state in registers
+    constexpr bool KEYS = APT < 4;
+    unsigned long long skey[KEYS ? APT : 1];
+    int hsl[KEYS ? APT : 1];     // H slot of the decide phase's lookup (-1: none)
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = BK_IA(j);
-        sa[j] = 0u; hsl[j] = -1; skey[j] = 0;
+        sa[j] = 0u;
+        if (KEYS) { skey[j] = 0; hsl[j] = -1; }
         if (tid + j * LPE >= n) continue;
         const int x = fdiv(BK_P(j), a.mW), y = BK_P(j) - x * W;
-        skey[j] = encode(a, smc, x, y);
+        const unsigned long long sk = encode(a, smc, x, y);
+        if (KEYS) skey[j] = sk;
         int coord[5], valid[5], inb[5];
         int cls[5];
         moves5_grid(a, x, y, grid, coord, valid, inb, cls);
@@ -1392,17 +1398,19 @@ void learn_batch_kernel(LearnArgs a) {
                 k = ex;
             } else {
                 if (trained) {
-                    trained_policy(a, tab_find(a.Ht, skey[j]), coord, valid, dff, hs, P);
+                    trained_policy(a, tab_find(a.Ht, sk), coord, valid, dff, hs, P);
                 } else if (!actor) {
                     critic_policy(a, coord, valid, dff, P);
                 } else if (a.Ht.dense_by) {
-                    hsl[j] = (int)dense_slot(skey[j], a.Ht);
-                    actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, false, P);
-                    dense_ensure(a.Ht, (uint32_t)hsl[j], skey[j]);
+                    const int h = (int)dense_slot(sk, a.Ht);
+                    if (KEYS) hsl[j] = h;
+                    actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, false, P);
+                    dense_ensure(a.Ht, (uint32_t)h, sk);
                 } else {
-                    hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
-                    if (hsl[j] < 0) continue;
-                    actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, false, P);
+                    const int h = tab_get(a.Ht, sk, a.overflow);
+                    if (KEYS) hsl[j] = h;
+                    if (h < 0) continue;
+                    actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, false, P);
                 }
                 DrawPh rng(a, genv, (uint32_t)i);
                 k = policy_draw(P, eps, rng);
@@ -1413,9 +1421,10 @@ void learn_batch_kernel(LearnArgs a) {
             // model/ffm_actor_only.py:214-355: decisions for the neighbours before the
             // first exit, then the exit for the rest; the last one is the agent's action.
             if (ex != 0) {
-                hsl[j] = tab_get(a.Ht, skey[j], a.overflow);
-                if (hsl[j] < 0) continue;
-                actor_policy(a, tval(a.Ht, hsl[j]), coord, valid, dff, hs, true, P);
+                const int h = tab_get(a.Ht, sk, a.overflow);
+                if (KEYS) hsl[j] = h;
+                if (h < 0) continue;
+                actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, true, P);
             }
             int k = 4;
 #pragma unroll
@@ -1507,6 +1516,13 @@ void learn_batch_kernel(LearnArgs a) {
         int snv = -1, kk = (int)kTileNoAct;
         do {
             if (i >= n || trained || (FFM_LABLATE & 2)) break;
+            unsigned long long skj;
+            if (KEYS) {
+                skj = skey[j];
+            } else {
+                const int px = fdiv(BK_P(j), a.mW);
+                skj = encode(a, smc, px, BK_P(j) - px * W);
+            }
             double r = a.step_penalty;
             if (BK_WEXIT(j)) r = r + a.exit_reward;
             if (BK_COLL(j) >= 0) r = r + (double)BK_COLL(j) * a.collision_penalty;
@@ -1526,10 +1542,10 @@ void learn_batch_kernel(LearnArgs a) {
             }
             int sv;
             if (a.V.dense_by) {
-                sv = (int)dense_slot(skey[j], a.V);
-                dense_ensure(a.V, (uint32_t)sv, skey[j]);
+                sv = (int)dense_slot(skj, a.V);
+                dense_ensure(a.V, (uint32_t)sv, skj);
             } else {
-                sv = tab_get(a.V, skey[j], a.overflow);
+                sv = tab_get(a.V, skj, a.overflow);
             }
             if (sv < 0) break;
             const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
@@ -1539,18 +1555,21 @@ void learn_batch_kernel(LearnArgs a) {
             snv = sn;
             if (!actor) break;
             if (BK_ACT(j) < 0) break;
-            if (hsl[j] < 0) hsl[j] = tab_get(a.Ht, skey[j], a.overflow);   // dense: slot + insert, no probe
-            if (hsl[j] < 0) break;
+            // the decide phase's H slot; without KEYS, dense tables recompute it (the decide
+            // phase inserted it unless the agent was exit-forced) and hashed ones probe again
+            int hslj = KEYS ? hsl[j] : (a.Ht.dense_by && !BK_WEXIT(j) ? (int)dense_slot(skj, a.Ht) : -1);
+            if (hslj < 0) hslj = tab_get(a.Ht, skj, a.overflow);   // dense: slot + insert, no probe
+            if (hslj < 0) break;
             if (TILED) {            // the tile kernels sum the increments (hsl == sv: one dense layout)
                 kk = BK_AVALID(j) ? BK_ACT(j) : (int)kTileNoAct;
                 break;
             }
             if (post_update) {
                 LearnRec rc;
-                rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hsl[j]; rc.k = BK_AVALID(j) ? BK_ACT(j) : -1;
+                rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hslj; rc.k = BK_AVALID(j) ? BK_ACT(j) : -1;
                 a.recs[e * A + i] = rc;
             } else if (BK_AVALID(j) && !(FFM_LABLATE & 1)) {
-                acc_add(acc_at(a.Ht, (size_t)hsl[j] * 5 + BK_ACT(j)), fx(a.alpha_h * td));
+                acc_add(acc_at(a.Ht, (size_t)hslj * 5 + BK_ACT(j)), fx(a.alpha_h * td));
             }
         } while (false);
         if (TILED) {
