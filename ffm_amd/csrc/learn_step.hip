@@ -2190,12 +2190,12 @@ __device__ __forceinline__ void tile_h_end(const LearnArgs& a, int t, TileHCtx& 
 // The fast form: every record of the tile in one window (tile_window), at most
 // kTileList records, so at most kTileList (slot, action) pairs are touched.  The sums
 // live in one fixed-point word per touched pair, found through a pair -> index map:
-// 22 KB of LDS instead of 40 KB for every pair of the tile, so five workgroups share a
-// CU (the register limit) instead of three, and their dependent loads overlap.
-//   1. per record: the slot's first record (its owner, an LDS bit) loads the H row, the
-//      pair's first record takes an index (wave-aggregated counter), V reads in flight;
+// 23 KB of LDS instead of 40 KB for every pair of the tile, so six workgroups share a
+// CU (the LDS limit) instead of three, and their dependent loads overlap.
+//   1. per record: the slot's first record is its owner (an LDS bit), the pair's first
+//      record takes an index (wave-aggregated counter), V reads in flight;
 //   2. (barrier) every record adds its increment into its pair's word;
-//   3. (barrier) owners apply their rows from registers.
+//   3. (barrier) owners read their rows and apply them.
 // A tile whose records need more than one window is queued (tcand, count reset by
 // learn_tile_v_kernel) for learn_tile_h_wide_kernel.
 constexpr int kTilePairs = 256 * kTileCells * 5;
@@ -2243,11 +2243,6 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
         ix[j] = tile_idx(sv, qsh, Q, c0);
         const uint32_t bit = 1u << (ix[j] & 31);
         own[j] = !(atomicOr(&touched[ix[j] >> 5], bit) & bit);
-        if (own[j]) {
-            const double* vp = tval(a.Ht, sv);
-#pragma unroll
-            for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
-        }
         tile_h_vpair(a, rc[j], sv, vn[j], vs[j]);
         if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
         const int k = (int)(rc[j].svk >> 28);
@@ -2273,6 +2268,15 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
             atomicAdd(reinterpret_cast<unsigned long long*>(&hq[pid[pr[j]]]),
                       (unsigned long long)tile_h_q(a, rc[j], vn[j], vs[j]));
     __syncthreads();
+    // the owners' rows are read only now: with no row held across the sums the pass
+    // needs 70 VGPRs instead of 98, and six workgroups share a CU instead of five
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++) {
+        if (!own[j]) continue;
+        const double* vp = tval(a.Ht, rc[j].svk & 0x0FFFFFFFu);
+#pragma unroll
+        for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
+    }
 #pragma unroll
     for (int j = 0; j < kTileJ; j++) {
         if (!own[j]) continue;
