@@ -172,7 +172,7 @@ void core_group_kernel(CoreStepArgs a) {
 
     for (int i = threadIdx.x; i < PHW; i += 256) {
         pmap[i] = a.pmap[i];
-        psff[i] = reinterpret_cast<const float*>(a.psff)[i];
+        psff[i] = a.kS32 * reinterpret_cast<const float*>(a.psff)[i];   // the score's SFF term
     }
     for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
     for (int i = lane; i < G * TS; i += 64) tile[i] = 0.0f;
@@ -244,11 +244,12 @@ void core_group_kernel(CoreStepArgs a) {
                 const float* dk = tile + s * TS;
                 const int dd0 = 3 - 2 * cs_xp1(v);
                 bool to_exit = false;
-                uint32_t slot = lane_decide<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
+                uint32_t slot = lane_decide<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
                 slot = live ? slot : kNoReq;
                 if (slot == kPending)   // u near a cdf boundary: the exact NumPy arithmetic decides
-                    slot = NB == 4 ? lane_decide_exact<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, u53(pb.x, pb.y))
-                                   : lane_decide_exact_arr<NB>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32,
+                    slot = NB == 4 ? lane_decide_exact<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32,
+                                                                 u53(pb.x, pb.y))
+                                   : lane_decide_exact_arr<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32,
                                                                u53(pb.x, pb.y));
                 const uint32_t sd = slot <= (uint32_t)NB ? slot : DirCodes::kNoDir;
                 if (live)

@@ -37,7 +37,9 @@ __device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, int off, float
 
 // Candidate cells, validity and float32 scores of decide() (model/ffm_core.py:41-80)
 // for the agent at padded cell pp; shared by the fast and the exact pass.
-template <int NB>
+// PRE: psff holds f32(-k_S) * SFF already (the product the score takes, staged once per
+// workgroup), so kS is not applied again; results are identical.
+template <int NB, bool PRE = false>
 __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, const float* psff, const float* dk,
                                            int dd0, float kS, float kD, bool (&v)[NB + 1], float (&xs)[NB + 1],
                                            int& exit_slot) {
@@ -69,7 +71,7 @@ __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, c
     float sc[NB + 1];
 #pragma unroll
     for (int k = 0; k <= NB; k++) {
-        const float a = kS * sf[k];
+        const float a = PRE ? sf[k] : kS * sf[k];
         const float b = kD * df[k];
         sc[k] = a + b;                                                   // :77
     }
@@ -85,14 +87,14 @@ __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, c
 // kPending when u lies within the margin of a cdf boundary.  The fast path compares
 // a float32 copy of u (|error| < 2^-24) inside fast_choice's 1e-4 margin; selects
 // only, no branch.
-template <int NB>
+template <int NB, bool PRE = false>
 __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
                                                 const float* dk, int dd0, float kS, float kD, uint32_t wx,
                                                 bool& to_exit) {
     bool v[NB + 1];
     float xs[NB + 1];
     int exit_slot;
-    const int nvalid = lane_scores<NB>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
+    const int nvalid = lane_scores<NB, PRE>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
     float cum[NB + 1];
     float acc = 0.0f;
 #pragma unroll
@@ -124,7 +126,7 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
 // (max, sum, cdf total, search) with one candidate live at a time: this path sets
 // the kernel's register peak otherwise.  Neumann only (the 8-lane pairwise sum of
 // add.reduce needs every term at once: lane_decide_exact_arr).
-template <int NB>
+template <int NB, bool PRE = false>
 __device__ __forceinline__ float lane_score1(int k, int pp, int PW, const uint16_t* gk, const float* psff,
                                              const float* dk, int dd0, float kS, float kD, bool& valid) {
     int dx = 0, dy = 0;
@@ -136,33 +138,33 @@ __device__ __forceinline__ float lane_score1(int k, int pp, int PW, const uint16
     const int cell = pp + dx * PW + dy;
     const uint32_t g = gk[cell];
     valid = k == NB || g == 0u || g == 3u;
-    const float sa = kS * psff[cell];
+    const float sa = PRE ? psff[cell] : kS * psff[cell];
     const float sb = kD * dk[cell + dd0 - dx * 2];
     return sa + sb;                                                      // :77
 }
 
-template <int NB>
+template <int NB, bool PRE = false>
 __device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint16_t* gk, const float* psff,
                                                       const float* dk, int dd0, float kS, float kD, double u) {
     float mx = -__builtin_inff();
 #pragma unroll 1
     for (int k = 0; k <= NB; k++) {
         bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         mx = (v && sc > mx) ? sc : mx;                                   // :78
     }
     float sum = -0.0f;                                                   // add.reduce, < 8 terms: left fold
 #pragma unroll 1
     for (int k = 0; k <= NB; k++) {
         bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         if (v) sum += np_expf(sc - mx);                                  // :80-81
     }
     double last = 0.0;
 #pragma unroll 1
     for (int k = 0; k <= NB; k++) {
         bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         if (v) last += (double)(np_expf(sc - mx) / sum);                 // :83, cumsum in choice
     }
     const double inv = 1.0 / last;
@@ -171,7 +173,7 @@ __device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint
 #pragma unroll 1
     for (int k = 0; k < NB; k++) {
         bool v;
-        const float sc = lane_score1<NB>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         if (v) {
             run += (double)(np_expf(sc - mx) / sum);
             if (cdf_gt(run, last, inv, u)) {
@@ -184,13 +186,13 @@ __device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint
 }
 
 // The same with every term held (Moore: add.reduce pairs 8 terms).
-template <int NB>
+template <int NB, bool PRE = false>
 __device__ __forceinline__ uint32_t lane_decide_exact_arr(int pp, int PW, const uint16_t* gk, const float* psff,
                                                           const float* dk, int dd0, float kS, float kD, double u) {
     bool v[NB + 1];
     float xs[NB + 1];
     int exit_slot;
-    const int nvalid = lane_scores<NB>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
+    const int nvalid = lane_scores<NB, PRE>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
     float e[NB + 1];
 #pragma unroll
     for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;   // :80
