@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: learner GPU tests, then interleaved A/B (C5 and C4) of library builds.
-# Usage: bash tools/r03_k.sh <tag> "<libs>" ["<pytest files / -k>"]
+# Usage: bash tools/ab_learn.sh <tag> "<libs>" ["<pytest files>"]  (words, no -k expression)
 set -o pipefail
 OUT=gpurun_out/${1:-k}
 LIBS=${2:-"build_ab/base.so ffm_amd/_lib/libffm_amd.so"}
