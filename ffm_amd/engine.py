@@ -813,15 +813,16 @@ class Learner:
         return self._tiled
 
     def tiled_buffers(self):
-        """(records uint8 [E * A * 16], tile offsets [E * (NT + 1)]: uint16 values in an int16
-        tensor, the dtype every collective backend carries) torch views of
-        this learner's device buffers (zero copy), filled by step_tiled_local."""
+        """(records uint8 [E * A * 16], tile offsets uint8 [E * (NT + 1) * 2]: the bytes of
+        the uint16 offsets -- uint8 is carried by every collective backend, 16-bit integers
+        by neither gloo nor RCCL) torch views of this learner's device buffers (zero copy),
+        filled by step_tiled_local."""
         import torch
         r, t, nr, nt = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int64()
         _check(self._L.ffm_learner_tiled_buffers(self._h, C.byref(r), C.byref(nr), C.byref(t), C.byref(nt)))
         dev = torch.device("cuda", self.device)
         return (torch.as_tensor(_DevArray(r.value, nr.value, "|u1"), device=dev),
-                torch.as_tensor(_DevArray(t.value, nt.value, "<i2"), device=dev))
+                torch.as_tensor(_DevArray(t.value, 2 * nt.value, "|u1"), device=dev))
 
     def step_tiled_local(self, stream=None):
         _check(self._L.ffm_learner_step_tiled_local(self._h, _stream_handle(stream)))

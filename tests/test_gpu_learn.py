@@ -274,6 +274,28 @@ def test_learner_tiled_general_tile_pass_equals_accumulators(monkeypatch, n, N, 
         L.close()
 
 
+def test_learner_tiled_buffers_are_collective_dtypes():
+    """The tiled exchange's buffers are byte tensors: gloo and RCCL carry uint8, neither
+    carries 16-bit integers (the uint16 tile offsets once went out as int16 and the
+    all-gather raised "Invalid scalar type").  Sizes: 16 B per agent slot, 2 B per env
+    and tile boundary."""
+    import torch
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(64, 64)
+    L = _learner(m, l1_sff(m), "unified", n_envs=4, n_agents=600, mode="actor_only",
+                 params={"epsilon": 0.1, "block_size": 1}, rng="philox", seed=3, auto_reset=True, max_steps=20)
+    assert L.tiled
+    L.reset()
+    L.step_tiled_local()
+    recs, tst = L.tiled_buffers()
+    assert recs.dtype == torch.uint8 and tst.dtype == torch.uint8
+    assert recs.numel() == 4 * 600 * 16
+    assert tst.numel() == 4 * (64 * 64 // 4 + 1) * 2
+    L.step_tiled_apply(recs.data_ptr(), tst.data_ptr(), 4)     # ends the step (own records only)
+    L.get_state()
+    L.close()
+
+
 @pytest.mark.parametrize("mode", ["actor_only", "both"])
 def test_learner_tiled_shards_equal_one_learner(mode):
     """The tiled step across ranks (TableSync's exchange for tiled learners, coupled in one
