@@ -84,6 +84,7 @@ struct ffm_learner {
     ffm::TrajCapture traj{};                 // trajectory capture (n_sel = 0: off)
     int sync_period = 1;                     // tables applied every sync_period-th step
     int since_apply = 0;                     // steps since the last apply
+    bool external_sync = false;              // driven by a multi-rank TableSync: no local flush
     // tiled step: ffm_unified, dense tables at block size 1, the raster
     // batch kernel; ffm_learner_step at sync period 1 (the phased multi-rank step keeps
     // the accumulators, which its exchange sums)
@@ -514,8 +515,13 @@ static int phase_end(ffm_learner* l, hipStream_t s) {
 // applies.  Reading, replacing or re-periodising the tables at such a point applies them
 // first (as if the period ended with the last step) and restarts the period, so an
 // export never misses steps and a new period never stretches the current one.
-static int flush_pending(ffm_learner* l, hipStream_t s) {
-    if (l->mt || l->since_apply == 0 || l->phase != 0) return FFM_OK;
+//
+// A learner driven by a multi-rank exchange (external_sync) never flushes on its own: its
+// pending increments are only this rank's, and applying them alone would leave the ranks'
+// tables and apply schedules out of step.  Its exports are read-only (the tables as of
+// the last apply) and TableSync.flush() applies the exchanged deltas collectively
+// (ffm_learner_flush_begin / _end).
+static int apply_pending(ffm_learner* l, hipStream_t s) {
     if (!l->trained) HIP_TRY(ffm::launch_learn_apply(make_args(l), true, false, s));
     if (l->actor) {
         HIP_TRY(ffm::launch_learn_apply(make_args(l), false, true, s));
@@ -524,6 +530,11 @@ static int flush_pending(ffm_learner* l, hipStream_t s) {
     }
     l->since_apply = 0;
     return FFM_OK;
+}
+
+static int flush_pending(ffm_learner* l, hipStream_t s) {
+    if (l->mt || l->since_apply == 0 || l->phase != 0 || l->external_sync) return FFM_OK;
+    return apply_pending(l, s);
 }
 
 int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
@@ -816,6 +827,8 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
         }
     }
     hipStream_t s = (hipStream_t)stream;
+    if (l->external_sync && l->since_apply != 0 && !l->mt)
+        return fail(FFM_E_INVALID, "import between two applies of a shared learner: TableSync.flush() first");
     if (int rc = flush_pending(l, s)) return rc;
     if (which == FFM_TABLE_H) l->hstat_valid = l->tstats_valid = false;
     HIP_TRY(clear_table(l, *T, which == FFM_TABLE_V ? l->L.v_default : 0.0, s));
@@ -979,6 +992,8 @@ int ffm_learner_set_sync_period(ffm_learner* l, int32_t period) {
     if (!l || period < 1) return fail(FFM_E_INVALID, "sync period must be >= 1");
     if (l->mt && period != 1) return fail(FFM_E_INVALID, "the exact (MT) step applies every step");
     if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    if (l->since_apply != 0 && l->external_sync)
+        return fail(FFM_E_INVALID, "new sync period between two applies of a shared learner: TableSync.flush() first");
     if (l->since_apply != 0) {   // no stream argument: order behind every queued step
         HIP_TRY(hipDeviceSynchronize());
         if (int rc = flush_pending(l, nullptr)) return rc;
@@ -987,6 +1002,32 @@ int ffm_learner_set_sync_period(ffm_learner* l, int32_t period) {
     l->sync_period = period;
     l->since_apply = 0;
     return FFM_OK;
+}
+
+int ffm_learner_set_external_sync(ffm_learner* l, int32_t on) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    l->external_sync = on != 0;
+    return FFM_OK;
+}
+
+// The collective flush of a shared learner (TableSync.flush): begin opens a phase in which
+// the pending accumulators can be exchanged (delta export / merge, dense buffers / adopt),
+// end applies them (V, then H; the post-update actor increments of the pending steps were
+// added at their steps) and restarts the period.  *pending = 0: nothing to apply, no phase
+// opened (every rank of a TableSync agrees: the periods advance in lockstep).
+int ffm_learner_flush_begin(ffm_learner* l, int32_t* pending) {
+    if (!l || !pending) return fail(FFM_E_INVALID, "null argument");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    *pending = (!l->mt && l->since_apply != 0) ? 1 : 0;
+    if (*pending) l->phase = 6;
+    return FFM_OK;
+}
+
+int ffm_learner_flush_end(ffm_learner* l, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->phase != 6) return fail(FFM_E_INVALID, "flush_end must follow flush_begin with pending increments");
+    l->phase = 0;
+    return apply_pending(l, (hipStream_t)stream);
 }
 
 int ffm_learner_apply_due(ffm_learner* l, int32_t* due) {

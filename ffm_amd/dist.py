@@ -122,14 +122,18 @@ class TableSync:
         self.max_count = {"V": 0, "H": 0}   # largest touched count observed (reported)
         self.sync_period = int(sync_period)
         shard.set_sync_period(self.sync_period)
+        if hasattr(shard, "set_external_sync"):
+            shard.set_external_sync(True)   # exports read-only; pending increments flushed collectively
         self.dense = bool(getattr(shard, "dense_tables", False)) if dense is None else bool(dense)
-        self.tiled = bool(getattr(shard, "tiled", False)) and self.sync_period == 1 and dense is None
-        if self.tiled:      # the gathered records are indexed [rank * E + env]: equal E everywhere
-            n = torch.tensor([int(shard.n_envs)], dtype=torch.int64, device=device)
-            mx = n.clone()
-            dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-            dist.all_reduce(n, op=dist.ReduceOp.MIN, group=group)
-            self.tiled = int(n.item()) == int(mx.item())
+        # Tiled mode needs every rank tiled (a per-process property: FFM_TILED, sizes) with
+        # equal env counts (records are indexed [rank * E + env]).  Every rank takes part in
+        # the same collective, whatever its own flag, so a disagreement falls back instead
+        # of leaving some ranks inside a collective the others never enter.
+        local_tiled = bool(getattr(shard, "tiled", False)) and self.sync_period == 1 and dense is None
+        n_envs = int(getattr(shard, "n_envs", getattr(shard, "E", 0)))
+        v = torch.tensor([int(local_tiled), n_envs, -n_envs], dtype=torch.int64, device=device)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
+        self.tiled = bool(v[0].item()) and int(v[1].item()) == -int(v[2].item())
         self.bufs = {}
         self.bytes_sent = 0          # per rank, summed over exchanges (what this rank contributes)
         self.exchanges = 0
@@ -183,9 +187,12 @@ class TableSync:
             if e is not None:
                 e.synchronize()             # an exchange `lag` steps back: already done
             m = max(m, int(h.max()))
+        # the capacity follows the largest count ever observed, never a window's: counts
+        # fall near episode ends and jump back after lockstep resets, faster than the
+        # window-old estimate could grow again
         self.max_count[which] = max(self.max_count[which], m)
         cap = 1024
-        while cap < self.headroom * m and cap < self.max_capacity:
+        while cap < self.headroom * self.max_count[which] and cap < self.max_capacity:
             cap *= 2
         self.caps[which] = cap
         self.capacity = max(self.caps.values())
@@ -223,6 +230,19 @@ class TableSync:
         s.step_tiled_apply(g[0].data_ptr(), g[1].data_ptr(), self.world * s.n_envs)
         self.exchanges += 1
         self.bytes_sent += recs.numel() * recs.element_size() + tst.numel() * tst.element_size()
+
+    def flush(self):
+        """Apply the increments pending since the last apply (sync period K > 1) on every
+        rank, exchanged as at an apply step.  Collective: every rank calls it at the same
+        step.  Call it before reading the tables mid-period (an export of a shared learner
+        is read-only: it returns the tables as of the last apply)."""
+        s = self.shard
+        if self.tiled or not s.flush_begin():    # the periods advance in lockstep: all ranks agree
+            return
+        self._exchange("V")
+        if s.actor:
+            self._exchange("H")
+        s.flush_end()
 
     def step(self, n_steps: int = 1):
         s = self.shard

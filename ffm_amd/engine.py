@@ -41,6 +41,7 @@ EXPORTED = [
     "ffm_learner_delta_export_async", "ffm_learner_delta_merge_async", "ffm_learner_set_sync_period",
     "ffm_learner_apply_due", "ffm_learner_dense_buffers", "ffm_learner_dense_adopt",
     "ffm_learner_tiled_buffers", "ffm_learner_step_tiled_local", "ffm_learner_step_tiled_apply",
+    "ffm_learner_set_external_sync", "ffm_learner_flush_begin", "ffm_learner_flush_end",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -151,6 +152,9 @@ def load_library():
     L.ffm_learner_step_tiled_local.argtypes = [P, P]
     L.ffm_learner_step_tiled_apply.argtypes = [P, P, P, i64, P]
     L.ffm_learner_drain_trajectory.argtypes = [P, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
+    L.ffm_learner_set_external_sync.argtypes = [P, i32]
+    L.ffm_learner_flush_begin.argtypes = [P, C.POINTER(i32)]
+    L.ffm_learner_flush_end.argtypes = [P, P]
     for name in EXPORTED:
         if name != "ffm_last_error":
             getattr(L, name).restype = C.c_int
@@ -771,6 +775,20 @@ class Learner:
     def set_sync_period(self, k: int):
         """Apply the tables every k-th step (increments of k steps accumulate; default 1)."""
         _check(self._L.ffm_learner_set_sync_period(self._h, int(k)))
+
+    def set_external_sync(self, on: bool = True):
+        """Tables shared with other ranks (TableSync): exports are read-only and the pending
+        increments are applied only collectively (flush_begin / flush_end)."""
+        _check(self._L.ffm_learner_set_external_sync(self._h, int(bool(on))))
+
+    def flush_begin(self) -> bool:
+        """True: increments are pending and a flush phase is open (exchange, then flush_end)."""
+        p = C.c_int32()
+        _check(self._L.ffm_learner_flush_begin(self._h, C.byref(p)))
+        return bool(p.value)
+
+    def flush_end(self, stream=None):
+        _check(self._L.ffm_learner_flush_end(self._h, _stream_handle(stream)))
 
     def apply_due(self) -> bool:
         d = C.c_int32()

@@ -305,6 +305,15 @@ int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const u
  * restarts the period. */
 int ffm_learner_set_sync_period(ffm_learner* l, int32_t period);
 int ffm_learner_apply_due(ffm_learner* l, int32_t* due);
+/* A learner whose tables are shared with other ranks (TableSync sets it): an export is
+ * read-only (the tables as of the last apply: the pending increments are only this rank's),
+ * an import or a new period between two applies fails, and the pending increments are
+ * applied collectively: flush_begin (*pending = 1 opens a phase in which the deltas are
+ * exchanged as in a step) -> exchange V and H -> flush_end (applies them, restarts the
+ * period).  *pending = 0: nothing pending, no phase opened. */
+int ffm_learner_set_external_sync(ffm_learner* l, int32_t on);
+int ffm_learner_flush_begin(ffm_learner* l, int32_t* pending);
+int ffm_learner_flush_end(ffm_learner* l, void* stream);
 /* Dense (ffm_unified rank-key) tables: the device fixed-point accumulators (acc_count
  * int64) and presence bitmap (present_words u32), for an all-reduce of the increments;
  * dense_adopt then takes the presence union of all ranks (a DEVICE bitmap): slots other

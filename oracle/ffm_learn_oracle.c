@@ -995,6 +995,15 @@ void ffo_lbatch_post(ffo_lbatch* b) {
         }
 }
 
+/* The pending increments of V and H applied at once, no post-update pass (the post
+ * increments of the pending steps were added at their steps): ffm_learner_flush_end. */
+void ffo_lbatch_flush(ffo_lbatch* b) {
+    const ffo_learn_cfg* c = b->c;
+    ffo_tab_apply(b->V);
+    if (c->variant == FFO_VAR_ACTOR_ONLY || (c->variant == FFO_VAR_UNIFIED && c->mode != FFO_MODE_CRITIC))
+        ffo_tab_apply(b->Ht);
+}
+
 void ffo_lbatch_apply(ffo_lbatch* b, int which) {
     if (which == 1) { ffo_tab_apply(b->Ht); return; }
     ffo_tab_apply(b->V);

@@ -94,6 +94,7 @@ int ffo_lbatch_local(ffo_lbatch* b, uint16_t* pos, int32_t* counts, float* dff, 
 void ffo_lbatch_set_placement(ffo_lbatch* b, const uint16_t* cells, int32_t count);
 void ffo_lbatch_apply(ffo_lbatch* b, int which);
 void ffo_lbatch_post(ffo_lbatch* b);
+void ffo_lbatch_flush(ffo_lbatch* b);
 /* Episode ends; log (may be NULL) receives one record per ended episode:
  * {global env, index of the episode, its steps, 1 if emptied / 0 if truncated};
  * returns the record count. */

@@ -81,6 +81,7 @@ def _lib():
         L.ffo_lbatch_local.restype = C.c_int
         L.ffo_lbatch_apply.argtypes = [P, C.c_int]
         L.ffo_lbatch_post.argtypes = [P]
+        L.ffo_lbatch_flush.argtypes = [P]
         L.ffo_lbatch_end.argtypes = [P, P, P, P, P, P, C.c_uint64, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_int64, P]
         L.ffo_lbatch_end.restype = C.c_int64
@@ -252,6 +253,19 @@ class Shard:
 
     def apply_due(self) -> bool:
         return self.since_apply + 1 >= self.sync_period
+
+    def set_external_sync(self, on: bool = True):
+        """The engine's shared-learner flag: the CPU tables are read-only on export anyway."""
+        self.external_sync = bool(on)
+
+    def flush_begin(self) -> bool:
+        return self.since_apply != 0
+
+    def flush_end(self):
+        """Apply the pending (exchanged) increments of V and H without the post-update pass
+        (ffm_learner_flush_end) and restart the period."""
+        _lib().ffo_lbatch_flush(self.b)
+        self.since_apply = 0
 
     def step_apply(self, which):
         if self.apply_due():

@@ -107,9 +107,12 @@ def sorted_tables(learn):
     return out
 
 
-def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1, sync_period=1, steps=LEARN_STEPS):
+def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1, sync_period=1, steps=LEARN_STEPS,
+                     flush_at=None):
     """Single shard (or `coupled_shards` shards coupled in-process) of the batched
-    learning step on the CPU restatement, tables applied every `sync_period` steps."""
+    learning step on the CPU restatement, tables applied every `sync_period` steps
+    (flush_at: the pending increments applied after that many steps, as
+    TableSync.flush does; the tables right after it are returned as well)."""
     from oracle import learn as LO
     from ffm_amd.dist import shard_range, step_coupled
     m, s = room()
@@ -119,14 +122,23 @@ def run_learn_oracle(variant, mode, env_base, n, coupled_shards=1, sync_period=1
         L = LO.Learn(m, s, variant, mode, learn_params(variant), log2_cap=20)
         learns.append(L)
         shards.append(LO.Shard(L, c, LEARN_N, LEARN_N, SEED, env_base + b, LEARN_MAX))
+    mid = None
+    if flush_at is not None:
+        assert coupled_shards == 1
+        step_coupled(shards, flush_at, device="cpu", sync_period=sync_period)
+        if shards[0].flush_begin():
+            shards[0].flush_end()
+        mid = sorted_tables(learns[0])
+        steps -= flush_at
     step_coupled(shards, steps, device="cpu", sync_period=sync_period)
     cat = lambda f: np.concatenate([f(x) for x in shards])
-    return (cat(lambda x: x.pos), cat(lambda x: x.counts), cat(lambda x: x.dff), cat(lambda x: x.episodes),
-            cat(lambda x: x.ep_steps), sorted_tables(learns[0])), [sorted_tables(L) for L in learns]
+    out = ((cat(lambda x: x.pos), cat(lambda x: x.counts), cat(lambda x: x.dff), cat(lambda x: x.episodes),
+            cat(lambda x: x.ep_steps), sorted_tables(learns[0])), [sorted_tables(L) for L in learns])
+    return out if flush_at is None else out + (mid,)
 
 
 def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_period=1, steps=LEARN_STEPS,
-                 adaptive=False):
+                 adaptive=False, flush_at=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -140,7 +152,18 @@ def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_peri
             sync = TableSync(shard, device="cpu", capacity=None, sync_period=sync_period, adapt_every=4, lag=2)
         else:
             sync = TableSync(shard, device="cpu", capacity=8192, sync_period=sync_period)
-        sync.step(steps)
+        mid = None
+        if flush_at is not None:      # a collective flush in the middle of a sync period
+            sync.step(flush_at)
+            assert not shard.apply_due() or sync_period == 1
+            sync.flush()
+            assert shard.since_apply == 0
+            mids = [None] * world
+            dist.all_gather_object(mids, sorted_tables(L))
+            mid = mids
+            sync.step(steps - flush_at)
+        else:
+            sync.step(steps)
         assert sync.exchanges > 0
         parts = {}
         for name, a in (("pos", shard.pos), ("cnt", shard.counts), ("dff", shard.dff), ("eps", shard.episodes),
@@ -155,6 +178,10 @@ def learn_worker(rank, world, port, n_global, variant, mode, out_path, sync_peri
             for r in range(1, world):      # every rank ends with the same tables
                 for k, v in tabs[r].items():
                     summ[f"r{r}_{k}"] = v
+            if mid is not None:
+                for r in range(world):
+                    for k, v in mid[r].items():
+                        summ[f"mid{r}_{k}"] = v
             summ["caps"] = np.array([sync.caps["V"], sync.caps["H"]])
             summ["max_count"] = np.array([sync.max_count["V"], sync.max_count["H"]])
             np.savez(out_path, **summ)

@@ -145,3 +145,26 @@ def test_gloo_world2_adaptive_record_capacity(variant, mode, tmp_path):
     caps, mx = got["caps"], got["max_count"]
     assert (mx > 0).all() or variant == "ac"
     assert caps[0] < (1 << 17) and caps[0] >= 2 * mx[0]
+
+
+@pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None)])
+def test_gloo_world2_flush_mid_period_keeps_ranks_in_step(variant, mode, tmp_path):
+    """a sharded K = 4 run that reads its tables in the middle of a period.
+    TableSync.flush() exchanges the pending deltas and applies them on every rank at the
+    same step, so after it both ranks hold the same tables (== one batch of all envs
+    flushed at that step), their periods restart together, and the rest of the run still
+    equals the single-process run bit for bit."""
+    n, steps, flush_at = 37, 50, 22      # 22 = 5 periods of 4 + 2 pending steps; 28 more: 7 periods
+    out = str(tmp_path / "learn.npz")
+    mp.spawn(W.learn_worker, args=(2, _port(), n, variant, mode, out, 4, steps, False, flush_at), nprocs=2,
+             join=True)
+    got = dict(np.load(out))
+    single, _, mid = W.run_learn_oracle(variant, mode, 0, n, sync_period=4, steps=steps, flush_at=flush_at)
+    want = W.learn_summary(single)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), k
+        if k.startswith(("V_", "H_")):
+            assert np.array_equal(got[f"r1_{k}"], want[k]), f"rank 1 {k}"
+    for k, v in mid.items():
+        for r in (0, 1):
+            assert np.array_equal(got[f"mid{r}_{k}"], v), f"rank {r} {k} after the flush"
