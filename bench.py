@@ -343,8 +343,10 @@ def bench_learner(args, world, rank, torch, dist):
     torch.cuda.synchronize()
     print(f"[bench] config {args.config}: warmup done", file=sys.stderr, flush=True)
     sent0 = sync.bytes_sent if world > 1 else 0
+    recv0 = getattr(sync, "received_bytes", 0) if world > 1 else 0
     reps = timed_repeats(args, world, dist, torch, lambda: run(args.steps), lambda: L.counters(stream))
     sent_timed = (sync.bytes_sent - sent0) if world > 1 else 0
+    recv_timed = (getattr(sync, "received_bytes", 0) - recv0) if world > 1 else 0
     elapsed, agent_steps = reps["elapsed"], reps["agent_steps"]
     print(f"[bench] timed regions {reps['summary']['elapsed_s']} s", file=sys.stderr, flush=True)
     nk = min(args.steps, 100)
@@ -388,9 +390,14 @@ def bench_learner(args, world, rank, torch, dist):
             "step_ms_events": step_ms,
             "tables": {"V": v_size, "H": h_size},
             "table_sync": (dict({"period": args.sync_period,
-                                 "mode": ("tiled records all-gather" if sync.tiled else
+                                 "mode": ("owner-sharded tiles: records all-to-all, updates all-gathered"
+                                          if getattr(sync, "owner", False) else
+                                          "tiled records all-gather" if sync.tiled else
                                           "dense all-reduce" if sync.dense else "records (adaptive capacity)"),
                                  "bytes_per_rank_per_step": sent_timed / (reps["summary"]["n"] * args.steps),
+                                 **({"received_bytes_per_rank_per_step":
+                                     recv_timed / (reps["summary"]["n"] * args.steps)}
+                                    if getattr(sync, "owner", False) else {}),
                                  "note": "bytes this rank contributes to the collectives per step, over the "
                                          "timed regions"},
                                 **({} if sync.dense or sync.tiled else {"record_capacity": dict(sync.caps),

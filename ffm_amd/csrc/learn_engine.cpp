@@ -89,6 +89,7 @@ struct ffm_learner {
     // batch kernel; ffm_learner_step at sync period 1 (the phased multi-rank step keeps
     // the accumulators, which its exchange sums)
     int eps_phase = 0;                       // ffm_learner_set_epsilon_phase
+    long long eps_stride = 1;
     bool tiled_ok = false;
     bool tstats_valid = false;               // d_tstats summarises the current H
     int NT = 0;
@@ -97,6 +98,26 @@ struct ffm_learner {
     double* d_tstats = nullptr;
     int* d_tdirty = nullptr;
     int* d_tcand = nullptr;
+    // tile-major records and the owner-sharded exchange
+    bool tile_major = true;                  // FFM_TILE_MAJOR=0: the env-major tile passes
+    int ow = 1, orank = 0, ths = 0;          // ranks, this rank, header row stride
+    uint32_t* d_pe = nullptr;                // [E][NT] records of tile t in envs before e
+    uint32_t* d_ttot = nullptr;              // [NT] records of the tiles before t in its ownership chunk
+    uint32_t* d_toff = nullptr;              // [NT] + chunk sums and offsets
+    uint32_t* d_hdr = nullptr;               // [ow][ths] per destination: its tiles' record offsets
+    ffm::TileRec* d_pack = nullptr;          // [E][A] records, grouped by destination, tile-major
+    long long* d_xcnt = nullptr;             // [kMaxOwners + 2] records per destination, new V / H slots
+    uint32_t* d_newv = nullptr;              // [2 E A] new V slots of the step
+    uint32_t* d_newh = nullptr;              // [2 E A] new H slots (the V list's capacity: one stride)
+    uint32_t* d_vslot = nullptr;             // owner outputs, grown on demand
+    double* d_vval = nullptr;
+    uint32_t* d_hkey = nullptr;
+    long long* d_hq = nullptr;
+    unsigned long long* d_on = nullptr;      // [2] V / H output counts
+    size_t ocap = 0;
+    double* d_tsum = nullptr;                // [ths][5] this rank's tile summaries
+    const ffm::TileRec* own_recs = nullptr;  // the received records of the current owner step
+    const uint32_t* own_hdr = nullptr;
     DevTable V, H;
 };
 
@@ -120,7 +141,9 @@ static void release(ffm_learner* l) {
     void* bufs[] = {l->d_map, l->d_map2, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
-                    l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand};
+                    l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand,
+                    l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_pack, l->d_xcnt, l->d_newv, l->d_newh,
+                    l->d_vslot, l->d_vval, l->d_hkey, l->d_hq, l->d_on, l->d_tsum};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
     free_traj(l);
@@ -204,6 +227,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.eps_start = l->L.eps_start; a.eps_end = l->L.eps_end;
     a.eps_offset = l->L.eps_offset; a.eps_span = l->L.eps_span;
     a.eps_phase = l->eps_phase;
+    a.eps_stride = l->eps_stride;
     a.eplog = l->d_eplog; a.eplog_n = l->d_eplog_n; a.eplog_cap = l->eplog_cap;
     auto magic = [](int div) { return div <= 1 ? 0u : (uint32_t)(((1ull << 32) + (unsigned)div - 1) / (unsigned)div); };
     a.mW = magic(d.W);
@@ -401,12 +425,22 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     }
     if (l->tiled_ok) {
         l->NT = (HW + ffm::kTileCells - 1) / ffm::kTileCells;
+        const char* tm = getenv("FFM_TILE_MAJOR");
+        l->tile_major = !(tm && tm[0] == '0');
+        l->ths = l->NT + 1;
         if (hipMalloc((void**)&l->d_trecs, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
             hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 2) != hipSuccess ||
             hipMalloc((void**)&l->d_tstats, (size_t)l->NT * 32) != hipSuccess ||
             hipMalloc((void**)&l->d_tdirty, (size_t)l->NT * 4) != hipSuccess ||
             hipMalloc((void**)&l->d_tcand, (size_t)(l->NT + 1) * 4) != hipSuccess ||
-            hipMemset(l->d_tdirty, 0, (size_t)l->NT * 4) != hipSuccess)
+            hipMemset(l->d_tdirty, 0, (size_t)l->NT * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_pe, E * (size_t)l->NT * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_ttot, (size_t)l->NT * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_toff, ((size_t)l->NT + 2 * ((size_t)l->NT / ffm::kOwnChunk + 1)) * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_hdr, (size_t)l->ths * 4) != hipSuccess ||
+            hipMalloc((void**)&l->d_pack, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
+            hipMalloc((void**)&l->d_xcnt, (ffm::kMaxOwners + 2) * 8) != hipSuccess ||
+            hipMalloc((void**)&l->d_on, 16) != hipSuccess)
             return cleanup(fail(FFM_E_NOMEM, "hipMalloc (tiled step)"));
     }
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
@@ -553,6 +587,7 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             continue;
         }
         if (l->tiled_ok && l->sync_period == 1) {
+            if (l->ow > 1) return fail(FFM_E_INVALID, "an owner-sharded learner steps through its exchange (TableSync)");
             // tiled: records -> per-tile sums in LDS -> applied (no accumulators, no full-table pass)
             if (l->actor && !l->tstats_valid) {
                 HIP_TRY(ffm::launch_learn_tiles(make_args(l), true, s));
@@ -561,6 +596,17 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             ffm::LearnArgs a = make_args(l);
             a.trecs = l->d_trecs;
             HIP_TRY(ffm::launch_learn_batch(a, s));
+            if (l->tile_major) {     // records reordered tile-major, then the passes
+                a.ow = 1;
+                a.orank = 0;
+                a.ochunk = ffm::kOwnChunk;
+                a.ths = l->ths;
+                HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt, l->d_pack, s));
+                a.trecs = l->d_pack;
+                a.thdr = l->d_hdr;
+                a.tR = 1;
+                a.NTk = l->NT;
+            }
             HIP_TRY(ffm::launch_learn_tiles(a, false, s));
             if (int rc = phase_end(l, s)) return rc;
             continue;
@@ -933,9 +979,200 @@ int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const u
     return rc;
 }
 
+// ---- owner-sharded tiled step ---------------------------------------
+int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
+    if (world < 1 || world > ffm::kMaxOwners || rank < 0 || rank >= world)
+        return fail(FFM_E_INVALID, "tile owners: 1 <= world <= 64, 0 <= rank < world");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    if (!l->tile_major && world > 1) return fail(FFM_E_UNSUPPORTED, "owner sharding needs tile-major records");
+    HIP_TRY(hipDeviceSynchronize());
+    int mx = 0;
+    for (int q = 0; q < world; q++) mx = std::max(mx, ffm::owner_tiles(l->NT, world, ffm::kOwnChunk, q));
+    const size_t E = (size_t)l->d.n_envs, A = (size_t)l->d.agent_capacity;
+    (void)hipFree(l->d_hdr);
+    (void)hipFree(l->d_tsum);
+    (void)hipFree(l->d_newv);
+    (void)hipFree(l->d_newh);
+    l->d_hdr = nullptr; l->d_tsum = nullptr; l->d_newv = nullptr; l->d_newh = nullptr;
+    l->ow = world;
+    l->orank = rank;
+    l->ths = mx + 1;
+    if (hipMalloc((void**)&l->d_hdr, (size_t)world * l->ths * 4) != hipSuccess ||
+        hipMalloc((void**)&l->d_tsum, (size_t)l->ths * 5 * 8) != hipSuccess ||
+        hipMalloc((void**)&l->d_newv, 2 * E * A * 4) != hipSuccess ||
+        hipMalloc((void**)&l->d_newh, 2 * E * A * 4) != hipSuccess) {
+        l->ow = 1;
+        return fail(FFM_E_NOMEM, "hipMalloc (owner exchange)");
+    }
+    HIP_TRY(hipMemset(l->d_hdr, 0, (size_t)world * l->ths * 4));
+    return FFM_OK;
+}
+
+int ffm_learner_owner_buffers(ffm_learner* l, ffm_owner_buffers* b) {
+    if (!l || !b) return fail(FFM_E_INVALID, "null argument");
+    if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
+    const size_t E = (size_t)l->d.n_envs, A = (size_t)l->d.agent_capacity;
+    b->world = l->ow;
+    b->rank = l->orank;
+    b->send_recs = l->d_pack;
+    b->send_rec_capacity = (int64_t)(E * A);
+    b->send_hdr = l->d_hdr;
+    b->hdr_stride = l->ths;
+    b->counts = reinterpret_cast<int64_t*>(l->d_xcnt);
+    b->new_v = l->d_newv;
+    b->new_h = l->d_newh;
+    b->new_v_capacity = (int64_t)(2 * E * A);
+    b->new_h_capacity = (int64_t)(2 * E * A);
+    b->v_slot = l->d_vslot;
+    b->v_val = l->d_vval;
+    b->h_key = l->d_hkey;
+    b->h_q = reinterpret_cast<int64_t*>(l->d_hq);
+    b->out_counts = reinterpret_cast<int64_t*>(l->d_on);
+    b->out_capacity = (int64_t)l->ocap;
+    b->tsum = l->d_tsum;
+    b->tsum_count = (int64_t)ffm::owner_tiles(l->NT, l->ow, ffm::kOwnChunk, l->orank);
+    return FFM_OK;
+}
+
+static ffm::LearnArgs owner_args(ffm_learner* l) {
+    ffm::LearnArgs a = make_args(l);
+    a.ow = l->ow;
+    a.orank = l->orank;
+    a.ochunk = ffm::kOwnChunk;
+    a.ths = l->ths;
+    a.NTk = ffm::owner_tiles(l->NT, l->ow, ffm::kOwnChunk, l->orank);
+    return a;
+}
+
+static ffm::OwnerCounts owner_counts(const int64_t* c, int ranks, int64_t step = 1) {
+    ffm::OwnerCounts oc{};
+    for (int r = 0; r < ranks; r++) oc.n[r] = c ? (long long)c[(size_t)r * step] : 0;
+    return oc;
+}
+
+int ffm_learner_step_owner_local(ffm_learner* l, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (!l->tiled_ok || l->sync_period != 1 || !l->tile_major)
+        return fail(FFM_E_UNSUPPORTED, "owner step: tiled learner, tile-major records, sync period 1");
+    if (!l->d_newv) return fail(FFM_E_INVALID, "owner step: ffm_learner_set_tile_owners first");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "step_owner_local: previous step not ended");
+    if (int rc = async_overflow(l)) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (l->actor && !l->tstats_valid) {     // every rank: the same tables, the same summaries
+        HIP_TRY(ffm::launch_learn_tiles(make_args(l), true, s));
+        l->tstats_valid = l->hstat_valid = true;
+    }
+    ffm::LearnArgs a = owner_args(l);
+    a.trecs = l->d_trecs;
+    HIP_TRY(ffm::launch_learn_batch(a, s));
+    HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt, l->d_pack, s));
+    HIP_TRY(ffm::launch_learn_new_slots(l->V.t, l->d_newv, l->d_xcnt + l->ow, s));
+    if (l->actor) HIP_TRY(ffm::launch_learn_new_slots(l->H.t, l->d_newh, l->d_xcnt + l->ow + 1, s));
+    else HIP_TRY(hipMemsetAsync(l->d_xcnt + l->ow + 1, 0, 8, s));
+    l->phase = 7;
+    return FFM_OK;
+}
+
+int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, const int64_t* recv_counts,
+                             const uint32_t* d_new_v, const uint32_t* d_new_h, const int64_t* new_counts,
+                             int64_t new_stride, void* stream) {
+    if (!l || !d_hdrs || !recv_counts || !new_counts) return fail(FFM_E_INVALID, "null argument");
+    if (l->phase != 7) return fail(FFM_E_INVALID, "step_owner_v must follow step_owner_local");
+    hipStream_t s = (hipStream_t)stream;
+    long long total = 0;
+    for (int r = 0; r < l->ow; r++) {
+        if (recv_counts[r] < 0) return fail(FFM_E_INVALID, "negative record count");
+        total += recv_counts[r];
+    }
+    if (total >= (1ll << 32)) return fail(FFM_E_INVALID, "owner step: 2^32 records or more");
+    if (total > 0 && !d_recs) return fail(FFM_E_INVALID, "null records");
+    // the outputs: at most one V value and one H increment per (slot, action) per record
+    if ((size_t)total > l->ocap) {
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(l->d_vslot); (void)hipFree(l->d_vval); (void)hipFree(l->d_hkey); (void)hipFree(l->d_hq);
+        l->d_vslot = nullptr; l->d_vval = nullptr; l->d_hkey = nullptr; l->d_hq = nullptr;
+        const size_t cap = std::max<size_t>((size_t)total + (size_t)total / 4, 1 << 16);
+        if (hipMalloc((void**)&l->d_vslot, cap * 4) != hipSuccess || hipMalloc((void**)&l->d_vval, cap * 8) != hipSuccess ||
+            hipMalloc((void**)&l->d_hkey, cap * 4) != hipSuccess || hipMalloc((void**)&l->d_hq, cap * 8) != hipSuccess) {
+            l->ocap = 0;
+            return fail(FFM_E_NOMEM, "hipMalloc (owner outputs)");
+        }
+        l->ocap = cap;
+    }
+    // the other ranks' new slots join this rank's tables (presence, key, order)
+    HIP_TRY(ffm::launch_learn_adopt_slots(l->V.t, d_new_v, new_stride, owner_counts(new_counts, l->ow, 2), l->ow,
+                                          l->orank, s));
+    if (l->actor)
+        HIP_TRY(ffm::launch_learn_adopt_slots(l->H.t, d_new_h, new_stride, owner_counts(new_counts + 1, l->ow, 2),
+                                              l->ow, l->orank, s));
+    l->own_recs = reinterpret_cast<const ffm::TileRec*>(d_recs);
+    l->own_hdr = d_hdrs;
+    ffm::LearnArgs a = owner_args(l);
+    a.trecs = const_cast<ffm::TileRec*>(l->own_recs);
+    a.thdr = d_hdrs;
+    a.tR = l->ow;
+    a.vout_slot = l->d_vslot;
+    a.vout_val = l->d_vval;
+    a.vout_n = l->d_on;
+    HIP_TRY(ffm::launch_learn_tiles_owner_v(a, s));
+    l->phase = 8;
+    return FFM_OK;
+}
+
+int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const double* d_v_val,
+                             const int64_t* v_counts, int64_t v_stride, void* stream) {
+    if (!l || !v_counts) return fail(FFM_E_INVALID, "null argument");
+    if (l->phase != 8) return fail(FFM_E_INVALID, "step_owner_h must follow step_owner_v");
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(ffm::launch_learn_v_scatter(l->V.t, d_v_slot, d_v_val, v_stride, owner_counts(v_counts, l->ow), l->ow,
+                                        l->orank, s));
+    if (l->actor) {     // the actor's td reads the V every owner updated
+        ffm::LearnArgs a = owner_args(l);
+        a.trecs = const_cast<ffm::TileRec*>(l->own_recs);
+        a.thdr = l->own_hdr;
+        a.tR = l->ow;
+        a.hout_key = l->d_hkey;
+        a.hout_q = l->d_hq;
+        a.hout_n = l->d_on + 1;
+        HIP_TRY(ffm::launch_learn_tiles_owner_h(a, l->d_tsum, s));
+    }
+    l->phase = 9;
+    return FFM_OK;
+}
+
+int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q, const int64_t* h_counts,
+                               int64_t h_stride, const double* d_tsum_all, int64_t tsum_stride, void* stream) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->phase != 9) return fail(FFM_E_INVALID, "step_owner_end must follow step_owner_h");
+    hipStream_t s = (hipStream_t)stream;
+    ffm::LearnArgs a = owner_args(l);
+    if (l->actor) {
+        if (!h_counts || !d_tsum_all) return fail(FFM_E_INVALID, "null argument");
+        HIP_TRY(ffm::launch_learn_h_deltas(l->H.t, d_h_key, reinterpret_cast<const long long*>(d_h_q), h_stride,
+                                           owner_counts(h_counts, l->ow), l->ow, l->orank, s));
+        HIP_TRY(ffm::launch_learn_tsum_unpack(a, d_tsum_all, tsum_stride, s));
+        HIP_TRY(ffm::launch_learn_tile_stats(a, s));     // every rank: the same summaries, the same statistics
+    } else {
+        HIP_TRY(ffm::launch_learn_mark(a, s));
+    }
+    l->own_recs = nullptr;
+    l->own_hdr = nullptr;
+    int rc = phase_end(l, s);
+    if (!rc && l->h_overflow) HIP_TRY(hipMemcpyAsync(l->h_overflow, l->d_overflow, 4, hipMemcpyDeviceToHost, s));
+    return rc;
+}
+
 int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period) {
     if (!l || period < 0) return fail(FFM_E_INVALID, "epsilon phase period must be >= 0");
     l->eps_phase = period;
+    return FFM_OK;
+}
+
+int ffm_learner_set_epsilon_stride(ffm_learner* l, int64_t stride) {
+    if (!l || stride < 1) return fail(FFM_E_INVALID, "epsilon stride must be >= 1");
+    l->eps_stride = stride;
     return FFM_OK;
 }
 

@@ -104,6 +104,24 @@ struct LearnArgs {
     int* tcand;                 // [NT + 1] tiled step: tiles to rescan ([0] = count, then the tiles)
     int NT;                     // tiles: ceil(HW / kTileCells)
     int tile_ensure;            // tile kernels: insert the records' slots (records gathered from other ranks)
+    // Tile-major records: the tile passes read trecs through per-range
+    // headers instead of the env-major tstart.  Range r (a source rank; one range on one
+    // device) is a block of records holding the launch's tiles in order: tile k's records
+    // at [thdr[r * ths + k], thdr[r * ths + k + 1]) of the block, thdr[r * ths + NTk] = the
+    // block's size; the blocks lie back to back in trecs.  The launch processes NTk tiles:
+    // tile k is tile own_tile(k) (ow > 1: the tiles rank orank owns, chunks of ochunk tiles
+    // dealt round-robin over ow ranks; ow <= 1: k itself).
+    const uint32_t* thdr;       // nullptr: env-major (tstart)
+    int tR, ths, NTk;
+    int ow, orank, ochunk;
+    // owner mode outputs: the V values the launch's tiles updated (slot, new value) and the
+    // H increments (slot | action << 28, fixed-point sum), appended for the other ranks
+    uint32_t* vout_slot;
+    double* vout_val;
+    unsigned long long* vout_n;
+    uint32_t* hout_key;
+    long long* hout_q;
+    unsigned long long* hout_n;
     int* overflow;              // [1] table full / reset capacity exceeded
     uint32_t key0, key1, t;
     int auto_reset, max_steps;
@@ -113,7 +131,8 @@ struct LearnArgs {
     const uint16_t* free_cells;    // [F] placement candidates: x*W+y of the free cells, row-major
                                    // (np.argwhere(map == 0)), or a radius-limited subset of them
     double eps_start, eps_end, eps_offset, eps_span;   // batched epsilon schedule (eps_span > 0)
-    int eps_phase;              // > 0: global env g adds g % eps_phase to its episode count k
+    int eps_phase;              // > 0: global env g adds (g % eps_phase) * eps_stride to its episode count k
+    long long eps_stride;
     uint32_t mW, mBS;           // ceil(2^32 / d) for d = W, bs (0 when d = 1): n / d = mulhi(n, m)
     int* eplog;                 // [eplog_cap][4] ended episodes: global env, index, steps, emptied
     unsigned long long* eplog_n;
@@ -121,6 +140,26 @@ struct LearnArgs {
 };
 
 constexpr int kHstatBlocks = 2048;
+
+// Tile ownership across ranks: chunks of kOwnChunk consecutive tiles (one
+// 256-cell row at W = 256) dealt round-robin, so the crowded rows near an exit spread over
+// every rank.
+constexpr int kOwnChunk = 64;
+constexpr int kMaxOwners = 64;    // ranks of an owner-sharded exchange (one wave scans the ranges)
+
+// Tiles rank q owns among NT (ow ranks, chunks of C tiles).
+inline __host__ __device__ int owner_tiles(int NT, int ow, int C, int q) {
+    if (ow <= 1) return NT;
+    const int nch = NT / C, rem = NT % C;
+    int n = nch > q ? ((nch - 1 - q) / ow + 1) * C : 0;
+    if (rem && nch % ow == q) n += rem;
+    return n;
+}
+
+// Host-known per-rank element counts of an exchange (kernel argument).
+struct OwnerCounts {
+    long long n[kMaxOwners];
+};
 
 // Trajectory capture of the batched step (ffm_learner_set_trajectory_capture): the
 // selected envs' positions after every step of a captured episode, appended as rows.
@@ -145,6 +184,24 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
 bool learn_batch_raster(int HW, int A, int D);
 hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s);
+// tile-major records: the column scan, the tile offsets in destination order (per-destination
+// headers, hdr row stride ths, and record counts xcnt[ow]) and the scatter of trecs into out.
+// pe [E][NT], tpre [NT], toff [NT + 2 * ceil(NT / kOwnChunk)] words.
+hipError_t launch_learn_tile_pack(const LearnArgs& a, uint32_t* pe, uint32_t* tpre, uint32_t* toff, uint32_t* hdr,
+                                  long long* xcnt, TileRec* out, hipStream_t s);
+// owner mode: V table only (critic) or the H passes + statistics inputs, then the exchanges
+hipError_t launch_learn_tiles_owner_v(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStream_t s);
+hipError_t launch_learn_tile_stats(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_new_slots(const LearnTable& T, uint32_t* out, long long* count, hipStream_t s);
+hipError_t launch_learn_mark(const LearnArgs& a, hipStream_t s);
+hipError_t launch_learn_adopt_slots(const LearnTable& T, const uint32_t* slots, long long stride,
+                                    const OwnerCounts& c, int ranks, int self, hipStream_t s);
+hipError_t launch_learn_v_scatter(const LearnTable& T, const uint32_t* slots, const double* vals, long long stride,
+                                  const OwnerCounts& c, int ranks, int self, hipStream_t s);
+hipError_t launch_learn_h_deltas(const LearnTable& T, const uint32_t* keys, const long long* q, long long stride,
+                                 const OwnerCounts& c, int ranks, int self, hipStream_t s);
+hipError_t launch_learn_tsum_unpack(const LearnArgs& a, const double* tsum, long long stride, hipStream_t s);
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_capture(const LearnArgs& a, const TrajCapture& c, hipStream_t s);

@@ -1149,11 +1149,12 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
 
 // This env's epsilon: the learner's, or the batched schedule's after k ended
 // episodes (run_actor_only_training.py:190-196, run_unified_actor_training.py:253-259).
-// eps_phase spreads envs over the schedule: env g starts at its (g % eps_phase)-th episode,
-// so E >= P envs running one episode each cover a per-configuration schedule of P episodes.
+// eps_phase spreads envs over the schedule: env g starts at its ((g % eps_phase) * eps_stride)-th
+// episode, so E >= P envs running one episode each cover a per-configuration schedule of P
+// episodes, and envs running `stride` episodes each cover a run-wide schedule env-major.
 __device__ __forceinline__ double env_epsilon(const LearnArgs& a, int k, long long genv) {
     if (!(a.eps_span > 0)) return a.epsilon;
-    const double ph = a.eps_phase > 0 ? (double)(genv % a.eps_phase) : 0.0;
+    const double ph = a.eps_phase > 0 ? (double)((genv % a.eps_phase) * (a.eps_stride > 0 ? a.eps_stride : 1)) : 0.0;
     const double e = a.eps_start + (a.eps_end - a.eps_start) * (((double)k + a.eps_offset + ph) / a.eps_span);
     return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
 }
@@ -1862,6 +1863,182 @@ __device__ __forceinline__ int tile_of_block(int NT) {
     return (b & 7) * per + (b >> 3);
 }
 
+// Owner mode: launch tile k <-> tile t (LearnArgs ow / orank / ochunk).
+__device__ __forceinline__ int own_tile(const LearnArgs& a, int k) {
+    return a.ow <= 1 ? k : ((k / a.ochunk) * a.ow + a.orank) * a.ochunk + k % a.ochunk;
+}
+__device__ __forceinline__ int own_local(const LearnArgs& a, int t) {
+    return a.ow <= 1 ? t : ((t / a.ochunk) / a.ow) * a.ochunk + t % a.ochunk;
+}
+
+// A launch's tiles: block -> (launch tile k, tile t); k >= the launch's tiles: nothing to do.
+__device__ __forceinline__ void tile_of_launch(const LearnArgs& a, int& k, int& t) {
+    k = tile_of_block(a.thdr ? a.NTk : a.NT);
+    t = a.thdr ? own_tile(a, k) : k;
+}
+__device__ __forceinline__ int launch_tiles(const LearnArgs& a) { return a.thdr ? a.NTk : a.NT; }
+
+// Tile-major records: the ranges of launch tile k (wave 0, tR <= 64 lanes) -> rs[r] = records
+// of the ranges before r (rs[tR] = the tile's total), rb[r] = first record of range r (the
+// ranges' blocks lie back to back in trecs).
+// Ends with a barrier.
+__device__ __forceinline__ int tm_spans(const LearnArgs& a, int k, uint32_t* rs, uint32_t* rb) {
+    if (threadIdx.x < 64) {
+        const int r = (int)threadIdx.x;
+        // range r's block starts after the blocks of the ranges before it (each header ends
+        // with its block's record count)
+        uint32_t lo = 0, n = 0, blk = 0;
+        if (r < a.tR) {
+            const uint32_t* h = a.thdr + (size_t)r * a.ths;
+            lo = h[k];
+            n = h[k + 1] - lo;
+            blk = h[a.NTk];
+        }
+        uint32_t incl = n, bincl = blk;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o), w = (uint32_t)__shfl_up((int)bincl, o);
+            if (r >= o) {
+                incl += v;
+                bincl += w;
+            }
+        }
+        lo += bincl - blk;
+        if (r < a.tR) {
+            rs[r + 1] = incl;
+            rb[r] = lo;
+        }
+        if (r == 0) rs[0] = 0u;
+    }
+    __syncthreads();
+    return (int)rs[a.tR];
+}
+
+// Record index of the tile's j-th record (rs / rb of tm_spans).
+__device__ __forceinline__ uint32_t tm_index(const LearnArgs& a, const uint32_t* rs, const uint32_t* rb, uint32_t j) {
+    int lo = 0, hi = a.tR;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (rs[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    return rb[lo] + (j - rs[lo]);
+}
+
+// Block-aggregated append: every thread of the block calls it (uniformly) with P predicates;
+// idx[i] = the output index of item i (-1 where p[i] is false).  One global atomic per block:
+// a per-wave append on one counter would queue thousands of requests at one address.
+// lw: kTileWaves + 1 words of LDS.  Ends with a barrier (lw reusable).
+template <int P>
+__device__ __forceinline__ void block_append(unsigned long long* ctr, const bool (&p)[P], int (&idx)[P], int* lw) {
+    const int lane = (int)__lane_id(), w = (int)threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long m[P];
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < P; i++) {
+        m[i] = __ballot(p[i]);
+        cnt += __popcll(m[i]);
+    }
+    if (lane == 0) lw[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int v = 0; v < kTileWaves; v++) {
+            const int c = lw[v];
+            lw[v] = tot;
+            tot += c;
+        }
+        lw[kTileWaves] = tot ? (int)atomicAdd(ctr, (unsigned long long)tot) : 0;
+    }
+    __syncthreads();
+    int base = lw[kTileWaves] + lw[w];
+#pragma unroll
+    for (int i = 0; i < P; i++) {
+        idx[i] = p[i] ? base + (int)__popcll(m[i] & lt) : -1;
+        base += __popcll(m[i]);
+    }
+    __syncthreads();
+}
+
+// The updated V values of J slots (one per item; p: updated here).
+template <int J>
+__device__ __forceinline__ void vout_push(const LearnArgs& a, const bool (&p)[J], const uint32_t (&slot)[J],
+                                          const double (&v)[J], int* lw) {
+    if (!a.vout_n) return;
+    int idx[J];
+    block_append<J>(a.vout_n, p, idx, lw);
+#pragma unroll
+    for (int j = 0; j < J; j++)
+        if (idx[j] >= 0) {
+            a.vout_slot[idx[j]] = slot[j];
+            a.vout_val[idx[j]] = v[j];
+        }
+}
+
+// Block-aggregated append of variable-size runs: n[i] items for run i of this thread;
+// base[i] = the output index of the run's first item (runs of one thread's rows lie in
+// order, every run contiguous).  Called uniformly by the block; lw: kTileWaves + 1 words.
+template <int P>
+__device__ __forceinline__ void block_append_runs(unsigned long long* ctr, const int (&n)[P], int (&base)[P], int* lw) {
+    const int lane = (int)__lane_id(), w = (int)threadIdx.x >> 6;
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < P; i++) tot += n[i];
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) lw[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int v = 0; v < kTileWaves; v++) {
+            const int c = lw[v];
+            lw[v] = t;
+            t += c;
+        }
+        lw[kTileWaves] = t ? (int)atomicAdd(ctr, (unsigned long long)t) : 0;
+    }
+    __syncthreads();
+    int b = lw[kTileWaves] + lw[w] + incl - tot;
+#pragma unroll
+    for (int i = 0; i < P; i++) {
+        base[i] = b;
+        b += n[i];
+    }
+    __syncthreads();
+}
+
+// The nonzero H increments of J rows (p: a row applied here), each row's increments
+// adjacent in the output, so a receiver's updates of one row share its record's line.
+template <int J>
+__device__ __forceinline__ void hout_push(const LearnArgs& a, const bool (&p)[J], const uint32_t (&slot)[J],
+                                          const long long (&q)[J][5], int* lw) {
+    if (!a.hout_n) return;
+    int n[J], base[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        n[j] = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) n[j] += (p[j] && q[j][k] != 0) ? 1 : 0;
+    }
+    block_append_runs<J>(a.hout_n, n, base, lw);
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        int o = base[j];
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (p[j] && q[j][k] != 0) {
+                a.hout_key[o] = slot[j] | ((uint32_t)k << 28);
+                a.hout_q[o] = q[j][k];
+                o++;
+            }
+    }
+}
+
 constexpr int kTileEnvChunk = 2 * kTileThreads;   // envs whose ranges one pass gathers
 constexpr int kTileList = 4 * kTileThreads;       // record indices per window
 
@@ -1921,8 +2098,20 @@ __device__ __forceinline__ void tile_fill(const LearnArgs& a, long long e0, cons
 // Calls f(g) for every record g of tile t's cells, dealt evenly over the threads: one
 // dependent chain (range, record, table reads) per record instead of one per env in turn.
 template <typename F>
-__device__ __forceinline__ void tile_records(const LearnArgs& a, int t, uint32_t* list, int* wsum, F f) {
+__device__ __forceinline__ void tile_records(const LearnArgs& a, int t, int k, uint32_t* list, int* wsum,
+                                             uint32_t* rs, uint32_t* rb, F f) {
     const int tid = (int)threadIdx.x;
+    if (a.thdr) {       // tile-major: the tile's records are the ranges' runs
+        const int total = tm_spans(a, k, rs, rb);
+        for (int b = 0; b < total; b += kTileList) {
+            const int m = total - b < kTileList ? total - b : kTileList;
+            for (int i = tid; i < m; i += kTileThreads) list[i] = tm_index(a, rs, rb, (uint32_t)(b + i));
+            __syncthreads();
+            for (int i = tid; i < m; i += kTileThreads) f(list[i]);
+            __syncthreads();
+        }
+        return;
+    }
     for (long long e0 = 0; e0 < a.E; e0 += kTileEnvChunk) {
         const TileRanges r = tile_ranges(a, t, e0, wsum);
         for (int b = 0; b < r.total; b += kTileList) {
@@ -1945,7 +2134,15 @@ __device__ __forceinline__ void tile_records(const LearnArgs& a, int t, uint32_t
 // owed).
 constexpr int kTileJ = kTileList / kTileThreads;
 
-__device__ __forceinline__ int tile_window(const LearnArgs& a, int t, uint32_t* list, int* wsum) {
+__device__ __forceinline__ int tile_window(const LearnArgs& a, int t, int k, uint32_t* list, int* wsum, uint32_t* rs,
+                                           uint32_t* rb) {
+    if (a.thdr) {       // tile-major: any number of envs, only the tile's record count matters
+        const int total = tm_spans(a, k, rs, rb);
+        if (total > kTileList) return -1;
+        for (int j = (int)threadIdx.x; j < total; j += kTileThreads) list[j] = tm_index(a, rs, rb, (uint32_t)j);
+        __syncthreads();
+        return total;
+    }
     if (a.E > kTileEnvChunk) return -1;
     const TileRanges r = tile_ranges(a, t, 0, wsum);
     if (r.total > kTileList) {
@@ -1955,6 +2152,18 @@ __device__ __forceinline__ int tile_window(const LearnArgs& a, int t, uint32_t* 
     tile_fill(a, 0, r, 0, list);
     __syncthreads();
     return r.total;
+}
+
+// Tile-major, a tile beyond one window: window b's records, kTileJ per thread, every load in
+// flight before the first is used (rs / rb of tm_spans).  Returns the window's record count.
+__device__ __forceinline__ int tm_load(const LearnArgs& a, const uint32_t* rs, const uint32_t* rb, int total, int b,
+                                       TileRec (&rc)[kTileJ]) {
+    const int tid = (int)threadIdx.x;
+    const int m = total - b < kTileList ? total - b : kTileList;
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++)
+        if (tid + j * kTileThreads < m) rc[j] = a.trecs[tm_index(a, rs, rb, (uint32_t)(b + tid + j * kTileThreads))];
+    return m;
 }
 
 // The rank key of a dense slot (inverse of dense_slot): ranks in bits 0-7, bx, by.
@@ -1970,10 +2179,13 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     __shared__ long long qs[NS];
     __shared__ uint32_t ks[NS];
     __shared__ uint32_t list[kTileList];
-    __shared__ int wsum[kTileWaves];
-    const int t = tile_of_block(a.NT), tid = (int)threadIdx.x;
+    __shared__ int wsum[kTileWaves + 1];
+    __shared__ uint32_t rs[kMaxOwners + 1], rb[kMaxOwners];
+    const int tid = (int)threadIdx.x;
+    int k, t;
+    tile_of_launch(a, k, t);
     if (blockIdx.x == 0 && tid == 0) a.tcand[0] = 0;    // the H pass's queue of wide tiles
-    if (t >= a.NT) return;
+    if (k >= launch_tiles(a)) return;
     for (int i = tid; i < NS; i += kTileThreads) { qs[i] = 0; ks[i] = 0u; }
     __syncthreads();
     const uint32_t Q = (a.V.mask + 1u) >> 8;
@@ -1986,7 +2198,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
             if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
         }
     };
-    const int m = tile_window(a, t, list, wsum);
+    const int m = tile_window(a, t, k, list, wsum, rs, rb);
     if (m >= 0) {
         TileRec rc[kTileJ];
 #pragma unroll
@@ -2006,21 +2218,44 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
             add(rc[j], sv, ix[j]);
         }
         __syncthreads();
+        double nv[kTileJ];
+        uint32_t sl[kTileJ];
 #pragma unroll
         for (int j = 0; j < kTileJ; j++) {
-            if (!own[j]) continue;
-            double* vp = tval(a.V, rc[j].svk & 0x0FFFFFFFu);
-            vp[0] = v_visits(vv[j], qs[ix[j]], (long long)ks[ix[j]], a.V.alpha);
+            nv[j] = 0.0;
+            sl[j] = rc[j].svk & 0x0FFFFFFFu;
+            if (own[j]) {
+                nv[j] = v_visits(vv[j], qs[ix[j]], (long long)ks[ix[j]], a.V.alpha);
+                tval(a.V, sl[j])[0] = nv[j];
+            }
         }
+        vout_push<kTileJ>(a, own, sl, nv, wsum);
         return;
     }
-    tile_records(a, t, list, wsum, [&](uint32_t g) {
-        const TileRec rc = a.trecs[g];
-        const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-        const int idx = tile_idx(sv, qsh, Q, c0);
-        atomicAdd(&ks[idx], 1u);
-        add(rc, sv, idx);
-    });
+    if (a.thdr) {       // tile-major (tile_window left the spans in rs / rb)
+        const int total = (int)rs[a.tR];
+        for (int b = 0; b < total; b += kTileList) {
+            TileRec rc[kTileJ];
+            const int mw = tm_load(a, rs, rb, total, b, rc);
+#pragma unroll
+            for (int j = 0; j < kTileJ; j++) {
+                if (tid + j * kTileThreads >= mw) continue;
+                const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+                const int idx = tile_idx(sv, qsh, Q, c0);
+                atomicAdd(&ks[idx], 1u);
+                add(rc[j], sv, idx);
+            }
+        }
+        __syncthreads();
+    } else {
+        tile_records(a, t, k, list, wsum, rs, rb, [&](uint32_t g) {
+            const TileRec rc = a.trecs[g];
+            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+            const int idx = tile_idx(sv, qsh, Q, c0);
+            atomicAdd(&ks[idx], 1u);
+            add(rc, sv, idx);
+        });
+    }
     constexpr int kPer = NS / kTileThreads;
     double vv[kPer];
 #pragma unroll
@@ -2028,14 +2263,22 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
         const int i = tid + j * kTileThreads;
         if (ks[i]) vv[j] = tval(a.V, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells))[0];
     }
+    bool up[kPer];
+    uint32_t sl[kPer];
+    double nv[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; j++) {
         const int i = tid + j * kTileThreads;
-        const uint32_t k = ks[i];
-        if (!k) continue;
-        double* vp = tval(a.V, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
-        vp[0] = v_visits(vv[j], qs[i], (long long)k, a.V.alpha);
+        const uint32_t kv = ks[i];
+        sl[j] = (uint32_t)((size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+        up[j] = kv != 0u;
+        nv[j] = 0.0;
+        if (kv) {
+            nv[j] = v_visits(vv[j], qs[i], (long long)kv, a.V.alpha);
+            tval(a.V, sl[j])[0] = nv[j];
+        }
     }
+    vout_push<kPer>(a, up, sl, nv, wsum);
 }
 
 // Exact min / max / non-finite of one tile's present H rows (a block-wide scan).
@@ -2209,10 +2452,13 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
     __shared__ uint32_t list[kTileList];
-    __shared__ int wsum[kTileWaves];
+    __shared__ int wsum[kTileWaves + 1];
+    __shared__ uint32_t rs[kMaxOwners + 1], rb[kMaxOwners];
     __shared__ int npair;
-    const int t = tile_of_block(a.NT), tid = (int)threadIdx.x, lane = tid & 63;
-    if (t >= a.NT) return;
+    const int tid = (int)threadIdx.x, lane = tid & 63;
+    int k, t;
+    tile_of_launch(a, k, t);
+    if (k >= launch_tiles(a)) return;
     const uint32_t Q = (a.Ht.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
     for (int i = tid; i < kTileList; i += kTileThreads) hq[i] = 0;
@@ -2220,7 +2466,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     if (tid < NS / 32) touched[tid] = 0u;
     if (tid == 0) npair = 0;
     // (tile_window's barriers order these stores before any use)
-    const int m = tile_window(a, t, list, wsum);
+    const int m = tile_window(a, t, k, list, wsum, rs, rb);
     if (m < 0) {
         if (tid == 0) a.tcand[1 + atomicAdd(&a.tcand[0], 1)] = t;
         return;
@@ -2245,9 +2491,9 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
         own[j] = !(atomicOr(&touched[ix[j] >> 5], bit) & bit);
         tile_h_vpair(a, rc[j], sv, vn[j], vs[j]);
         if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
-        const int k = (int)(rc[j].svk >> 28);
-        if (k != (int)kTileNoAct) {
-            pr[j] = ix[j] * 5 + k;
+        const int act = (int)(rc[j].svk >> 28);
+        if (act != (int)kTileNoAct) {
+            pr[j] = ix[j] * 5 + act;
             const uint32_t pb = 1u << (pr[j] & 31);
             pown[j] = !(atomicOr(&pbit[pr[j] >> 5], pb) & pb);
         }
@@ -2277,17 +2523,19 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
 #pragma unroll
         for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
     }
+    long long q[kTileJ][5];
+    uint32_t sl[kTileJ];
 #pragma unroll
     for (int j = 0; j < kTileJ; j++) {
-        if (!own[j]) continue;
-        long long q[5];
+        sl[j] = rc[j].svk & 0x0FFFFFFFu;
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const int p = ix[j] * 5 + k;
-            q[k] = ((pbit[p >> 5] >> (p & 31)) & 1u) ? hq[pid[p]] : 0;
+        for (int kk = 0; kk < 5; kk++) {
+            const int p = ix[j] * 5 + kk;
+            q[j][kk] = own[j] && ((pbit[p >> 5] >> (p & 31)) & 1u) ? hq[pid[p]] : 0;
         }
-        tile_h_apply(tval(a.Ht, rc[j].svk & 0x0FFFFFFFu), q, hv[j], c);
+        if (own[j]) tile_h_apply(tval(a.Ht, sl[j]), q[j], hv[j], c);
     }
+    hout_push<kTileJ>(a, own, sl, q, wsum);
     tile_h_end(a, t, c, smn, smx, sfl);
 }
 
@@ -2301,30 +2549,54 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
     __shared__ uint32_t list[kTileList];
-    __shared__ int wsum[kTileWaves];
+    __shared__ int wsum[kTileWaves + 1];
+    __shared__ uint32_t rs[kMaxOwners + 1], rb[kMaxOwners];
     const int tid = (int)threadIdx.x;
     const uint32_t Q = (a.Ht.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q);
     const int n = a.tcand[0];
     for (int ci = (int)blockIdx.x; ci < n; ci += (int)gridDim.x) {
-        const int t = a.tcand[1 + ci], c0 = t * kTileCells;
+        const int t = a.tcand[1 + ci], c0 = t * kTileCells, kt = a.thdr ? own_local(a, t) : t;
         for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
         for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
         __syncthreads();
         TileHCtx c = tile_h_begin(a, t);
-        tile_records(a, t, list, wsum, [&](uint32_t g) {
-            const TileRec rc = a.trecs[g];
-            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
-            const int idx = tile_idx(sv, qsh, Q, c0);
-            atomicOr(&touched[idx >> 5], 1u << (idx & 31));
-            if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
-            const int k = (int)(rc.svk >> 28);
-            if (k == (int)kTileNoAct) return;
-            double vn, vs;
-            tile_h_vpair(a, rc, sv, vn, vs);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + k]),
-                      (unsigned long long)tile_h_q(a, rc, vn, vs));
-        });
+        if (a.thdr) {       // tile-major: windows of kTileJ records per thread, the loads first
+            const int total = tm_spans(a, kt, rs, rb);
+            for (int b = 0; b < total; b += kTileList) {
+                TileRec rc[kTileJ];
+                const int mw = tm_load(a, rs, rb, total, b, rc);
+                double vn[kTileJ], vs[kTileJ];
+#pragma unroll
+                for (int j = 0; j < kTileJ; j++)
+                    if (tid + j * kTileThreads < mw) tile_h_vpair(a, rc[j], rc[j].svk & 0x0FFFFFFFu, vn[j], vs[j]);
+#pragma unroll
+                for (int j = 0; j < kTileJ; j++) {
+                    if (tid + j * kTileThreads >= mw) continue;
+                    const int idx = tile_idx(rc[j].svk & 0x0FFFFFFFu, qsh, Q, c0);
+                    atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+                    const int act = (int)(rc[j].svk >> 28);
+                    if (act == (int)kTileNoAct) continue;
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + act]),
+                              (unsigned long long)tile_h_q(a, rc[j], vn[j], vs[j]));
+                }
+            }
+            __syncthreads();
+        } else {
+            tile_records(a, t, kt, list, wsum, rs, rb, [&](uint32_t g) {
+                const TileRec rc = a.trecs[g];
+                const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+                const int idx = tile_idx(sv, qsh, Q, c0);
+                atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+                if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
+                const int act = (int)(rc.svk >> 28);
+                if (act == (int)kTileNoAct) return;
+                double vn, vs;
+                tile_h_vpair(a, rc, sv, vn, vs);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + act]),
+                          (unsigned long long)tile_h_q(a, rc, vn, vs));
+            });
+        }
         // every touched row's loads are issued before the first is used (one latency, not four)
         constexpr int kPer = NS / kTileThreads;
         double hv[kPer][5];
@@ -2339,15 +2611,17 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
                 for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
             }
         }
+        long long q[kPer][5];
+        uint32_t sl[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const int i = tid + j * kTileThreads;
-            if (!tch[j]) continue;
-            long long q[5];
+            sl[j] = (uint32_t)((size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
 #pragma unroll
-            for (int k = 0; k < 5; k++) q[k] = hq[i * 5 + k];
-            tile_h_apply(tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells)), q, hv[j], c);
+            for (int kk = 0; kk < 5; kk++) q[j][kk] = tch[j] ? hq[i * 5 + kk] : 0;
+            if (tch[j]) tile_h_apply(tval(a.Ht, sl[j]), q[j], hv[j], c);
         }
+        hout_push<kPer>(a, tch, sl, q, wsum);
         tile_h_end(a, t, c, smn, smx, sfl);
     }
 }
@@ -2484,6 +2758,239 @@ __global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
         *a.Ht.mark = *a.Ht.n;
         *a.V.mark = *a.V.n;
     }
+}
+
+// ===========================================================================
+// Tile-major records.  The batch kernel leaves each env's records in
+// raster order with per-env tile offsets (tstart); the pack reorders them tile-major, every
+// tile's records of all envs contiguous, grouped by the rank that owns the tile: one
+// column scan over the envs, one scan over the tiles, one scatter.  The tile passes then
+// read a tile's records as at most one run per source rank -- no per-env ranges, and the
+// one-window fast form holds for any number of envs -- and the groups are the
+// all-to-all's per-destination blocks.
+// ===========================================================================
+constexpr int kColTiles = kOwnChunk, kColSplit = 4;   // a colscan block covers one ownership chunk
+
+// pe[e][t] = records of tile t in envs < e, minus tstart[e][t] (mod 2^32: a record's raster
+// rank plus it is the record's rank among the tile's records); tpre[t] = records of the tiles before t in its
+// chunk of kOwnChunk tiles; csum[c] = records of chunk c.  A block owns one chunk (lanes =
+// tiles) and splits the envs in four (waves).
+__global__ __launch_bounds__(kColTiles * kColSplit) void learn_tile_colscan_kernel(LearnArgs a, uint32_t* pe,
+                                                                                  uint32_t* tpre, uint32_t* csum) {
+    __shared__ uint32_t part[kColSplit][kColTiles];
+    const int lane = (int)threadIdx.x & 63, q = (int)threadIdx.x >> 6;
+    const int t = (int)blockIdx.x * kColTiles + lane;
+    const long long per = (a.E + kColSplit - 1) / kColSplit;
+    const long long e0 = q * per, e1 = e0 + per < a.E ? e0 + per : a.E;
+    const bool ok = t < a.NT;
+    const long long S = a.NT + 1;
+    const uint16_t* ts = a.tstart + t;
+    uint32_t sum = 0;
+    if (ok) {
+#pragma unroll 8
+        for (long long e = e0; e < e1; e++) sum += (uint32_t)(ts[e * S + 1] - ts[e * S]);
+    }
+    part[q][lane] = sum;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kColSplit; w++) {
+        base += w < q ? part[w][lane] : 0u;
+        tot += part[w][lane];
+    }
+    if (q == 0) {     // the chunk's tiles: exclusive prefix over the lanes, and the chunk's sum
+        uint32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (ok) tpre[t] = incl - tot;
+        if (lane == 63) csum[blockIdx.x] = incl;
+    }
+    if (!ok) return;
+#pragma unroll 8
+    for (long long e = e0; e < e1; e++) {
+        const uint32_t lo = ts[e * S];
+        pe[e * a.NT + t] = base - lo;       // mod 2^32: + the record's raster rank = its place in the tile
+        base += (uint32_t)(ts[e * S + 1] - lo);
+    }
+}
+
+// The chunks in destination order (rank q owns chunks q, q + ow, ...; q = 0 .. ow - 1): toff[t]
+// = first record of tile t in the packed buffer, hdr[q][k] = the same relative to q's block
+// (hdr[q][NTq] = q's record count), xcnt[q] = q's record count.  One 1024-thread block over
+// the chunks (256 at 256x256), then every tile.
+constexpr int kOffThreads = 1024;
+
+__global__ __launch_bounds__(kOffThreads) void learn_tile_offsets_kernel(LearnArgs a, const uint32_t* tpre,
+                                                                        const uint32_t* csum, uint32_t* coff,
+                                                                        uint32_t* toff, uint32_t* hdr,
+                                                                        long long* xcnt) {
+    __shared__ uint32_t wsum[kOffThreads / 64];
+    __shared__ uint32_t seg[kMaxOwners + 1];
+    const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int C = kOwnChunk, ow = a.ow <= 1 ? 1 : a.ow;
+    const int nch = (a.NT + C - 1) / C;
+    const int per = (nch + kOffThreads - 1) / kOffThreads;
+    // destination position p -> chunk: rank q's chunks (nq of them) after the ranks before q
+    auto chunk_at = [&](int p, int& q) {
+        int base = 0;
+        for (q = 0; q < ow; q++) {
+            const int nq = nch > q ? (nch - 1 - q) / ow + 1 : 0;
+            if (p < base + nq) return (p - base) * ow + q;
+            base += nq;
+        }
+        return -1;
+    };
+    const int p0 = tid * per, p1 = p0 + per < nch ? p0 + per : nch;
+    uint32_t sum = 0;
+    for (int p = p0; p < p1; p++) {
+        int q;
+        sum += csum[chunk_at(p, q)];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    if (tid <= ow) seg[tid] = 0xFFFFFFFFu;
+    __syncthreads();
+    uint32_t off = incl - sum, total = 0;
+    for (int v = 0; v < kOffThreads / 64; v++) {
+        off += v < w ? wsum[v] : 0u;
+        total += wsum[v];
+    }
+    for (int p = p0; p < p1; p++) {
+        int q;
+        const int c = chunk_at(p, q);
+        coff[c] = off;
+        if (c == q) seg[q] = off;          // q's first chunk starts its block
+        off += csum[c];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        seg[ow] = total;
+        for (int q = ow - 1; q >= 0; q--)        // ranks without chunks: an empty block
+            if (seg[q] == 0xFFFFFFFFu) seg[q] = seg[q + 1];
+    }
+    __syncthreads();
+    for (int t = tid; t < a.NT; t += kOffThreads) {
+        const int c = t / C, q = c % ow, k = (c / ow) * C + t % C;
+        const uint32_t o = coff[c] + tpre[t];
+        toff[t] = o;
+        hdr[(size_t)q * a.ths + k] = o - seg[q];
+    }
+    if (tid < ow) {
+        const int n = owner_tiles(a.NT, ow, C, tid);
+        hdr[(size_t)tid * a.ths + n] = seg[tid + 1] - seg[tid];
+        xcnt[tid] = (long long)(seg[tid + 1] - seg[tid]);
+    }
+}
+
+// Every record to its packed place: tile t of record i of env e is its cell's (the slot of s
+// is p * Q + cell); its place is toff[t] + pe[e][t] + i.
+// Four records per thread, every load issued before the first store.
+constexpr int kScatterJ = 4;
+
+__global__ __launch_bounds__(256) void learn_tile_scatter_kernel(LearnArgs a, const uint32_t* pe,
+                                                                 const uint32_t* toff, TileRec* out) {
+    const long long e = blockIdx.x;
+    const long long S = a.NT + 1;
+    const int n = a.tstart[e * S + a.NT];
+    const int i0 = (int)blockIdx.y * 256 * kScatterJ + (int)threadIdx.x;
+    if (i0 >= n) return;
+    const uint32_t Q = (a.V.mask + 1u) >> 8;
+    TileRec rc[kScatterJ];
+    int t[kScatterJ];
+#pragma unroll
+    for (int j = 0; j < kScatterJ; j++)
+        if (i0 + j * 256 < n) rc[j] = a.trecs[e * a.A + i0 + j * 256];
+#pragma unroll
+    for (int j = 0; j < kScatterJ; j++) t[j] = (int)(((rc[j].svk & 0x0FFFFFFFu) & (Q - 1u)) / kTileCells);
+    uint32_t d[kScatterJ];
+#pragma unroll
+    for (int j = 0; j < kScatterJ; j++)
+        if (i0 + j * 256 < n) d[j] = toff[t[j]] + pe[e * a.NT + t[j]] + (uint32_t)(i0 + j * 256);
+#pragma unroll
+    for (int j = 0; j < kScatterJ; j++)
+        if (i0 + j * 256 < n) out[d[j]] = rc[j];
+}
+
+// Slots this rank's step inserted (order[mark .. n)): the other ranks adopt them.
+__global__ __launch_bounds__(256) void learn_new_slots_kernel(LearnTable T, uint32_t* out, long long* count) {
+    const uint32_t m0 = *T.mark, m1 = *T.n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = (long long)(m1 - m0);
+    for (uint32_t i = m0 + blockIdx.x * 256 + threadIdx.x; i < m1; i += gridDim.x * 256) out[i - m0] = T.order[i];
+}
+
+__global__ void learn_mark_kernel(LearnArgs a) {
+    *a.V.mark = *a.V.n;
+    if (a.Ht.n) *a.Ht.mark = *a.Ht.n;
+}
+
+// The other ranks' new slots, inserted here (dense_ensure: presence bit, key, order).
+__global__ __launch_bounds__(256) void learn_adopt_slots_kernel(LearnTable T, const uint32_t* slots,
+                                                                long long stride, OwnerCounts c, int ranks,
+                                                                int self) {
+    const uint32_t Q = (T.mask + 1u) >> 8;
+    const int qsh = __builtin_ctz(Q);
+    for (int r = 0; r < ranks; r++) {
+        if (r == self) continue;
+        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < c.n[r]; i += (long long)gridDim.x * 256) {
+            const uint32_t h = slots[r * stride + i];
+            dense_ensure(T, h, dense_key(h, qsh, Q, T.dense_by));
+        }
+    }
+}
+
+// The other owners' updated V values.
+__global__ __launch_bounds__(256) void learn_v_scatter_kernel(LearnTable T, const uint32_t* slots,
+                                                              const double* vals, long long stride, OwnerCounts c,
+                                                              int ranks, int self) {
+    for (int r = 0; r < ranks; r++) {
+        if (r == self) continue;
+        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < c.n[r]; i += (long long)gridDim.x * 256)
+            tval(T, slots[r * stride + i])[0] = vals[r * stride + i];
+    }
+}
+
+// The other owners' H increments: v + q * 2^-32, the owner's tile_h_apply arithmetic.
+__global__ __launch_bounds__(256) void learn_h_deltas_kernel(LearnTable T, const uint32_t* keys, const long long* q,
+                                                             long long stride, OwnerCounts c, int ranks, int self) {
+    for (int r = 0; r < ranks; r++) {
+        if (r == self) continue;
+        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < c.n[r]; i += (long long)gridDim.x * 256) {
+            const uint32_t key = keys[r * stride + i];
+            double* vp = tval(T, key & 0x0FFFFFFFu) + (key >> 28);
+            *vp = *vp + (double)q[r * stride + i] * (1.0 / kFxOne);
+        }
+    }
+}
+
+// Owned tiles' H summaries (present, non-finite, min, max, stale bits) for the other ranks.
+__global__ __launch_bounds__(256) void learn_tsum_pack_kernel(LearnArgs a, double* tsum) {
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k >= a.NTk) return;
+    const int t = own_tile(a, k);
+#pragma unroll
+    for (int i = 0; i < 4; i++) tsum[(size_t)k * 5 + i] = a.tstats[4 * (size_t)t + i];
+    tsum[(size_t)k * 5 + 4] = (double)a.tdirty[t];
+}
+
+// ... and the other ranks' summaries of their tiles, here (tsum: [ow][stride][5]).
+__global__ __launch_bounds__(256) void learn_tsum_unpack_kernel(LearnArgs a, const double* tsum, long long stride) {
+    const int t = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (t >= a.NT) return;
+    const int q = (t / a.ochunk) % a.ow;
+    if (q == a.orank) return;
+    const int k = ((t / a.ochunk) / a.ow) * a.ochunk + t % a.ochunk;
+    const double* src = tsum + ((size_t)q * stride + k) * 5;
+#pragma unroll
+    for (int i = 0; i < 4; i++) a.tstats[4 * (size_t)t + i] = src[i];
+    a.tdirty[t] = (int)src[4];
 }
 
 __global__ __launch_bounds__(256) void learn_fill_default_kernel(LearnTable T, double v) {
@@ -3001,6 +3508,93 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_tile_pack(const LearnArgs& a, uint32_t* pe, uint32_t* tpre, uint32_t* toff, uint32_t* hdr,
+                                  long long* xcnt, TileRec* out, hipStream_t s) {
+    if (a.ow > kMaxOwners) return hipErrorInvalidValue;
+    // chunk sums and offsets live in toff's tail (NT + 2 * chunks words)
+    const int nch = (a.NT + kOwnChunk - 1) / kOwnChunk;
+    uint32_t* csum = toff + a.NT;
+    uint32_t* coff = csum + nch;
+    learn_tile_colscan_kernel<<<dim3((unsigned)nch), dim3(kColTiles * kColSplit), 0, s>>>(a, pe, tpre, csum);
+    learn_tile_offsets_kernel<<<dim3(1), dim3(kOffThreads), 0, s>>>(a, tpre, csum, coff, toff, hdr, xcnt);
+    learn_tile_scatter_kernel<<<dim3((unsigned)a.E, (unsigned)((a.A + 256 * kScatterJ - 1) / (256 * kScatterJ))),
+                                dim3(256), 0, s>>>(a, pe, toff, out);
+    return hipGetLastError();
+}
+
+// Owner mode: the V pass over the owned tiles (V values out), then the H passes (H
+// increments and the owned tiles' summaries out).  The statistics (candidates, rescans,
+// final) run on every rank once the summaries are exchanged (launch_learn_tile_stats).
+hipError_t launch_learn_tiles_owner_v(const LearnArgs& a, hipStream_t s) {
+    const unsigned tgrid = 8u * (unsigned)((a.NTk + 7) / 8);
+    if (a.vout_n) (void)hipMemsetAsync(a.vout_n, 0, 8, s);
+    if (a.NTk > 0) learn_tile_v_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStream_t s) {
+    const unsigned tgrid = 8u * (unsigned)((a.NTk + 7) / 8);
+    const unsigned nresc = (unsigned)(a.NTk < 2048 ? (a.NTk > 0 ? a.NTk : 1) : 2048);
+    if (a.hout_n) (void)hipMemsetAsync(a.hout_n, 0, 8, s);
+    if (a.NTk > 0) {
+        learn_tile_h_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+        learn_tile_h_wide_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        learn_tsum_pack_kernel<<<dim3((unsigned)((a.NTk + 255) / 256)), dim3(256), 0, s>>>(a, tsum);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_tile_stats(const LearnArgs& a, hipStream_t s) {
+    const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
+    learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
+    learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_new_slots(const LearnTable& T, uint32_t* out, long long* count, hipStream_t s) {
+    learn_new_slots_kernel<<<dim3(1024), dim3(256), 0, s>>>(T, out, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_mark(const LearnArgs& a, hipStream_t s) {
+    learn_mark_kernel<<<dim3(1), dim3(1), 0, s>>>(a);
+    return hipGetLastError();
+}
+
+static unsigned owner_grid(const OwnerCounts& c, int ranks, int self) {
+    long long mx = 0;
+    for (int r = 0; r < ranks; r++)
+        if (r != self && c.n[r] > mx) mx = c.n[r];
+    return (unsigned)std::min<long long>(32768, (mx + 255) / 256);
+}
+
+hipError_t launch_learn_adopt_slots(const LearnTable& T, const uint32_t* slots, long long stride,
+                                    const OwnerCounts& c, int ranks, int self, hipStream_t s) {
+    const unsigned g = owner_grid(c, ranks, self);
+    if (g) learn_adopt_slots_kernel<<<dim3(g), dim3(256), 0, s>>>(T, slots, stride, c, ranks, self);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_v_scatter(const LearnTable& T, const uint32_t* slots, const double* vals, long long stride,
+                                  const OwnerCounts& c, int ranks, int self, hipStream_t s) {
+    const unsigned g = owner_grid(c, ranks, self);
+    if (g) learn_v_scatter_kernel<<<dim3(g), dim3(256), 0, s>>>(T, slots, vals, stride, c, ranks, self);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_h_deltas(const LearnTable& T, const uint32_t* keys, const long long* q, long long stride,
+                                 const OwnerCounts& c, int ranks, int self, hipStream_t s) {
+    const unsigned g = owner_grid(c, ranks, self);
+    if (g) learn_h_deltas_kernel<<<dim3(g), dim3(256), 0, s>>>(T, keys, q, stride, c, ranks, self);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_tsum_unpack(const LearnArgs& a, const double* tsum, long long stride, hipStream_t s) {
+    learn_tsum_unpack_kernel<<<dim3((unsigned)((a.NT + 255) / 256)), dim3(256), 0, s>>>(a, tsum, stride);
     return hipGetLastError();
 }
 

@@ -8,6 +8,7 @@ the end-of-run reduction of counters (sum) and elapsed time (max).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -81,10 +82,11 @@ class TableSync:
       sizes it from the touched counts actually measured: every rank copies the
       all-gathered counts (identical on every rank) to pinned host memory behind the
       exchange, and every ``adapt_every`` exchanges the capacity becomes
-      ``headroom`` x the largest count of the last window (a power of two in
-      [1,024, ``max_capacity``]).  The window lags ``lag`` exchanges behind the
-      host, whose copies it waits for (a bounded queue depth, not a sync), so
-      every rank decides on the same numbers at the same exchange.
+      ``headroom`` x the largest count observed so far (4 K-record granularity, in
+      [1,024, ``max_capacity``]; it never shrinks below what any step needed).  The
+      window lags ``lag`` exchanges behind the host, whose copies it waits for (a
+      bounded queue depth, not a sync), so every rank decides on the same numbers at
+      the same exchange.
 
     * ``dense`` (default: the shard's tables are dense, i.e. ffm_unified): the whole
       fixed-point accumulator array is all-reduced (SUM; RCCL runs it as
@@ -103,8 +105,8 @@ class TableSync:
     """
 
     def __init__(self, shard, group=None, device=None, capacity: int | None = 1 << 16, sync_period: int = 1,
-                 dense: bool | None = None, max_capacity: int = 1 << 20, headroom: float = 2.0,
-                 adapt_every: int = 16, lag: int = 8):
+                 dense: bool | None = None, max_capacity: int = 1 << 20, headroom: float = 1.5,
+                 adapt_every: int = 16, lag: int = 8, tiled_exchange: str = "owner"):
         self.shard = shard
         self.group = group
         self.device = device
@@ -130,10 +132,18 @@ class TableSync:
         # the same collective, whatever its own flag, so a disagreement falls back instead
         # of leaving some ranks inside a collective the others never enter.
         local_tiled = bool(getattr(shard, "tiled", False)) and self.sync_period == 1 and dense is None
+        local_owner = local_tiled and bool(getattr(shard, "tile_major", False))
         n_envs = int(getattr(shard, "n_envs", getattr(shard, "E", 0)))
-        v = torch.tensor([int(local_tiled), n_envs, -n_envs], dtype=torch.int64, device=device)
+        v = torch.tensor([int(local_tiled), int(local_owner), n_envs, -n_envs], dtype=torch.int64, device=device)
         dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
-        self.tiled = bool(v[0].item()) and int(v[1].item()) == -int(v[2].item())
+        # owner: the tiles are dealt to the ranks, each sums its own tiles' records from all
+        # ranks; replicated: every rank sums every rank's records (9.7)
+        self.owner = bool(v[1].item()) and tiled_exchange == "owner"
+        self.tiled = self.owner or (bool(v[0].item()) and int(v[2].item()) == -int(v[3].item()))
+        if self.owner:
+            shard.set_tile_owners(self.world, self.rank)
+        self.backend = dist.get_backend(group)
+        self.received_bytes = 0        # per rank, summed over exchanges (owner mode)
         self.bufs = {}
         self.bytes_sent = 0          # per rank, summed over exchanges (what this rank contributes)
         self.exchanges = 0
@@ -191,9 +201,8 @@ class TableSync:
         # fall near episode ends and jump back after lockstep resets, faster than the
         # window-old estimate could grow again
         self.max_count[which] = max(self.max_count[which], m)
-        cap = 1024
-        while cap < self.headroom * self.max_count[which] and cap < self.max_capacity:
-            cap *= 2
+        need = int(self.headroom * self.max_count[which])
+        cap = min(max(1024, -(-need // 4096) * 4096), self.max_capacity)   # 4 K-record granularity
         self.caps[which] = cap
         self.capacity = max(self.caps.values())
 
@@ -215,6 +224,83 @@ class TableSync:
     def _exchange(self, which: str):
         self.exchanges += 1
         (self._exchange_dense if self.dense else self._exchange_records)(which)
+
+    # -- the owner-sharded tiled step ----------------------------------
+    def _host(self, t):
+        """A small device tensor on the host (the step's size decisions: a host sync)."""
+        return t.cpu().numpy()
+
+    def _gather_rows(self, x, n_bytes: int, key):
+        """all-gather the first n_bytes of every rank's byte buffer x: [world, n_bytes]
+        (a rank whose buffer is shorter sends a zero-padded copy)."""
+        n = max(int(n_bytes), 1)
+        src = x[:n] if x.numel() >= n else torch.nn.functional.pad(x, (0, n - x.numel()))
+        out = self._buf(key, (self.world, n), x.device)
+        dist.all_gather([out[r] for r in range(self.world)], src.contiguous(), group=self.group)
+        self.received_bytes += (self.world - 1) * n
+        self.bytes_sent += n
+        return out
+
+    def _buf(self, key, shape, device):
+        shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        b = self.bufs.get(key)
+        if b is None or b.numel() < int(np.prod(shape)):
+            b = torch.empty(int(np.prod(shape)), dtype=torch.uint8, device=device)
+            self.bufs[key] = b
+        return b[: int(np.prod(shape))].view(shape)
+
+    def _a2av(self, out, inp, out_splits, in_splits):
+        """all-to-all with uneven byte splits (gloo: staged through host memory)."""
+        if self.backend == "gloo" and inp.is_cuda:
+            ho = torch.empty(out.numel(), dtype=torch.uint8)
+            dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(ho)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def _step_owner(self):
+        s, W, r = self.shard, self.world, self.rank
+        s.step_owner_local()
+        b = s.owner_buffers()
+        dev = b["counts"].device
+        hs = b["hdr_stride"]
+        # 1. the record counts (per destination) and new-slot counts of every rank
+        g = self._buf("counts", (W, 8 * (W + 2)), dev)
+        dist.all_gather([g[q] for q in range(W)], b["counts"].view(torch.uint8), group=self.group)
+        allc = self._host(g).view(np.int64).reshape(W, W + 2)
+        send, recv = allc[r, :W], allc[:, r]
+        rrecs = self._buf("rrecs", 16 * max(1, int(recv.sum())), dev)
+        self._a2av(rrecs[: 16 * int(recv.sum())], b["send_recs"][: 16 * int(send.sum())],
+                   [16 * int(x) for x in recv], [16 * int(x) for x in send])
+        rhdr = self._buf("rhdr", (W, 4 * hs), dev)
+        self._a2av(rhdr.view(-1), b["send_hdr"].reshape(-1), [4 * hs] * W, [4 * hs] * W)
+        nmax = max(1, int(allc[:, W:].max()))
+        gv = self._gather_rows(b["new_v"], 4 * nmax, "gnewv")
+        gh = self._gather_rows(b["new_h"], 4 * nmax, "gnewh")
+        s.step_owner_v(rrecs.data_ptr(), rhdr.data_ptr(), recv, gv.data_ptr(), gh.data_ptr(), allc[:, W:], nmax)
+        self.received_bytes += 16 * int(recv.sum() - recv[r]) + 4 * hs * (W - 1)
+        self.bytes_sent += 16 * int(send.sum() - send[r]) + 4 * hs * (W - 1)
+        # 2. the V values every owner updated
+        b = s.owner_buffers()
+        vc = self._gather_rows(b["out_counts"].view(torch.uint8)[:8], 8, "vcnt")
+        vcount = self._host(vc).view(np.int64).reshape(W)
+        vmax = max(1, int(vcount.max()))
+        gs = self._gather_rows(b["v_slot"], 4 * vmax, "gvs")
+        gval = self._gather_rows(b["v_val"], 8 * vmax, "gvv")
+        s.step_owner_h(gs.data_ptr(), gval.data_ptr(), vcount, vmax)
+        if not s.actor:
+            s.step_owner_end(0, 0, None, 0, 0, 0)
+            self.exchanges += 1
+            return
+        # 3. the H increments and tile summaries every owner produced
+        hc = self._gather_rows(b["out_counts"].view(torch.uint8)[8:16], 8, "hcnt")
+        hcount = self._host(hc).view(np.int64).reshape(W)
+        hmax = max(1, int(hcount.max()))
+        gk = self._gather_rows(b["h_key"], 4 * hmax, "ghk")
+        gq = self._gather_rows(b["h_q"], 8 * hmax, "ghq")
+        gt = self._gather_rows(b["tsum"], 40 * hs, "gts")
+        s.step_owner_end(gk.data_ptr(), gq.data_ptr(), hcount, hmax, gt.data_ptr(), hs)
+        self.exchanges += 1
 
     def _step_tiled(self):
         s = self.shard
@@ -248,7 +334,7 @@ class TableSync:
         s = self.shard
         if self.tiled:
             for _ in range(int(n_steps)):
-                self._step_tiled()
+                self._step_owner() if self.owner else self._step_tiled()
             return
         for _ in range(int(n_steps)):
             due = s.apply_due()      # host-side state, no device sync
@@ -265,8 +351,55 @@ class TableSync:
             s.step_end()
 
 
+def _owner_step_coupled(shards):
+    """One owner-sharded step of shards coupled in-process: TableSync._step_owner's
+    exchanges done by slicing the shards' buffers (one device)."""
+    W = len(shards)
+    for s in shards:
+        s.step_owner_local()
+    bs = [s.owner_buffers() for s in shards]
+    hs = bs[0]["hdr_stride"]
+    allc = torch.stack([b["counts"] for b in bs]).cpu().numpy()
+    offs = np.concatenate([np.zeros((W, 1), np.int64), np.cumsum(allc[:, :W], axis=1)], axis=1)
+    nmax = max(1, int(allc[:, W:].max()))
+
+    def rows(key, nbytes):
+        out = []
+        for b in bs:
+            x = b[key]
+            out.append(x[:nbytes] if x.numel() >= nbytes else torch.nn.functional.pad(x, (0, nbytes - x.numel())))
+        return torch.stack(out).contiguous()
+
+    gv, gh = rows("new_v", 4 * nmax), rows("new_h", 4 * nmax)
+    keep = [gv, gh]
+    for q, s in enumerate(shards):
+        recv = allc[:, q]
+        recs = torch.cat([bs[r]["send_recs"][16 * int(offs[r, q]): 16 * int(offs[r, q + 1])] for r in range(W)]
+                         + [torch.empty(16, dtype=torch.uint8, device=gv.device)])
+        hdr = torch.stack([bs[r]["send_hdr"][q] for r in range(W)]).contiguous()
+        keep += [recs, hdr]
+        s.step_owner_v(recs.data_ptr(), hdr.data_ptr(), recv, gv.data_ptr(), gh.data_ptr(), allc[:, W:], nmax)
+    bs = [s.owner_buffers() for s in shards]
+    vcount = torch.stack([b["out_counts"][0] for b in bs]).cpu().numpy()
+    vmax = max(1, int(vcount.max()))
+    gs, gval = rows("v_slot", 4 * vmax), rows("v_val", 8 * vmax)
+    for s in shards:
+        s.step_owner_h(gs.data_ptr(), gval.data_ptr(), vcount, vmax)
+    if not shards[0].actor:
+        for s in shards:
+            s.step_owner_end(0, 0, None, 0, 0, 0)
+    else:
+        hcount = torch.stack([b["out_counts"][1] for b in bs]).cpu().numpy()
+        hmax = max(1, int(hcount.max()))
+        gk, gq, gt = rows("h_key", 4 * hmax), rows("h_q", 8 * hmax), rows("tsum", 40 * hs)
+        for s in shards:
+            s.step_owner_end(gk.data_ptr(), gq.data_ptr(), hcount, hmax, gt.data_ptr(), hs)
+    torch.cuda.synchronize()      # the gathered buffers outlive the kernels that read them
+    del keep
+
+
 def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16, sync_period: int = 1,
-                 dense: bool = False, async_records: bool = False, tiled: bool = False):
+                 dense: bool = False, async_records: bool = False, tiled: bool = False, owner: bool = False):
     """TableSync's protocol for several shards driven by one process (e.g. one
     Learner per device, or shards of one device): the same phases, with the
     collectives replaced by handing every shard the others' records (or, dense,
@@ -279,6 +412,14 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
     than ``capacity`` is reported at the shard's next sync point."""
     for s in shards:
         s.set_sync_period(sync_period)
+    if owner:      # TableSync's owner-sharded exchange: shard q sums the tiles it owns
+        for q, s in enumerate(shards):
+            if getattr(s, "_owners", None) != (len(shards), q):
+                s.set_tile_owners(len(shards), q)
+                s._owners = (len(shards), q)
+        for _ in range(int(n_steps)):
+            _owner_step_coupled(shards)
+        return
     if tiled:      # TableSync's tiled exchange: every shard sums all shards' records (equal E)
         for _ in range(int(n_steps)):
             for s in shards:

@@ -42,6 +42,9 @@ EXPORTED = [
     "ffm_learner_apply_due", "ffm_learner_dense_buffers", "ffm_learner_dense_adopt",
     "ffm_learner_tiled_buffers", "ffm_learner_step_tiled_local", "ffm_learner_step_tiled_apply",
     "ffm_learner_set_external_sync", "ffm_learner_flush_begin", "ffm_learner_flush_end",
+    "ffm_learner_set_tile_owners", "ffm_learner_owner_buffers", "ffm_learner_step_owner_local",
+    "ffm_learner_step_owner_v", "ffm_learner_step_owner_h", "ffm_learner_step_owner_end",
+    "ffm_learner_set_epsilon_stride",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -71,6 +74,20 @@ class LearnDesc(C.Structure):
         ("block_size", C.c_int32), ("max_steps", C.c_int32),
         ("log2_v_capacity", C.c_int32), ("log2_h_capacity", C.c_int32),
         ("eps_start", C.c_double), ("eps_end", C.c_double), ("eps_offset", C.c_double), ("eps_span", C.c_double),
+    ]
+
+
+class OwnerBuffers(C.Structure):
+    """ffm_owner_buffers (include/ffm_amd.h): the owner-sharded exchange's device buffers."""
+    _fields_ = [
+        ("world", C.c_int32), ("rank", C.c_int32),
+        ("send_recs", C.c_void_p), ("send_rec_capacity", C.c_int64),
+        ("send_hdr", C.c_void_p), ("hdr_stride", C.c_int64),
+        ("counts", C.c_void_p),
+        ("new_v", C.c_void_p), ("new_h", C.c_void_p), ("new_v_capacity", C.c_int64), ("new_h_capacity", C.c_int64),
+        ("v_slot", C.c_void_p), ("v_val", C.c_void_p), ("h_key", C.c_void_p), ("h_q", C.c_void_p),
+        ("out_counts", C.c_void_p), ("out_capacity", C.c_int64),
+        ("tsum", C.c_void_p), ("tsum_count", C.c_int64),
     ]
 
 
@@ -140,6 +157,7 @@ def load_library():
     L.ffm_learner_set_placement.argtypes = [P, P, i32, i32]
     L.ffm_learner_set_epsilon_schedule.argtypes = [P, C.c_double, C.c_double, C.c_double, C.c_double]
     L.ffm_learner_set_epsilon_phase.argtypes = [P, i32]
+    L.ffm_learner_set_epsilon_stride.argtypes = [P, i64]
     L.ffm_learner_drain_episodes.argtypes = [P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     L.ffm_learner_set_trajectory_capture.argtypes = [P, P, P, i32, i32, i64, P]
     L.ffm_learner_delta_export_async.argtypes = [P, i32, P, P, i64, P, P]
@@ -152,6 +170,12 @@ def load_library():
     L.ffm_learner_step_tiled_local.argtypes = [P, P]
     L.ffm_learner_step_tiled_apply.argtypes = [P, P, P, i64, P]
     L.ffm_learner_drain_trajectory.argtypes = [P, P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
+    L.ffm_learner_set_tile_owners.argtypes = [P, i32, i32]
+    L.ffm_learner_owner_buffers.argtypes = [P, C.POINTER(OwnerBuffers)]
+    L.ffm_learner_step_owner_local.argtypes = [P, P]
+    L.ffm_learner_step_owner_v.argtypes = [P, P, P, P, P, P, P, i64, P]
+    L.ffm_learner_step_owner_h.argtypes = [P, P, P, P, i64, P]
+    L.ffm_learner_step_owner_end.argtypes = [P, P, P, P, i64, P, i64, P]
     L.ffm_learner_set_external_sync.argtypes = [P, i32]
     L.ffm_learner_flush_begin.argtypes = [P, C.POINTER(i32)]
     L.ffm_learner_flush_end.argtypes = [P, P]
@@ -487,6 +511,7 @@ class Learner:
         self.n_envs, self.n_agents = int(n_envs), int(n_agents)
         self.A = int(agent_capacity if agent_capacity is not None else max(1, n_agents))
         self.rng = rng
+        self.env_base, self.max_steps = int(env_base), int(max_steps)
         d = EngineDesc()
         d.abi_version = ABI_VERSION
         d.variant = _LEARN_VARIANTS[variant]
@@ -568,9 +593,10 @@ class Learner:
         _check(self._L.ffm_learner_set_epsilon_schedule(self._h, float(start), float(end), float(offset),
                                                           float(span)))
 
-    def set_epsilon_phase(self, period: int):
-        """Env g starts the epsilon schedule at its (g % period)-th episode (0 = off)."""
+    def set_epsilon_phase(self, period: int, stride: int = 1):
+        """Env g starts the epsilon schedule at its ((g % period) * stride)-th episode (0 = off)."""
         _check(self._L.ffm_learner_set_epsilon_phase(self._h, int(period)))
+        _check(self._L.ffm_learner_set_epsilon_stride(self._h, int(stride)))
 
     def drain_episodes(self, stream=None) -> np.ndarray:
         """Ended episodes since the last drain: int32 [n, 4] rows {global env, episode index,
@@ -848,6 +874,65 @@ class Learner:
     def step_tiled_apply(self, recs_ptr: int, tstart_ptr: int, n_envs_all: int, stream=None):
         _check(self._L.ffm_learner_step_tiled_apply(self._h, recs_ptr, tstart_ptr, int(n_envs_all),
                                                     _stream_handle(stream)))
+
+    # -- the owner-sharded tiled step -----------------------------------------
+    @property
+    def tile_major(self) -> bool:
+        """Tiled learners reorder their records tile-major unless FFM_TILE_MAJOR=0 (A/B)."""
+        return self.tiled and os.environ.get("FFM_TILE_MAJOR", "1") != "0"
+
+    def set_tile_owners(self, world: int, rank: int):
+        """Deal the tiles of cells over `world` ranks; this learner owns rank `rank`'s."""
+        _check(self._L.ffm_learner_set_tile_owners(self._h, int(world), int(rank)))
+
+    def owner_buffers(self) -> dict:
+        """Torch views (zero copy) of the exchange buffers: byte views where a collective
+        carries them (records, headers, slot lists), typed views for the counts."""
+        import torch
+        b = OwnerBuffers()
+        _check(self._L.ffm_learner_owner_buffers(self._h, C.byref(b)))
+        dev = torch.device("cuda", self.device)
+
+        def view(ptr, n, typestr):
+            if not ptr or n <= 0:
+                return torch.empty(0, dtype=torch.uint8, device=dev)
+            return torch.as_tensor(_DevArray(ptr, n, typestr), device=dev)
+
+        w, hs, oc = int(b.world), int(b.hdr_stride), int(b.out_capacity)
+        return {
+            "world": w, "rank": int(b.rank), "hdr_stride": hs, "out_capacity": oc,
+            "tsum_count": int(b.tsum_count),
+            "send_recs": view(b.send_recs, 16 * int(b.send_rec_capacity), "|u1"),
+            "send_hdr": view(b.send_hdr, 4 * w * hs, "|u1").view(w, 4 * hs),
+            "counts": view(b.counts, w + 2, "<i8"),
+            "new_v": view(b.new_v, 4 * int(b.new_v_capacity), "|u1"),
+            "new_h": view(b.new_h, 4 * int(b.new_h_capacity), "|u1"),
+            "v_slot": view(b.v_slot, 4 * oc, "|u1"), "v_val": view(b.v_val, 8 * oc, "|u1"),
+            "h_key": view(b.h_key, 4 * oc, "|u1"), "h_q": view(b.h_q, 8 * oc, "|u1"),
+            "out_counts": view(b.out_counts, 2, "<i8"),
+            "tsum": view(b.tsum, 40 * hs, "|u1"),
+        }
+
+    def step_owner_local(self, stream=None):
+        _check(self._L.ffm_learner_step_owner_local(self._h, _stream_handle(stream)))
+
+    def step_owner_v(self, recs_ptr: int, hdrs_ptr: int, recv_counts, new_v_ptr: int, new_h_ptr: int, new_counts,
+                     new_stride: int, stream=None):
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        nc = np.ascontiguousarray(new_counts, np.int64)
+        _check(self._L.ffm_learner_step_owner_v(self._h, recs_ptr, hdrs_ptr, _ptr(rc), new_v_ptr, new_h_ptr, _ptr(nc),
+                                                int(new_stride), _stream_handle(stream)))
+
+    def step_owner_h(self, v_slot_ptr: int, v_val_ptr: int, v_counts, v_stride: int, stream=None):
+        vc = np.ascontiguousarray(v_counts, np.int64)
+        _check(self._L.ffm_learner_step_owner_h(self._h, v_slot_ptr, v_val_ptr, _ptr(vc), int(v_stride),
+                                                _stream_handle(stream)))
+
+    def step_owner_end(self, h_key_ptr: int, h_q_ptr: int, h_counts, h_stride: int, tsum_ptr: int, tsum_stride: int,
+                       stream=None):
+        hc = np.ascontiguousarray(h_counts if h_counts is not None else np.zeros(1), np.int64)
+        _check(self._L.ffm_learner_step_owner_end(self._h, h_key_ptr, h_q_ptr, _ptr(hc), int(h_stride), tsum_ptr,
+                                                  int(tsum_stride), _stream_handle(stream)))
 
     # -- telemetry -----------------------------------------------------------------------
     def counters(self, stream=None) -> dict:

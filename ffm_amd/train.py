@@ -17,6 +17,12 @@ the reference's local schedule ``start + (end - start) * episode / episodes``
 with the episode index counted per env (``Learner.set_epsilon_schedule``).
 
     python -m ffm_amd.train --variant unified --mode critic_only --out runs/critic
+    python -m ffm_amd.train --variant actor_only --n 32 --envs 65536 --out runs/actor   # config 4
+    python -m torch.distributed.run --nproc-per-node 8 -m ffm_amd.train --variant actor_only --n 32 --envs 65536
+
+The per-N drivers (``--variant actor_only``: run_actor_only_training.py; ``--variant ac``:
+run_critic_training.py) shard over ranks under torch.distributed.run: every rank steps
+its own global env ids and ffm_amd.dist.TableSync exchanges the table increments.
 """
 from __future__ import annotations
 
@@ -199,42 +205,358 @@ def write_outputs(L: Learner, result: dict, out_dir: str, exit_pos, radius_list,
                     f"V states {c['v_before']:6d} -> {c['v_after']:6d} (+{c['v_after'] - c['v_before']:5d})\n")
 
 
-def main():
+# ---------------------------------------------------------------------------
+# The per-N drivers: run_actor_only_training.py (ffm_actor_only, config 4) and
+# run_critic_training.py (ffm_ac_core)
+# ---------------------------------------------------------------------------
+# Each reference driver's module constants (MODEL_PARAMS, N list, episodes, MAX_STEPS, epsilon).
+DRIVERS = {
+    "actor_only": {     # run_actor_only_training.py:27-58
+        "script": "run_actor_only_training.py",
+        "params": {"k_D": 1, "k_A": 10, "alpha_v": 0.1, "alpha_h": 0.1, "gamma": 0.95, "exit_reward": 100.0,
+                   "step_penalty": 0.0, "collision_penalty": -1.0, "neighborhood": "neumann", "epsilon": 0.2},
+        "n_list": [1, 1],                   # N_FIXED + range(N_START, N_END + 1, N_STEP) = [1] + [1]
+        "episodes": 10000, "max_steps": 1000, "eps": (0.2, 0.01), "trajectory_every": 100,
+    },
+    "ac": {             # run_critic_training.py:19-43
+        "script": "run_critic_training.py",
+        "params": {"k_S": 10, "k_D": 1, "alpha_v": 0.01, "gamma": 0.99, "exit_reward": 100.0, "step_penalty": -1.0,
+                   "collision_penalty": -1.0, "neighborhood": "neumann", "block_size": 5},
+        "n_list": [1] + list(range(10, 101, 10)),
+        "episodes": 1000, "max_steps": 500, "eps": None, "trajectory_every": 0,
+    },
+    "unified": {        # run_unified_{critic,actor}_training.py MODEL_PARAMS
+        "script": "run_unified_actor_training.py",
+        "params": {"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99,
+                   "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0, "neighborhood": "neumann",
+                   "block_size": 1},
+        "n_list": [1] + list(range(10, 91, 10)),
+        "episodes": 1000, "max_steps": 300, "eps": (0.2, 0.01), "trajectory_every": 100,
+    },
+}
+
+
+class _Group:
+    """The ranks of a sharded run (torch.distributed), or one process."""
+
+    def __init__(self, sync=None):
+        self.sync = sync
+        if sync is not None:
+            import torch.distributed as dist
+            self.dist, self.rank, self.world = dist, dist.get_rank(), dist.get_world_size()
+        else:
+            self.dist, self.rank, self.world = None, 0, 1
+
+    def step(self, L, n):
+        if self.sync is not None:
+            self.sync.step(n)
+        else:
+            L.step(n)
+
+    def min_int(self, x: int) -> int:
+        if self.dist is None:
+            return int(x)
+        import torch
+        t = torch.tensor([int(x)], dtype=torch.int64, device=self.sync.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return int(t.item())
+
+    def gather(self, obj) -> list:
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def flush(self):
+        if self.sync is not None:
+            self.sync.flush()
+
+
+def _pickle_table(L: Learner, which: str) -> dict:
+    """get_v_table() / get_h_table() of the reference's model (key objects, insertion order)."""
+    keys, vals = L.export_table(which)
+    if which == "V":
+        return {_key_obj(L.variant, k): float(v) for k, v in zip(keys.tolist(), vals.tolist())}
+    return {_key_obj(L.variant, k): [float(x) for x in r] for k, r in zip(keys.tolist(), vals.tolist())}
+
+
+def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: str | None = None,
+              trajectory_every: int = 0, group: _Group | None = None, log_every: int = 16, verbose: bool = True,
+              params: dict | None = None, global_envs: int | None = None, inert_v: dict | None = None) -> dict:
+    """The reference's per-N drivers (run_actor_only_training.py:165-300, run_critic_training.py:
+    136-209), batched: for every N of n_list the E envs (of every rank) run
+    `episodes_per_n` full-room episodes in parallel (placement over every free cell,
+    model/ffm_actor_only.py:557-563), the tables shared by all of them.
+
+    Episodes are numbered env-major over the global envs: env g's k-th episode of pattern
+    i is pattern episode g * per_env + k + 1 (per_env = ceil(P / G) for G global envs) and
+    run episode i * P + that; the first P of every pattern are reported (the envs past them
+    run on, unreported, until every env has ended per_env episodes).  With `eps`, the
+    explore rate follows the drivers' one linear schedule over all episodes of the run
+    (run_actor_only_training.py:190-196: start + (end - start) * (j - 1) / (total - 1) for
+    run episode j).  Trajectories of pattern episodes that are multiples of
+    `trajectory_every` (:199-218).  Writes the driver's files (per-N H snapshots, the final
+    tables, training_results.pkl, summary.txt) on rank 0."""
+    L = learner
+    g = group or _Group()
+    E = L.n_envs
+    G = int(global_envs or E * g.world)
+    env_base = L.env_base
+    P = int(episodes_per_n)
+    per_env = max(1, math.ceil(P / G))
+    total = len(n_list) * P
+    chunk = max(1, min(int(log_every), 16))
+    actor = L.actor
+    t_start = time.time()
+    all_results, episode_results = [], []
+    inert_v = dict(inert_v or {})      # ffm_actor_only's pretrained critic: counted, never read (its module doc)
+    v_initial = len(inert_v)
+    n_traj = 0
+    if out_dir and g.rank == 0:
+        os.makedirs(out_dir, exist_ok=True)
+    # trajectories: pattern episode n = g * per_env + k + 1 with n % every == 0, n <= P
+    tsel, tph = np.zeros(0, np.int32), None
+    if trajectory_every > 0:
+        envs, phases = [], []
+        for e in range(E):
+            ph = ((env_base + e) * per_env + 1) % trajectory_every
+            if (-ph) % trajectory_every < per_env:
+                envs.append(e)
+                phases.append(ph)
+        tsel, tph = np.asarray(envs, np.int32), np.asarray(phases, np.int32)
+        if len(tsel):
+            L.set_trajectory_capture(tsel, period=trajectory_every, phases=tph, capacity_rows=len(tsel) * chunk * 2)
+    for pi, N in enumerate(n_list):
+        L.set_placement(None, n_agents=N)                  # every free cell: the full-room reset
+        base = pi * P                                      # run episodes before this pattern
+        if eps is not None and actor:
+            es, ee = eps
+            if total > 1:
+                L.set_epsilon_schedule(es, ee, base, total - 1)
+                L.set_epsilon_phase(G, per_env)            # + g * per_env: env-major numbering
+            else:
+                L.set_epsilon_schedule(es, ee, 0, 0)
+                L.set_epsilon(es)
+        L.reset()
+        done, trajs, sizes = [], {}, []
+        while True:
+            g.step(L, chunk)
+            d = L.drain_episodes()
+            vs = L.table_size("V") + v_initial
+            hs = L.table_size("H") if actor else 0
+            if len(d):
+                done.append(np.concatenate([d, np.full((len(d), 1), len(sizes), np.int64)], axis=1))
+            sizes.append((vs, hs))
+            if len(tsel):
+                for key, val in L.drain_trajectories().items():
+                    st, ps = trajs.setdefault(key, ([], []))
+                    st.extend(val[0])
+                    ps.extend(val[1])
+            if g.min_int(int(L.episodes()[0].min())) >= per_env:
+                break
+        ended = np.concatenate(done) if done else np.zeros((0, 5), np.int64)
+        ended = ended[ended[:, 1] < per_env]
+        n_pat = ended[:, 0] * per_env + ended[:, 1] + 1       # pattern episode (global env g = column 0)
+        keep = n_pat <= P
+        ended, n_pat = ended[keep], n_pat[keep]
+        rows = []
+        for (genv, k, steps, emptied, ci), n in zip(ended.tolist(), n_pat.tolist()):
+            j = base + n
+            vs, hs = sizes[ci]
+            e_j = 0.0
+            if eps is not None and actor:
+                prog = (j - 1) / (total - 1) if total > 1 else 0.0
+                e_j = float(np.clip(eps[0] + (eps[1] - eps[0]) * prog, 0.0, 1.0))
+            rows.append({"episode_num": j, "N": N, "steps": int(steps), "emptied": int(emptied),
+                         "v_initial_size": v_initial, "v_current_size": vs, "v_new_states": vs - v_initial,
+                         "h_states": hs, "h_total_actions": hs * L.n_actions, "epsilon": e_j, "v_table_size": vs})
+            tr = trajs.get((genv, k))
+            if tr is not None and out_dir and n % trajectory_every == 0:
+                assert len(tr[0]) == steps and tr[0] == list(range(1, steps + 1)), "trajectory rows"
+                save_trajectory(os.path.join(out_dir, "trajectories"), N, n, j, tr[1], steps)
+                n_traj += 1
+        rows = sorted(sum(g.gather(rows), []), key=lambda r: r["episode_num"])
+        pattern = {"N": N, "episodes": [r["episode_num"] - base for r in rows],
+                   "v_initial_size": [r["v_initial_size"] for r in rows],
+                   "v_current_size": [r["v_current_size"] for r in rows],
+                   "v_new_states": [r["v_new_states"] for r in rows],
+                   "h_table_sizes": [(r["h_states"], r["h_total_actions"]) for r in rows],
+                   "v_table_sizes": [r["v_table_size"] for r in rows],
+                   "avg_steps": [r["steps"] for r in rows], "epsilons": [r["epsilon"] for r in rows]}
+        all_results.append(pattern)
+        episode_results.extend(rows)
+        g.flush()
+        if actor:
+            h_n = _pickle_table(L, "H")
+            if out_dir and g.rank == 0:                     # run_actor_only_training.py:293-300
+                with open(os.path.join(out_dir, f"H_actor_N{N}_total{P}ep.pkl"), "wb") as f:
+                    pickle.dump(h_n, f)
+        if verbose and g.rank == 0:
+            print(f"N={N:3d}: mean steps={np.mean(pattern['avg_steps']):7.2f} over {len(rows)} episodes, "
+                  f"V {L.table_size('V')}, H {L.table_size('H') if actor else 0}", flush=True)
+    g.flush()
+    result = {"n_list": list(n_list), "episodes_per_n": P, "model_params": dict(params or {}),
+              "results_by_n": all_results, "all_episodes": episode_results, "total_time": time.time() - t_start,
+              "trajectories": n_traj}
+    if len(tsel):
+        L.set_trajectory_capture([])
+    v_table = {**inert_v, **_pickle_table(L, "V")}
+    h_table = _pickle_table(L, "H") if actor else {}
+    result["final_v_table_size"] = result["final_v_current_size"] = len(v_table)
+    if actor:
+        result.update(final_v_initial_size=v_initial, final_v_new_states=len(v_table) - v_initial,
+                      final_h_states=len(h_table), final_h_total_actions=len(h_table) * L.n_actions,
+                      epsilon_start=eps[0] if eps else None, epsilon_end=eps[1] if eps else None)
+    if out_dir and g.rank == 0:
+        _write_per_n_outputs(out_dir, L, result, v_table, h_table, total)
+    return result
+
+
+def _write_per_n_outputs(out_dir, L, result, v_table, h_table, total):
+    """The final tables, training_results.pkl and summary.txt of the driver
+    (run_actor_only_training.py:317-443, run_critic_training.py:216-309)."""
+    actor = L.actor
+    vname = f"V_updated_total{total}ep.pkl" if actor else f"V_integrated_total{total}ep.pkl"
+    with open(os.path.join(out_dir, vname), "wb") as f:
+        pickle.dump(v_table, f)
+    if actor:
+        with open(os.path.join(out_dir, f"H_actor_total{total}ep.pkl"), "wb") as f:
+            pickle.dump(h_table, f)
+    with open(os.path.join(out_dir, "training_results.pkl"), "wb") as f:
+        pickle.dump(result, f)
+    vals = list(v_table.values())
+    with open(os.path.join(out_dir, "summary.txt"), "w", encoding="utf-8") as f:
+        f.write("=" * 80 + "\n")
+        f.write(f"batched {L.variant} training, {L.n_envs} envs per rank, seed-keyed Philox streams\n")
+        f.write("=" * 80 + "\n")
+        f.write(f"total time: {result['total_time']:.1f} s\n")
+        f.write(f"final V states: {len(v_table)}\n")
+        if vals:
+            f.write(f"  V range: [{min(vals):.2f}, {max(vals):.2f}]\n  V mean: {np.mean(vals):.2f}\n")
+        if actor:
+            f.write(f"  actor H states: {len(h_table)} (actions: {len(h_table) * L.n_actions})\n")
+            hv = [x for r in h_table.values() for x in r]
+            if hv:
+                f.write(f"  H logit range: [{min(hv):.2f}, {max(hv):.2f}]\n  H mean logit: {np.mean(hv):.2f}\n")
+            if result.get("epsilon_start") is not None:
+                f.write(f"  epsilon schedule: start={result['epsilon_start']:.3f}, end={result['epsilon_end']:.3f}\n")
+        f.write(f"\nN list: {result['n_list']}\ntotal episodes: {total}\n"
+                f"episodes per N: {result['episodes_per_n']}\nmax steps: {L.max_steps}\n")
+        f.write("\nmodel parameters:\n")
+        for k, v in result["model_params"].items():
+            f.write(f"  {k}: {v}\n")
+        f.write("\nper N:\n" + "-" * 80 + "\n")
+        for r in result["results_by_n"]:
+            v0, v1 = r["v_current_size"][0], r["v_current_size"][-1]
+            line = (f"N={r['N']:3d}: mean steps={np.mean(r['avg_steps']):6.2f}, V states {v0:5d}->{v1:5d} "
+                    f"(+{v1 - v0:4d})")
+            if actor:
+                line += f", H states {r['h_table_sizes'][-1][0]:5d} (actions: {r['h_table_sizes'][-1][1]})"
+            f.write(line + "\n")
+
+
+def driver_settings(variant: str, a=None) -> dict:
+    """The settings a run of `variant` uses: the reference driver's constants, overridden by
+    the command line where given (a: parsed arguments)."""
+    d = {k: (list(v) if isinstance(v, list) else v) for k, v in DRIVERS[variant].items()}
+    d["params"] = dict(d["params"])
+    if a is not None:
+        if a.max_steps is not None:
+            d["max_steps"] = a.max_steps
+        if a.episodes is not None:
+            d["episodes"] = a.episodes
+        if a.n is not None:
+            d["n_list"] = [int(x) for x in a.n.split(",")]
+        if a.eps is not None:
+            d["eps"] = tuple(float(x) for x in a.eps.split(","))
+        if a.trajectory_every is not None:
+            d["trajectory_every"] = a.trajectory_every
+    return d
+
+
+def _init_dist():
+    """torch.distributed.run sets WORLD_SIZE / RANK / LOCAL_RANK: one rank per GPU."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("FFM_DIST_BACKEND", "nccl")
+    dev = local if backend == "nccl" else int(os.environ.get("FFM_DEVICE", str(local)))
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group(backend)
+    return dev
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("--variant", default="unified", choices=["unified", "actor_only", "ac"])
+    ap.add_argument("--variant", default="unified", choices=["unified", "actor_only", "ac"],
+                    help="unified: the radius curriculum (run_unified_*_training.py); actor_only: "
+                         "run_actor_only_training.py; ac: run_critic_training.py")
     ap.add_argument("--mode", default="critic_only", choices=["critic_only", "actor_only", "both"])
     ap.add_argument("--size", type=int, default=12)
-    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--map", default=None, help="map .npy (default: the synthetic --size room)")
+    ap.add_argument("--sff", default=None, help="SFF .npy (default: the L1 distance field of the map)")
+    ap.add_argument("--envs", type=int, default=4096, help="envs per rank")
     ap.add_argument("--radius", default="3,5,7,9,11,13,15")
-    ap.add_argument("--n", default="1,10,20,30,40,50,60,70,80,90")
-    ap.add_argument("--episodes", type=int, default=1000, help="episodes per configuration")
-    ap.add_argument("--max-steps", type=int, default=300)
-    ap.add_argument("--eps", default="0.2,0.01", help="epsilon start,end (actor modes)")
+    ap.add_argument("--n", default=None, help="N list (default: the driver's)")
+    ap.add_argument("--episodes", type=int, default=None, help="episodes per configuration / per N")
+    ap.add_argument("--max-steps", type=int, default=None)
+    ap.add_argument("--eps", default=None, help="epsilon start,end (actor modes)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--out", default=None)
     ap.add_argument("--critic", default=None,
                     help="pretrained V table (a V_table.pkl this tool wrote; the reference's actor drivers "
                          "load their critic run's pickle, run_unified_actor_training.py PRETRAINED_CRITIC)")
     ap.add_argument("--trajectory-every", type=int, default=None,
-                    help="save every n-th episode's trajectory (default 100 for actor modes, as "
-                         "run_actor_only_training.py; 0 = none)")
+                    help="save every n-th episode's trajectory (default: the driver's, 100 for actor modes)")
     ap.add_argument("--no-eps-phase", action="store_true",
                     help="with envs >= episodes: every env at the schedule's first episode (no spread)")
-    a = ap.parse_args()
-    m = make_room(a.size, a.size)
-    # run_unified_*_training.py MODEL_PARAMS
-    params = {"k_S": 10, "k_D": 1, "k_A": 10, "alpha_v": 0.01, "alpha_h": 0.1, "gamma": 0.99,
-              "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0, "neighborhood": "neumann",
-              "block_size": 1}
-    n_list = [int(x) for x in a.n.split(",")]
-    L = Learner(m, l1_sff(m), a.variant, n_envs=a.envs, n_agents=max(n_list), mode=a.mode, params=params,
-                seed=a.seed, max_steps=a.max_steps)
-    if a.critic:
+    a = ap.parse_args(argv)
+    d = driver_settings(a.variant, a)
+    if a.map:
+        m = np.load(a.map, allow_pickle=False).astype(np.uint8)
+    else:
+        m = make_room(a.size, a.size)
+    s = np.load(a.sff, allow_pickle=False) if a.sff else l1_sff(m)
+    dev = _init_dist()
+    rank = 0
+    if dev is not None:
+        import torch.distributed as dist
+        rank = dist.get_rank()
+    n_list = d["n_list"]
+    L = Learner(m, s, a.variant, n_envs=a.envs, n_agents=max(n_list), mode=a.mode if a.variant == "unified" else None,
+                params=d["params"], seed=a.seed, max_steps=d["max_steps"], env_base=rank * a.envs,
+                device=dev or 0)
+    inert = None
+    if a.critic and a.variant == "actor_only":
+        # model/ffm_actor_only.py:55-66 re-keys the pretrained critic by tuples of ints, which never
+        # equal the step's pickled-bytes keys: the entries only count (the drop-in class does the same)
+        with open(a.critic, "rb") as f:
+            table = pickle.load(f)   # a V table this tool wrote (never a reference file)
+        inert = {tuple(tuple(int(x) for x in sub) for sub in pickle.loads(k)): v for k, v in table.items()}
+    elif a.critic:
         load_critic(L, a.critic)
-    es, ee = (float(x) for x in a.eps.split(","))
-    every = a.trajectory_every if a.trajectory_every is not None else (100 if L.actor else 0)
-    run_curriculum(L, (0, a.size // 2), [int(x) for x in a.radius.split(",")], n_list, a.episodes, es, ee, a.out,
-                   trajectory_every=every, eps_phase=not a.no_eps_phase)
+    if a.variant == "unified":
+        if dev is not None:
+            raise SystemExit("the radius curriculum runs on one device (use --variant actor_only / ac to shard)")
+        es, ee = d["eps"]
+        run_curriculum(L, (0, m.shape[1] // 2), [int(x) for x in a.radius.split(",")], n_list, d["episodes"], es, ee,
+                       a.out, trajectory_every=d["trajectory_every"] if L.actor else 0, eps_phase=not a.no_eps_phase)
+        return
+    group = _Group()
+    if dev is not None:
+        from .dist import TableSync
+        group = _Group(TableSync(L, device="cuda", capacity=None))
+    run_per_n(L, n_list, d["episodes"], d["eps"], a.out, d["trajectory_every"] if L.actor else 0, group,
+              params=d["params"], inert_v=inert)
+    if dev is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -296,6 +296,57 @@ int ffm_learner_tiled_buffers(ffm_learner* l, void** d_recs, int64_t* rec_bytes,
 int ffm_learner_step_tiled_local(ffm_learner* l, void* stream);
 int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const uint16_t* d_tstart_all,
                                  int64_t n_envs_all, void* stream);
+/* The owner-sharded tiled step: the tiles of cells are dealt to the ranks
+ * (chunks of 64 tiles round-robin) and each rank sums only its own tiles' records, from all
+ * ranks, so the per-rank table work does not grow with the rank count.  Per step:
+ *   step_owner_local: the step; the records packed tile-major by destination rank
+ *     (send_recs, counts[q] records for rank q from offset sum(counts[<q]); send_hdr row q:
+ *     q's tiles' record offsets within its block, hdr_stride u32 per row) and this rank's new
+ *     V / H slots (new_v / new_h, counts[world] / counts[world + 1]);
+ *   the ranks all-to-all the records and header rows and all-gather the new slots;
+ *   step_owner_v: adopts the other ranks' new slots, sums this rank's tiles' V (the received
+ *     blocks back to back, source rank order; hdrs = the received header rows), writes the
+ *     updated V values to v_slot / v_val (out_counts[0]);
+ *   the ranks all-gather those;
+ *   step_owner_h: stores the other ranks' V values; actor modes sum this rank's tiles' H
+ *     (h_key = slot | action << 28, h_q = the fixed-point increment; out_counts[1]) and write
+ *     the tiles' H summaries (tsum, tsum_count rows of 5 doubles);
+ *   the ranks all-gather those;
+ *   step_owner_end: applies the other ranks' H increments and summaries, the H statistics,
+ *     ends the step.
+ * Counts passed as int64_t* are HOST arrays ([world]; new_counts [world][2]); record and
+ * table buffers are DEVICE pointers, "_all" buffers rank-major with the given row stride in
+ * elements.  Every rank ends each step with the tables one device stepping all envs would
+ * hold, bit for bit.  Buffer pointers can change at step_owner_v (out_capacity grows). */
+typedef struct ffm_owner_buffers {
+    int32_t world, rank;
+    void* send_recs;                 /* 16-B records */
+    int64_t send_rec_capacity;
+    uint32_t* send_hdr;
+    int64_t hdr_stride;
+    int64_t* counts;                 /* [world + 2] */
+    uint32_t* new_v;
+    uint32_t* new_h;
+    int64_t new_v_capacity, new_h_capacity;
+    uint32_t* v_slot;
+    double* v_val;
+    uint32_t* h_key;
+    int64_t* h_q;
+    int64_t* out_counts;             /* [2] */
+    int64_t out_capacity;
+    double* tsum;
+    int64_t tsum_count;
+} ffm_owner_buffers;
+int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank);
+int ffm_learner_owner_buffers(ffm_learner* l, ffm_owner_buffers* b);
+int ffm_learner_step_owner_local(ffm_learner* l, void* stream);
+int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, const int64_t* recv_counts,
+                             const uint32_t* d_new_v, const uint32_t* d_new_h, const int64_t* new_counts,
+                             int64_t new_stride, void* stream);
+int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const double* d_v_val,
+                             const int64_t* v_counts, int64_t v_stride, void* stream);
+int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q, const int64_t* h_counts,
+                               int64_t h_stride, const double* d_tsum_all, int64_t tsum_stride, void* stream);
 /* Table sync period K >= 1 (default 1 = the reference's per-step updates): the fixed-point
  * increments of K steps accumulate and V / H (and the actor's H statistics) are applied
  * at every K-th step only; a multi-rank run exchanges deltas at those steps only, so
@@ -332,6 +383,10 @@ int ffm_learner_set_epsilon_schedule(ffm_learner* l, double eps_start, double ep
  * P-episode per-configuration schedule (run_unified_actor_training.py:253-259) between them;
  * 0 = off (the default). */
 int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period);
+/* stride >= 1 (default 1): global env g adds (g % period) * stride instead, so envs that each
+ * run `stride` episodes cover a run-wide schedule with episodes numbered env-major (the single
+ * linear schedule over all episodes of run_actor_only_training.py:186-196). */
+int ffm_learner_set_epsilon_stride(ffm_learner* l, int64_t stride);
 /* Ended episodes since the last drain, in no particular order: records of 4 int32
  * {global env, episode index, steps, 1 = emptied / 0 = truncated at max_steps}
  * (the per-episode rows of run_*_training.py's steps_per_episode.csv).  *dropped counts

@@ -906,7 +906,7 @@ void ffo_lbatch_set_placement(ffo_lbatch* b, const uint16_t* cells, int32_t coun
 
 static double eps_of(const ffo_learn_cfg* c, int32_t k, int64_t genv) {
     if (!(c->eps_span > 0)) return c->epsilon;
-    const double ph = c->eps_phase > 0 ? (double)(genv % c->eps_phase) : 0.0;
+    const double ph = c->eps_phase > 0 ? (double)((genv % c->eps_phase) * (c->eps_stride > 0 ? c->eps_stride : 1)) : 0.0;
     double e = c->eps_start + (c->eps_end - c->eps_start) * (((double)k + c->eps_offset + ph) / c->eps_span);
     return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
 }

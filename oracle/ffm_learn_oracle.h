@@ -53,7 +53,8 @@ typedef struct {
      * run_unified_actor_training.py:253-259: offset 1, span episodes per config) */
     double eps_start, eps_end, eps_offset, eps_span;
     int32_t nb;               /* neighbours: 4 (neumann; 0 means 4) or 8 (moore, ffm_ac_core) */
-    int32_t eps_phase;        /* > 0: global env g adds g % eps_phase to k (envs spread over the schedule) */
+    int32_t eps_phase;        /* > 0: global env g adds (g % eps_phase) * eps_stride to k (envs spread over the schedule) */
+    int64_t eps_stride;       /* 0 means 1 */
 } ffo_learn_cfg;
 
 typedef struct ffo_tab ffo_tab;

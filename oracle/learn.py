@@ -46,7 +46,7 @@ class LearnCfg(C.Structure):
         ("exit_reward", C.c_double), ("step_penalty", C.c_double), ("collision_penalty", C.c_double),
         ("epsilon", C.c_double), ("v_default", C.c_double), ("block_size", C.c_int32),
         ("eps_start", C.c_double), ("eps_end", C.c_double), ("eps_offset", C.c_double), ("eps_span", C.c_double),
-        ("nb", C.c_int32), ("eps_phase", C.c_int32),
+        ("nb", C.c_int32), ("eps_phase", C.c_int32), ("eps_stride", C.c_int64),
     ]
 
 
@@ -166,9 +166,10 @@ class Learn:
         self.cfg.eps_start, self.cfg.eps_end = float(start), float(end)
         self.cfg.eps_offset, self.cfg.eps_span = float(offset), float(span)
 
-    def set_epsilon_phase(self, period: int):
-        """Global env g adds g % period to its ended-episode count in the schedule."""
+    def set_epsilon_phase(self, period: int, stride: int = 1):
+        """Global env g adds (g % period) * stride to its ended-episode count in the schedule."""
         self.cfg.eps_phase = int(period)
+        self.cfg.eps_stride = int(stride)
 
     def step_mt(self, pos, dff, np_rng, py_rng):
         p = np.ascontiguousarray(pos, dtype=np.int32).copy()

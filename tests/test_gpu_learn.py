@@ -334,6 +334,77 @@ def test_learner_tiled_shards_equal_one_learner(mode):
         L.close()
 
 
+@pytest.mark.parametrize("mode,world", [("actor_only", 3), ("both", 2), ("critic_only", 3), ("actor_only", 1)])
+def test_learner_owner_shards_equal_one_learner(mode, world):
+    """The owner-sharded tiled step (TableSync's exchange for tiled learners,
+    coupled in one process): the 1,024 tiles of a 64x64 room are dealt to the shards in
+    chunks of 64, each shard sums only its own tiles' records from every shard (all-to-all),
+    adopts the others' new slots, and takes the others' updated V values, H increments and
+    tile summaries.  Shards of unequal size (envs 7 / 5 / 4) end with the tables (values and
+    key sets) and env states of one learner stepping all envs, bit for bit."""
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.dist import step_coupled
+    m = make_room(64, 64)
+    s = l1_sff(m)
+    p = {"epsilon": 0.1, "block_size": 1}
+    sizes = {1: [16], 2: [9, 7], 3: [7, 5, 4]}[world]
+    n, N, T = sum(sizes), 600, 30
+    kw = dict(mode=mode, params=p, rng="philox", seed=8, auto_reset=True, max_steps=20)
+    one = _learner(m, s, "unified", n_envs=n, n_agents=N, **kw)
+    assert one.tiled and one.tile_major
+    one.reset()
+    one.step(T)
+    bases = np.concatenate([[0], np.cumsum(sizes)])
+    shards = [_learner(m, s, "unified", n_envs=c, n_agents=N, env_base=int(b), **kw) for b, c in zip(bases, sizes)]
+    for L in shards:
+        L.reset()
+    step_coupled(shards, T, device="cuda", owner=True)
+    op, oc, od = one.get_state()
+    sp = [L.get_state() for L in shards]
+    assert np.array_equal(oc, np.concatenate([x[1] for x in sp]))
+    assert np.array_equal(od.view(np.uint32), np.concatenate([x[2] for x in sp]).view(np.uint32))
+    for which in ("V", "H") if mode != "critic_only" else ("V",):
+        k0, v0 = one.export_table(which)
+        o0 = np.argsort(k0)
+        assert len(k0) > 1000
+        for L in shards:
+            k, v = L.export_table(which)
+            o = np.argsort(k)
+            assert np.array_equal(k[o], k0[o0]), which
+            assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), which
+    for L in shards + [one]:
+        L.close()
+
+
+def test_learner_tile_major_equals_env_major(monkeypatch):
+    """The tile-major record layout (pack: column scan, tile offsets, scatter) and the
+    env-major tile passes (FFM_TILE_MAJOR=0) give the same tables and states at a size whose
+    tiles need the general (multi-window) form in both: 700 envs > the env-major window."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(64, 64)
+    s = l1_sff(m)
+    kw = dict(mode="actor_only", params={"epsilon": 0.1, "block_size": 1}, rng="philox", seed=3, auto_reset=True,
+              max_steps=25)
+    out = []
+    for tm in ("1", "0"):
+        monkeypatch.setenv("FFM_TILE_MAJOR", tm)
+        L = _learner(m, s, "unified", n_envs=700, n_agents=300, **kw)
+        assert L.tile_major == (tm == "1")
+        L.reset()
+        L.step(12)
+        st = L.get_state()
+        tabs = {w: L.export_table(w) for w in ("V", "H")}
+        L.close()
+        out.append((st, tabs))
+    (s0, t0), (s1, t1) = out
+    assert np.array_equal(s0[1], s1[1]) and np.array_equal(s0[2].view(np.uint32), s1[2].view(np.uint32))
+    for w in ("V", "H"):
+        (k0, v0), (k1, v1) = t0[w], t1[w]
+        o0, o1 = np.argsort(k0), np.argsort(k1)
+        assert np.array_equal(k0[o0], k1[o1])
+        assert np.array_equal(np.asarray(v0)[o0].view(np.uint64), np.asarray(v1)[o1].view(np.uint64))
+
+
 def test_learner_philox_config5_geometry():
     """256x256 room, 8,192 agents (BASELINE config 5, ffm_unified actor_only): thresholded
     on-device placement (> 16,384 free cells) and the 8-agents-per-lane kernel."""
@@ -570,12 +641,14 @@ def test_rccl_table_sync_equals_one_learner(variant, mode, dense, tmp_path):
         assert np.array_equal(r[k], r["sync_" + k[4:]]), k
 
 
-@pytest.mark.parametrize("variant,mode", [("unified", "actor_only"), ("actor_only", None), ("unified", "critic_only")])
-def test_learner_curriculum_schedule_and_episode_log(variant, mode):
+@pytest.mark.parametrize("variant,mode,stride", [("unified", "actor_only", 1), ("actor_only", None, 3),
+                                                 ("unified", "critic_only", 1)])
+def test_learner_curriculum_schedule_and_episode_log(variant, mode, stride):
     """The batched training drivers' knobs against the CPU restatement: radius-limited
     placement (model/ffm_unified.py:150-171: min(N, cells within the radius)), the
-    per-env epsilon schedule (run_unified_actor_training.py:253-259), and the episode
-    log (one record per ended episode: env, index, steps, emptied)."""
+    per-env epsilon schedule (run_unified_actor_training.py:253-259; stride 3: env g at
+    episode (g % 7) * 3 of a run-wide schedule, run_actor_only_training.py:190-196), and the
+    episode log (one record per ended episode: env, index, steps, emptied)."""
     from ffm_amd.data import make_room, l1_sff
     from oracle import learn as LO
     from oracle import oracle as O
@@ -587,11 +660,11 @@ def test_learner_curriculum_schedule_and_episode_log(variant, mode):
     ncell = L.set_radius_placement((0, 6), 4, N)
     n = min(N, ncell)
     L.set_epsilon_schedule(0.2, 0.01, 1, 10)
-    L.set_epsilon_phase(7)                      # env g starts the schedule at episode g % 7
+    L.set_epsilon_phase(7, stride)              # env g starts the schedule at episode (g % 7) * stride
     L.reset()
     cpu = LO.Learn(m, s, variant, mode, p, log2_cap=22)
     cpu.set_epsilon_schedule(0.2, 0.01, 1, 10)
-    cpu.set_epsilon_phase(7)
+    cpu.set_epsilon_phase(7, stride)
     sh = LO.Shard(cpu, E, N, n, seed, 0, maxs, nthreads=16)
     free = np.argwhere(m == 0)
     r = np.abs(free[:, 0]) + np.abs(free[:, 1] - 6) <= 4
@@ -842,3 +915,165 @@ def test_batched_actor_curriculum_mid_density_at_bench_envs():
         ok += abs(dev) <= 3.0
         assert rel <= 0.015, rows
     assert ok >= 5, rows
+
+
+def _per_n_run(tmp, world=1, rank=0, envs=16, sync=None):
+    """A small run of the config-4 driver (ffm_amd.train.run_per_n, run_actor_only_training.py's
+    loop) on a 12x12 room: two N patterns, 40 episodes each, trajectories every 10th."""
+    from ffm_amd import train as T
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    d = T.driver_settings("actor_only")
+    E = envs // world
+    L = _learner(m, s, "actor_only", n_envs=E, n_agents=8, params=d["params"], seed=11, max_steps=30,
+                 env_base=rank * E)
+    g = T._Group(sync(L) if sync else None)
+    res = T.run_per_n(L, [4, 8], 40, d["eps"], tmp, trajectory_every=10, group=g, verbose=False, params=d["params"],
+                      global_envs=envs)
+    L.close()
+    return res
+
+
+def test_per_n_driver_writes_reference_outputs(tmp_path):
+    """run_actor_only_training.py's outputs from the batched driver: per-N H snapshots, the
+    final V / H pickles, training_results.pkl with every episode numbered 1..total in
+    order, the one linear epsilon over all episodes (:190-196), trajectories of every 10th
+    pattern episode."""
+    import pickle
+    out = str(tmp_path / "run")
+    res = _per_n_run(out)
+    total = 80
+    for f in ("H_actor_N4_total40ep.pkl", "H_actor_N8_total40ep.pkl", f"V_updated_total{total}ep.pkl",
+              f"H_actor_total{total}ep.pkl", "training_results.pkl", "summary.txt"):
+        assert os.path.exists(os.path.join(out, f)), f
+    with open(os.path.join(out, "training_results.pkl"), "rb") as f:
+        r = pickle.load(f)      # written by the test's own run
+    eps = [e["episode_num"] for e in r["all_episodes"]]
+    assert eps == list(range(1, total + 1))
+    for e in r["all_episodes"]:
+        want = float(np.clip(0.2 + (0.01 - 0.2) * ((e["episode_num"] - 1) / (total - 1)), 0.0, 1.0))
+        assert e["epsilon"] == want
+        assert 1 <= e["steps"] <= 30
+    assert [p["N"] for p in r["results_by_n"]] == [4, 8]
+    with open(os.path.join(out, f"H_actor_total{total}ep.pkl"), "rb") as f:
+        H = pickle.load(f)
+    assert len(H) == r["final_h_states"] > 0 and all(len(v) == 5 for v in H.values())
+    traj = sorted(os.listdir(os.path.join(out, "trajectories")))
+    assert len(traj) == 8 and traj[0].startswith("trajectory_N4_ep00010_total00010")
+    assert res["model_params"]["gamma"] == 0.95
+
+
+def _per_n_worker(rank, world, port, out, res_path):
+    import pickle
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ffm_amd.dist import TableSync
+        res = _per_n_run(out, world, rank, sync=lambda L: TableSync(L, device="cuda", capacity=None))
+        if rank == 0:
+            with open(res_path, "wb") as f:
+                pickle.dump(res, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_per_n_driver_sharded_gloo_world2_equals_single(tmp_path):
+    """The config-4 driver sharded over two ranks on one GPU (gloo; TableSync exchanges the
+    hashed tables' records; global env ids): the per-episode results and the H / V pickles
+    equal a single process stepping the same 16 global envs, bit for bit."""
+    import pickle
+    import socket
+    import torch.multiprocessing as mp
+    one = _per_n_run(str(tmp_path / "one"))
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    res_path = str(tmp_path / "two.pkl")
+    mp.spawn(_per_n_worker, args=(2, port, str(tmp_path / "two"), res_path), nprocs=2, join=True)
+    with open(res_path, "rb") as f:
+        two = pickle.load(f)
+    strip = lambda rows: [(e["episode_num"], e["N"], e["steps"], e["emptied"], e["epsilon"]) for e in rows]
+    assert strip(one["all_episodes"]) == strip(two["all_episodes"])
+    for name in ("H_actor_N4_total40ep.pkl", "H_actor_N8_total40ep.pkl", "V_updated_total80ep.pkl",
+                 "H_actor_total80ep.pkl"):
+        with open(tmp_path / "one" / name, "rb") as f:
+            a = pickle.load(f)
+        with open(tmp_path / "two" / name, "rb") as f:
+            b = pickle.load(f)
+        assert a.keys() == b.keys(), name
+        for k in a:
+            assert np.array_equal(np.asarray(a[k], np.float64).view(np.uint64),
+                                  np.asarray(b[k], np.float64).view(np.uint64)), name
+
+
+def _owner_sync_worker(rank, world, port, sizes, mode, T, out_path):
+    import pickle
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ffm_amd.data import make_room, l1_sff
+        from ffm_amd.dist import TableSync
+        m = make_room(64, 64)
+        s = l1_sff(m)
+        base = int(sum(sizes[:rank]))
+        L = _learner(m, s, "unified", n_envs=sizes[rank], n_agents=600, mode=mode,
+                     params={"epsilon": 0.1, "block_size": 1}, rng="philox", seed=8, auto_reset=True, max_steps=20,
+                     env_base=base)
+        L.reset()
+        sync = TableSync(L, device="cuda")
+        assert sync.tiled and sync.owner
+        sync.step(T)
+        torch.cuda.synchronize()
+        st = L.get_state()
+        tabs = {w: L.export_table(w) for w in (("V", "H") if L.actor else ("V",))}
+        parts = [None] * world
+        dist.all_gather_object(parts, (st[1], st[2], tabs, sync.received_bytes, sync.exchanges))
+        if rank == 0:
+            with open(out_path, "wb") as f:
+                pickle.dump(parts, f)
+        L.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["actor_only", "critic_only"])
+def test_gloo_world2_owner_table_sync_equals_one_learner(mode, tmp_path):
+    """TableSync's owner-sharded exchange over a real process group (two ranks on one GPU,
+    gloo; all-to-all of the packed records, all-gathers of new slots, V values, H increments
+    and tile summaries; shards of 9 and 7 envs): both ranks end with the tables of one
+    learner stepping all 16 envs, and the env states agree, bit for bit."""
+    import pickle
+    import socket
+    import torch.multiprocessing as mp
+    from ffm_amd.data import make_room, l1_sff
+    sizes, T = [9, 7], 25
+    m = make_room(64, 64)
+    s = l1_sff(m)
+    one = _learner(m, s, "unified", n_envs=16, n_agents=600, mode=mode, params={"epsilon": 0.1, "block_size": 1},
+                   rng="philox", seed=8, auto_reset=True, max_steps=20)
+    one.reset()
+    one.step(T)
+    _, oc, od = one.get_state()
+    otabs = {w: one.export_table(w) for w in (("V", "H") if one.actor else ("V",))}
+    one.close()
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    out = str(tmp_path / "owner.pkl")
+    mp.spawn(_owner_sync_worker, args=(2, port, sizes, mode, T, out), nprocs=2, join=True)
+    with open(out, "rb") as f:
+        parts = pickle.load(f)
+    assert np.array_equal(oc, np.concatenate([p[0] for p in parts]))
+    assert np.array_equal(od.view(np.uint32), np.concatenate([p[1] for p in parts]).view(np.uint32))
+    for p in parts:
+        assert p[3] > 0 and p[4] == T
+        for w, (k0, v0) in otabs.items():
+            k, v = p[2][w]
+            o0, o = np.argsort(k0), np.argsort(k)
+            assert np.array_equal(k[o], k0[o0]), w
+            assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), w

@@ -45,9 +45,16 @@ def main():
     step_coupled(shards, a.steps, **kw)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    print(json.dumps({"shards": a.shards, "envs_per_shard": a.envs, "steps": a.steps, "owner": a.owner,
-                      "ms_per_coupled_step": 1e3 * el / a.steps,
-                      "V": shards[0].table_size("V"), "H": shards[0].table_size("H")}), flush=True)
+    out = {"shards": a.shards, "envs_per_shard": a.envs, "steps": a.steps, "owner": a.owner,
+           "ms_per_coupled_step": 1e3 * el / a.steps,
+           "V": shards[0].table_size("V"), "H": shards[0].table_size("H")}
+    if a.owner:     # the last step's exchange volumes per shard (records in, V values out, H increments out)
+        b = [L.owner_buffers() for L in shards]
+        out["records_out"] = [int(x["counts"][: a.shards].sum()) for x in b]
+        out["v_values_out"] = [int(x["out_counts"][0]) for x in b]
+        out["h_increments_out"] = [int(x["out_counts"][1]) for x in b]
+        out["new_v_slots"] = [int(x["counts"][a.shards]) for x in b]
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
