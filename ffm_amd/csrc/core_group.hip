@@ -71,8 +71,10 @@ __host__ __device__ inline GroupCarve group_carve(int PHW, int TS, int F) {
     return c;
 }
 
+// Block-shared: the map (u8), the staged SFF term (f32), the free-cell list (u16) and
+// the map widened to the grid's u16 codes (each wave's grids are copied from it).
 __host__ __device__ inline size_t group_shared_bytes(int PHW, int F) {
-    return a16((size_t)PHW) + a16((size_t)PHW * 4) + a16((size_t)(F > 0 ? F : 1) * 2);
+    return a16((size_t)PHW) + a16((size_t)PHW * 4) + a16((size_t)(F > 0 ? F : 1) * 2) + a16((size_t)PHW * 2);
 }
 
 // Packed per-chunk state (one VGPR each):
@@ -91,6 +93,10 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 #define FFM_GROUP_ABLATE 0   // diagnostic builds only
 #endif
 
+#ifndef FFM_GROUP_TAIL
+#define FFM_GROUP_TAIL 1    // the stencil's partial last slot, one cell per lane
+#endif
+
 #ifndef FFM_GROUP_WAVES
 #define FFM_GROUP_WAVES 1   // minimum waves per SIMD asked of the register allocator
 #endif
@@ -103,7 +109,12 @@ void core_group_kernel(CoreStepArgs a) {
     constexpr int TS = lane_tile_floats(H, W);
     constexpr int Q4 = HW / 4;                 // float4s per env
     constexpr int Q = G * Q4;                  // float4s per group
-    constexpr int NS = (Q + 63) / 64;          // float4 slots per lane
+    constexpr int NS = (Q + 63) / 64;          // float4 slots per lane (staging)
+    constexpr int NSF = Q / 64;                // full float4 slots
+    // a partial last slot of at most 16 float4s is stepped as one cell per lane instead
+    // (G = 4 at 12x12: 144 float4s = 2 full slots + 64 cells), so its stencil keeps every
+    // lane busy (Neumann only: the Moore stencil keeps the float4 form)
+    constexpr bool SCALAR_TAIL = NB == 4 && FFM_GROUP_TAIL && Q % 64 != 0 && (Q % 64) * 4 == 64;
     constexpr int MAXC = (G * 32 + 63) / 64;   // agent chunks per group (A <= 32)
     constexpr int PWORDS = G * 16;             // position dwords per group (A <= 32)
     static_assert(G >= 1 && G <= 8 && HW % 4 == 0 && H + 1 < 128, "group geometry");
@@ -115,6 +126,8 @@ void core_group_kernel(CoreStepArgs a) {
     uint8_t* pmap = smem;
     float* psff = reinterpret_cast<float*>(smem + a16((size_t)PHW));
     uint16_t* pfree = reinterpret_cast<uint16_t*>(smem + a16((size_t)PHW) + a16((size_t)PHW * 4));
+    uint16_t* pmap16 = reinterpret_cast<uint16_t*>(smem + a16((size_t)PHW) + a16((size_t)PHW * 4) +
+                                                   a16((size_t)(a.F > 0 ? a.F : 1) * 2));
     unsigned char* wbase = smem + group_shared_bytes(PHW, a.F) + (size_t)wv * cv.per_wave;
     uint16_t* const grid = reinterpret_cast<uint16_t*>(wbase + cv.grid);
     float* const tile = reinterpret_cast<float*>(wbase + cv.tile);
@@ -171,17 +184,25 @@ void core_group_kernel(CoreStepArgs a) {
     load(g < ngroups ? g : -1, cur);
 
     for (int i = threadIdx.x; i < PHW; i += 256) {
-        pmap[i] = a.pmap[i];
+        const uint8_t mv = a.pmap[i];
+        pmap[i] = mv;
+        pmap16[i] = mv;
         psff[i] = a.kS32 * reinterpret_cast<const float*>(a.psff)[i];   // the score's SFF term
     }
     for (int i = threadIdx.x; i < a.F; i += 256) pfree[i] = a.free_padded[i];
-    for (int i = lane; i < G * TS; i += 64) tile[i] = 0.0f;
+    static_assert((G * TS) % 4 == 0 && PHW % 2 == 0, "16-B tile clears, 4-B grid copies");
+    for (int i = lane; i < G * TS / 4; i += 64) reinterpret_cast<float4*>(tile)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (lane < kGroupPendWords) pend[lane] = 0u;
     __syncthreads();
-    for (int i = lane; i < G * PHW; i += 64) grid[i] = pmap[i % PHW];
+    // every env's grid starts as the map: dword copies of the widened map, no per-cell modulo
+#pragma unroll
+    for (int s = 0; s < G; s++)
+        for (int i = lane; i < PHW / 2; i += 64)
+            reinterpret_cast<uint32_t*>(grid)[s * (PHW / 2) + i] = reinterpret_cast<const uint32_t*>(pmap16)[i];
     wave_sync();
 
     unsigned c_steps = 0, c_exits = 0, c_resets = 0;
+    const bool kd1 = a.kD32 == 1.0f;          // k_D * DFF == DFF (wave-uniform)
     constexpr uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W, c < 2^16
     const int g_first = g;
     for (int iter = 0; g < ngroups; g += wstride, iter++) {
@@ -244,7 +265,8 @@ void core_group_kernel(CoreStepArgs a) {
                 const float* dk = tile + s * TS;
                 const int dd0 = 3 - 2 * cs_xp1(v);
                 bool to_exit = false;
-                uint32_t slot = lane_decide<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
+                uint32_t slot = kd1 ? lane_decide<NB, true, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit)
+                                    : lane_decide<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
                 slot = live ? slot : kNoReq;
                 if (slot == kPending)   // u near a cdf boundary: the exact NumPy arithmetic decides
                     slot = NB == 4 ? lane_decide_exact<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32,
@@ -370,8 +392,25 @@ void core_group_kernel(CoreStepArgs a) {
         // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb],
         // then the DFF stores (an env reset this step starts its next episode at zero) ----
         const __amdgpu_buffer_rsrc_t rd = pair_rsrc(a.dff + e0 * HW, nenv * HW * 4);
+        if (SCALAR_TAIL) {     // the last, partial float4 slot as one cell per lane (all lanes busy)
+            const int q = 4 * 64 * NSF + lane;                 // the group's cell
+            const int s = q / HW, c = q - s * HW, y = c % W;
+            const float* p = tile + s * TS + 4 + W + c;
+            const float m0 = p[0], mu = p[-W], md = p[W];
+            const float ml = y == 0 ? 0.0f : p[-1], mr = y == W - 1 ? 0.0f : p[1];
+            // B = c0 * D per operand, then A = B + sum c1 * B[nb] in neighbour order (:106-117)
+            const float b0 = a.c0 * m0, bu = a.c0 * mu, bd = a.c0 * md, bl = a.c0 * ml, br = a.c0 * mr;
+            float acc = b0;
+            acc = acc + a.c1 * bu;
+            acc = acc + a.c1 * bd;
+            acc = acc + a.c1 * bl;
+            acc = acc + a.c1 * br;
+            const bool z = ((rsm >> s) & 1ull) != 0ull;
+            const float o = z || acc < 1e-4f ? 0.0f : acc;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rd, q * 4, 0, 0);
+        }
 #pragma unroll
-        for (int k = 0; k < NS; k++) {
+        for (int k = 0; k < (SCALAR_TAIL ? NSF : NS); k++) {
             const int tb = toff[k];
             if (tb < 0) continue;
             const bool yl = ((yfl >> (2 * k)) & 1u) != 0u, yr = ((yfl >> (2 * k)) & 2u) != 0u;

@@ -87,21 +87,56 @@ __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, c
 // kPending when u lies within the margin of a cdf boundary.  The fast path compares
 // a float32 copy of u (|error| < 2^-24) inside fast_choice's 1e-4 margin; selects
 // only, no branch.
-template <int NB, bool PRE = false>
+//   * An invalid candidate's score is masked to -inf before the max and the exp, so
+//     its term is exactly 0 and its cum equals the previous one: the lowest slot with
+//     cum >= t - d is then valid, or slot 0 invalid with u <= the margin, which the
+//     acceptance test (cum > t + d) sends to the exact pass -- the same decisions as
+//     masking every step separately, in 7 instead of 11 VALU per candidate.
+//   * KD1 (k_D == 1, the drivers' setting): k_D * DFF is DFF itself (an exact product).
+template <int NB, bool PRE = false, bool KD1 = false>
 __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
                                                 const float* dk, int dd0, float kS, float kD, uint32_t wx,
                                                 bool& to_exit) {
+    int cell[NB + 1], dcell[NB + 1];
+    uint32_t g[NB];
+    float sf[NB + 1], df[NB + 1];
+#pragma unroll
+    for (int s = 0; s < NB; s++) {
+        cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
+        dcell[s] = cell[s] + dd0 - nb_dx<NB>(s) * 2;   // the tile row is 2 shorter than the grid row
+        g[s] = gk[cell[s]];
+    }
+    cell[NB] = pp;
+    dcell[NB] = pp + dd0;
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        sf[k] = psff[cell[k]];
+        df[k] = dk[dcell[k]];
+    }
     bool v[NB + 1];
-    float xs[NB + 1];
-    int exit_slot;
-    const int nvalid = lane_scores<NB, PRE>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
+    v[NB] = true;
+    int nvalid = 0, exit_slot = -1;
+#pragma unroll
+    for (int s = NB - 1; s >= 0; s--) {
+        v[s] = g[s] == 0u || g[s] == 3u;                                 // :52-60
+        nvalid += v[s] ? 1 : 0;
+        exit_slot = g[s] == 3u ? s : exit_slot;                          // :66-72
+    }
+    float scm[NB + 1];
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int k = 0; k <= NB; k++) {
+        const float a = PRE ? sf[k] : kS * sf[k];
+        const float b = KD1 ? df[k] : kD * df[k];
+        scm[k] = v[k] ? a + b : -__builtin_inff();                       // :77
+        mx = __builtin_fmaxf(mx, scm[k]);                                // :78
+    }
     float cum[NB + 1];
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k <= NB; k++) {
-        const float e = __builtin_amdgcn_exp2f(xs[k] * 1.44269504088896341f);
-        acc += v[k] ? e : 0.0f;
-        cum[k] = v[k] ? acc : -1.0f;
+        acc += __builtin_amdgcn_exp2f((scm[k] - mx) * 1.44269504088896341f);
+        cum[k] = acc;
     }
     const float uf = (float)(wx >> 8) * 0x1p-24f;
     const float t = uf * acc;

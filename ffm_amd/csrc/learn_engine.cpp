@@ -99,7 +99,9 @@ struct ffm_learner {
     int* d_tdirty = nullptr;
     int* d_tcand = nullptr;
     // tile-major records and the owner-sharded exchange
-    bool tile_major = true;                  // FFM_TILE_MAJOR=0: the env-major tile passes
+    bool tile_major = true;                  // owner exchange available (FFM_TILE_MAJOR=0: off)
+    bool single_tm = false;                  // one device: tile-major passes too (FFM_TILE_MAJOR=1; env-major
+                                             // is faster there: the pack costs more than the passes save)
     int ow = 1, orank = 0, ths = 0;          // ranks, this rank, header row stride
     uint32_t* d_pe = nullptr;                // [E][NT] records of tile t in envs before e
     uint32_t* d_ttot = nullptr;              // [NT] records of the tiles before t in its ownership chunk
@@ -427,6 +429,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         l->NT = (HW + ffm::kTileCells - 1) / ffm::kTileCells;
         const char* tm = getenv("FFM_TILE_MAJOR");
         l->tile_major = !(tm && tm[0] == '0');
+        l->single_tm = tm && tm[0] == '1';
         l->ths = l->NT + 1;
         if (hipMalloc((void**)&l->d_trecs, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
             hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 2) != hipSuccess ||
@@ -596,7 +599,7 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             ffm::LearnArgs a = make_args(l);
             a.trecs = l->d_trecs;
             HIP_TRY(ffm::launch_learn_batch(a, s));
-            if (l->tile_major) {     // records reordered tile-major, then the passes
+            if (l->single_tm) {      // records reordered tile-major, then the passes
                 a.ow = 1;
                 a.orank = 0;
                 a.ochunk = ffm::kOwnChunk;

@@ -878,8 +878,9 @@ class Learner:
     # -- the owner-sharded tiled step -----------------------------------------
     @property
     def tile_major(self) -> bool:
-        """Tiled learners reorder their records tile-major unless FFM_TILE_MAJOR=0 (A/B)."""
-        return self.tiled and os.environ.get("FFM_TILE_MAJOR", "1") != "0"
+        """Tiled learners can reorder their records tile-major (the owner-sharded exchange)
+        unless FFM_TILE_MAJOR=0; one device steps tile-major only with FFM_TILE_MAJOR=1."""
+        return self.tiled and os.environ.get("FFM_TILE_MAJOR", "") != "0"
 
     def set_tile_owners(self, world: int, rank: int):
         """Deal the tiles of cells over `world` ranks; this learner owns rank `rank`'s."""

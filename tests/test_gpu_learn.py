@@ -387,7 +387,7 @@ def test_learner_tile_major_equals_env_major(monkeypatch):
               max_steps=25)
     out = []
     for tm in ("1", "0"):
-        monkeypatch.setenv("FFM_TILE_MAJOR", tm)
+        monkeypatch.setenv("FFM_TILE_MAJOR", tm)   # 1: tile-major on one device too; 0: env-major only
         L = _learner(m, s, "unified", n_envs=700, n_agents=300, **kw)
         assert L.tile_major == (tm == "1")
         L.reset()
