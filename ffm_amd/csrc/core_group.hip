@@ -101,7 +101,7 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 #define FFM_GROUP_WAVES 1   // minimum waves per SIMD asked of the register allocator
 #endif
 
-template <int NB, int HT, int WT, int G>
+template <int NB, int HT, int WT, int G, bool KD1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FFM_GROUP_WAVES, 8)))
 void core_group_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -202,7 +202,6 @@ void core_group_kernel(CoreStepArgs a) {
     wave_sync();
 
     unsigned c_steps = 0, c_exits = 0, c_resets = 0;
-    const bool kd1 = a.kD32 == 1.0f;          // k_D * DFF == DFF (wave-uniform)
     constexpr uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W, c < 2^16
     const int g_first = g;
     for (int iter = 0; g < ngroups; g += wstride, iter++) {
@@ -265,8 +264,7 @@ void core_group_kernel(CoreStepArgs a) {
                 const float* dk = tile + s * TS;
                 const int dd0 = 3 - 2 * cs_xp1(v);
                 bool to_exit = false;
-                uint32_t slot = kd1 ? lane_decide<NB, true, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit)
-                                    : lane_decide<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
+                uint32_t slot = lane_decide<NB, true, KD1>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb.x, to_exit);
                 slot = live ? slot : kNoReq;
                 if (slot == kPending)   // u near a cdf boundary: the exact NumPy arithmetic decides
                     slot = NB == 4 ? lane_decide_exact<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32,
@@ -483,30 +481,37 @@ int core_group_envs() { return kGroupG; }
 
 int core_group_max_iters() { return kGroupMaxIters; }
 
-template <int NB>
+// KD1: k_D == 1 (the drivers' setting), where k_D * DFF is DFF itself: a kernel of its own
+// rather than a runtime flag, which the register allocator would keep (and spill) all launch.
+template <int NB, bool KD1>
 static hipError_t group_op(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
     const size_t smem = core_group_smem_bytes(a.H, a.W, a.F, 4);
     if (op) {
         *occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, core_group_kernel<NB, 12, 12, kGroupG>, 256, smem) !=
-            hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, core_group_kernel<NB, 12, 12, kGroupG, KD1>, 256,
+                                                         smem) != hipSuccess)
             *occ = 0;
         return hipSuccess;
     }
     const long long groups = (a.E + kGroupG - 1) / kGroupG;
     if (a.H != 12 || a.W != 12 || a.A > 32 || (groups + (long long)blocks * 4 - 1) / ((long long)blocks * 4) > kGroupMaxIters)
         return hipErrorInvalidConfiguration;   // shapes the kernel and its grid assume
-    core_group_kernel<NB, 12, 12, kGroupG><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
+    core_group_kernel<NB, 12, 12, kGroupG, KD1><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
     return hipGetLastError();
 }
 
+template <int NB>
+static hipError_t group_op_kd(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
+    return a.kD32 == 1.0f ? group_op<NB, true>(a, blocks, s, op, occ) : group_op<NB, false>(a, blocks, s, op, occ);
+}
+
 hipError_t launch_core_group(const CoreStepArgs& a, int nb, int blocks, hipStream_t s) {
-    return nb == 4 ? group_op<4>(a, blocks, s, 0, nullptr) : group_op<8>(a, blocks, s, 0, nullptr);
+    return nb == 4 ? group_op_kd<4>(a, blocks, s, 0, nullptr) : group_op_kd<8>(a, blocks, s, 0, nullptr);
 }
 
 int core_group_blocks_per_cu(const CoreStepArgs& a, int nb) {
     int n = 0;
-    (void)(nb == 4 ? group_op<4>(a, 0, nullptr, 1, &n) : group_op<8>(a, 0, nullptr, 1, &n));
+    (void)(nb == 4 ? group_op_kd<4>(a, 0, nullptr, 1, &n) : group_op_kd<8>(a, 0, nullptr, 1, &n));
     return n;
 }
 
