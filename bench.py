@@ -189,6 +189,15 @@ def main():
                 tj = json.load(f)
             if tj.get("config") == f"{H}x{W}_A{A}_E{E}":
                 traffic = tj.get("hbm_bytes_per_launch")
+        # the step kernel's VALU issue fraction (its real bound at 12x12) from a committed
+        # PMC summary (tools/pmc.sh + tools/valu_json.py)
+        valu = None
+        vpath = os.path.join(ROOT, "profiles", f"valu_{H}x{W}_A{A}_E{E}.json")
+        if os.path.exists(vpath):
+            with open(vpath) as f:
+                vj = json.load(f)
+            if vj.get("config") == f"{H}x{W}_A{A}_E{E}":
+                valu = vj
         out = {
             "metric": METRIC,
             "value": agent_steps / elapsed,
@@ -226,6 +235,8 @@ def main():
                 "bytes_per_launch_algorithmic": E * bytes_per_env_step,
                 "achievable_copy_GBs": copy_gbs,
                 "frac_of_copy": achieved / copy_gbs if copy_gbs else None,
+                **({"valu_issue_frac": valu["valu_issue_frac"], "valu_per_wave": valu["valu_per_wave"],
+                    "valu_source": f"profiles/valu_{H}x{W}_A{A}_E{E}.json ({valu['formula']})"} if valu else {}),
             },
             "cpu_baseline": None,
             "multi_step": multi,
@@ -427,9 +438,11 @@ def cpu_baseline_learner(args, cfg, m, s):
     from ffm_amd.engine import Learner
     H, W = m.shape
     A = args.agents
-    E = min(args.cpu_envs, 1024) if args.config == 4 else 2
     share, host = cpu_share()
     threads = args.cpu_threads or share
+    # the OpenMP loop runs over envs: C5 steps as many envs as threads (8,192 agents each),
+    # so every reported core has an env of its own
+    E = min(args.cpu_envs, 1024) if args.config == 4 else max(2, threads)
     cpu = LO.Learn(m, s, cfg["variant"], cfg["mode"], cfg["params"], log2_cap=22 if args.config == 4 else 24)
     core = O.Core(m, s, {"neighborhood": "neumann"})
     pos = np.full((E, A), 0xFFFF, np.uint16)
@@ -466,7 +479,7 @@ def cpu_baseline_learner(args, cfg, m, s):
     tab_ok = {k: bool(same_table(*v)) for k, v in tables.items()}
     ok = state_ok and all(tab_ok.values())
     return {
-        "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+        "value": total / elapsed, "unit": "agent-steps/s", "cores": min(threads, E), "kind": "port",
         "sample": (f"oracle/ffm_learn_oracle.c batched Philox mode, {E} envs x {t - 1} steps of the same "
                    f"workload (OpenMP {threads} threads, {host['cpu_model']}); positions, counts, DFF and "
                    f"tables {'/'.join(tables)} bit-exact vs GPU: {ok}"),
@@ -570,7 +583,7 @@ def cpu_baseline(args, m, s, params, snap, single_steps):
     ok = bool(np.array_equal(gc, cnt) and np.array_equal(gd.view(np.uint32), dff.view(np.uint32))
               and all(np.array_equal(gp[e, :gc[e]], pos[e, :gc[e]]) for e in range(E)))
     return {
-        "value": total / elapsed, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+        "value": total / elapsed, "unit": "agent-steps/s", "cores": min(threads, E), "kind": "port",
         "sample": (f"oracle/ffm_oracle.c Philox mode, {E} envs x {steps} steps of the same workload "
                    + (f"(the last {steps} of a {single_steps}-step replay) " if full else "")
                    + f"(OpenMP {threads} threads, {host['cpu_model']}); {what} bit-exact vs the oracle: {ok}"),

@@ -424,6 +424,19 @@ def test_learner_philox_config5_through_truncation():
     assert (eps == 1).all(), "every env truncates once at max_steps = 300"
 
 
+@pytest.mark.timeout(900)
+def test_learner_philox_config4_bench_workload_matches_cpu():
+    """The bench's config-4 workload itself (bench.LEARN_CONFIGS[4]: run_actor_only_training.py's
+    MODEL_PARAMS -- gamma 0.95, alpha_v 0.1, step_penalty 0, epsilon 0.2 -- max_steps 1000,
+    12x12, 32 agents) on 4,096 envs for 300 steps: positions, counts, episode ends, DFF bits
+    and the V / H tables equal the CPU restatement bit for bit."""
+    import bench
+    cfg = bench.LEARN_CONFIGS[4]
+    counts, eps = _philox_compare(cfg["variant"], cfg["mode"], cfg["params"], 12, 12, 32, 4096, 300,
+                                  max_steps=cfg["max_steps"], seed=42, log2_cap=22, chunks=10)
+    assert eps.sum() > 4096, "most envs have emptied and restarted"
+
+
 def test_learner_table_import_export_roundtrip():
     from ffm_amd.data import make_room, l1_sff
     from ffm_amd import learn_keys as K
