@@ -293,11 +293,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
     if ((long long)d.H * d.W == 65536 && (d.map[65535] == 0 || d.map[65535] == 3))
         return fail(FFM_E_UNSUPPORTED, "the last cell of a 65536-cell map must be blocked");
-    if (d.neighborhood != 4 &&
-        !(d.neighborhood == 8 && d.variant != FFM_VARIANT_TRAINED && d.rng_mode == FFM_RNG_MT))
-        return fail(FFM_E_UNSUPPORTED, "neighborhood 'moore' is built for the reference-exact (MT) step of ffm_ac_core, "
-                                       "ffm_unified and ffm_actor_only; the batched step and ffm_trained_core use "
-                                       "'neumann'");
+    if (d.neighborhood != 4 && !(d.neighborhood == 8 && d.rng_mode == FFM_RNG_MT))
+        return fail(FFM_E_UNSUPPORTED, "neighborhood 'moore' is built for the reference-exact (MT) step of every "
+                                       "learning variant; the batched step uses 'neumann'");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
     // batched: LDS grid codes hold 14-bit agent indices (<= 16383 agents); the exact (MT) step

@@ -899,6 +899,50 @@ __device__ __forceinline__ void trained_policy(const LearnArgs& a, int hslot, co
     finish_cdf(P, p);
 }
 
+// The same for the Moore neighbourhood (MT step only): nine moves in get_neighbors order
+// then stay (:76-85), a nine-value H row (:228-236; zeros when missing), NumPy's pairwise
+// add.reduce of the nine terms, np.random.choice over nine (cumsum, cdf /= cdf[-1],
+// searchsorted).  Same arithmetic as the oracle's trained_choose(NA = 9).
+template <class R>
+__device__ int trained_choose_n(const LearnArgs& a, int hslot, const int* coord, const int* valid, const float* dff,
+                                const HStat& hs, int NA, R& rng) {
+    float h[9], score[9], e[9];
+    double p[9];
+    for (int k = 0; k < NA; k++) h[k] = hslot >= 0 ? (float)tval(a.Ht, hslot)[k] : 0.0f;
+    if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
+        const float hmax = (float)hs.mx, den = (float)(hs.mx - hs.mn);
+        const float srange = (float)((double)a.smax - (double)a.smin), smin = a.smin;
+        for (int k = 0; k < NA; k++) {
+            const float q = (hmax - h[k]) / den;
+            const float d = q * srange;
+            h[k] = d + smin;
+        }
+    }
+    const float nkA = (float)a.nkA;
+    bool bad = false;
+    int nvalid = 0;
+    for (int k = 0; k < NA; k++) {
+        const float x = nkA * h[k];
+        const float y = a.kD32 * dff[coord[k]];
+        score[k] = x + y;
+        bad = bad || !__builtin_isfinite(score[k]);
+        nvalid += valid[k];
+    }
+    if (bad)
+        for (int k = 0; k < NA; k++) score[k] = valid[k] ? 1.0f : 0.0f;
+    float mx = score[0];
+    for (int k = 1; k < NA; k++) mx = score[k] > mx ? score[k] : mx;
+    for (int k = 0; k < NA; k++) e[k] = valid[k] ? np_expf(score[k] - mx) : 0.0f;
+    const float sum = np_sum_n(e, NA);
+    if (__builtin_isfinite(sum) && sum > 0) {
+        for (int k = 0; k < NA; k++) p[k] = (double)(e[k] / sum);
+    } else {
+        const float u = (float)(1.0 / (double)nvalid);
+        for (int k = 0; k < NA; k++) p[k] = valid[k] ? (double)u : 0.0;
+    }
+    return choice_cdf(p, NA, rng.u());
+}
+
 struct ExactScratch {
     int *occ, *rq_tgt, *rq_agent, *list, *nxt, *coll, *act, *avalid, *wexit;
     uint8_t *sm, *smn, *done;
@@ -979,7 +1023,9 @@ __global__ __launch_bounds__(64) void learn_exact_kernel(LearnArgs a) {
                 int k = -1;
                 for (int j = 0; j < nb; j++)
                     if (inb[j] && a.map[coord[j]] == 3) { k = j; break; }
-                if (k < 0) {
+                if (k < 0 && nb == 8) {
+                    k = trained_choose_n(a, tab_find(a.Ht, S.skey[i]), coord, valid, dff, hs, NA, rng);
+                } else if (k < 0) {
                     Policy P;
                     trained_policy(a, tab_find(a.Ht, S.skey[i]), coord, valid, dff, hs, P);
                     const double u = rng.u();

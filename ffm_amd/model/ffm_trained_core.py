@@ -3,9 +3,9 @@ evacuation driven by a trained actor (the H table of an ffm_unified run), steppe
 on the MI355X (see ``_learn_model``).  Nothing is learned; the table is read only.
 
 The trained table is a pickle whose keys are ``pickle.dumps(((r_U, r_D, r_L, r_R),
-(bx, by)))`` bytes and whose values are lists of five action preferences
-(model/ffm_trained_core.py:51-68); ``H`` exposes it re-keyed by tuples of ints,
-as the reference does.
+(bx, by)))`` bytes and whose values are lists of action preferences, one per move
+(five, or nine with the Moore neighbourhood: model/ffm_trained_core.py:51-68, 76-85,
+228-236); ``H`` exposes it re-keyed by tuples of ints, as the reference does.
 """
 from __future__ import annotations
 
@@ -44,9 +44,14 @@ class FloorFieldModel(LearnModel):
             ranks = tuple(int(r) for r in original[0])
             block = (int(original[1][0]), int(original[1][1]))
             self.H[(ranks, block)] = v
-        rows = [(K.from_rank_tuple(k), v) for k, v in self.H.items() if isinstance(v, list) and len(v) == 5]
+        # one preference per move: the neighbours then stay, 5 (neumann) or 9 (moore, :76-85);
+        # the reference reads a row of another length as zeros but still counts its values in
+        # the table's min / max (:228-267), which this table layout cannot hold
+        width = len(self.neighbors) + 1
+        rows = [(K.from_rank_tuple(k), v) for k, v in self.H.items() if isinstance(v, list) and len(v) == width]
         if len(rows) != len(self.H):
-            raise NotImplementedError("trained H rows must be lists of five preferences")
+            raise NotImplementedError(f"trained H rows must be lists of {width} preferences "
+                                      f"({self.params['neighborhood']} neighbourhood)")
         if rows:
             self._learner.import_table("H", np.array([k for k, _ in rows], np.uint64),
                                        np.array([[float(x) for x in v] for _, v in rows], np.float64))

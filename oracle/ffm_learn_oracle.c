@@ -525,15 +525,17 @@ static int critic_choose(lctx* L, const int32_t* coord, const int* valid, const 
  * table in float32 (NEP 50: Python floats are weak next to the f32 array,
  * :242-267), score -k_A*h + k_D*dff in float32, NumPy's float32 exp, the masked
  * sum and divide, uniform fallbacks (:270-296), then np.random.choice. */
-static int trained_choose(lctx* L, int64_t hslot, const int32_t* coord, const int* valid, const float* dff) {
+static int trained_choose(lctx* L, int64_t hslot, const int32_t* coord, const int* valid, const float* dff,
+                          int NA) {
     const ffo_learn_cfg* c = L->c;
-    float h[5], score[5], e[5];
-    double p[5];
-    for (int k = 0; k < 5; k++) h[k] = hslot >= 0 ? (float)L->Ht->vals[hslot * 5 + k] : 0.0f;
+    float h[9], score[9], e[9];
+    double p[9];
+    /* NA = 5 (Neumann) or 9 (Moore, :76-85): the H row has one value per move (:228-236) */
+    for (int k = 0; k < NA; k++) h[k] = hslot >= 0 ? (float)L->Ht->vals[hslot * NA + k] : 0.0f;
     if (L->hs.has && !L->hs.nonfinite && L->hs.mx - L->hs.mn > 1e-6) {
         const float hmax = (float)L->hs.mx, den = (float)(L->hs.mx - L->hs.mn);
         const float srange = (float)((double)L->smax - (double)L->smin), smin = L->smin;
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float a = hmax - h[k];
             const float b = a / den;
             const float d = b * srange;
@@ -542,7 +544,7 @@ static int trained_choose(lctx* L, int64_t hslot, const int32_t* coord, const in
     }
     const float nkA = (float)(-c->k_A), kD = (float)c->k_D;
     int bad = 0, nvalid = 0;
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const float a = nkA * h[k];
         const float b = kD * dff[coord[k]];
         score[k] = a + b;
@@ -550,18 +552,18 @@ static int trained_choose(lctx* L, int64_t hslot, const int32_t* coord, const in
         nvalid += valid[k];
     }
     if (bad)
-        for (int k = 0; k < 5; k++) score[k] = valid[k] ? 1.0f : 0.0f;
+        for (int k = 0; k < NA; k++) score[k] = valid[k] ? 1.0f : 0.0f;
     float mx = score[0];
-    for (int k = 1; k < 5; k++) mx = score[k] > mx ? score[k] : mx;
-    for (int k = 0; k < 5; k++) e[k] = valid[k] ? ffo_np_expf(score[k] - mx) : 0.0f;
-    const float sum = ffo_np_sumf(e, 5);
+    for (int k = 1; k < NA; k++) mx = score[k] > mx ? score[k] : mx;
+    for (int k = 0; k < NA; k++) e[k] = valid[k] ? ffo_np_expf(score[k] - mx) : 0.0f;
+    const float sum = ffo_np_sumf(e, NA);                 /* pairwise from 8 terms on */
     if (isfinite(sum) && sum > 0) {
-        for (int k = 0; k < 5; k++) p[k] = (double)(e[k] / sum);
+        for (int k = 0; k < NA; k++) p[k] = (double)(e[k] / sum);
     } else {
         const float u = (float)(1.0 / (double)nvalid);
-        for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)u : 0.0;
+        for (int k = 0; k < NA; k++) p[k] = valid[k] ? (double)u : 0.0;
     }
-    return choice_cdf(p, 5, dec_u53(&L->rng));
+    return choice_cdf(p, NA, dec_u53(&L->rng));
 }
 
 /* ffm_ac_core decide = ffm_core decide (model/ffm_ac_core.py:126-199):
@@ -695,10 +697,10 @@ static int env_step(lctx* L, int32_t* pos, int32_t* n_io, float* dff, int32_t* o
         if (c->variant == FFO_VAR_TRAINED) {            /* model/ffm_trained_core.py:169-258 */
             dec_begin(&L->rng, (uint32_t)i);
             int ex = -1;
-            for (int k = 0; k < 4; k++)
+            for (int k = 0; k < nb; k++)
                 if (inb[k] && c->map[coord[k]] == 3) { ex = k; break; }
             int k = ex;
-            if (ex < 0) k = trained_choose(L, tab_find(L->Ht, skey[i]), coord, valid, dff);
+            if (ex < 0) k = trained_choose(L, tab_find(L->Ht, skey[i]), coord, valid, dff, NA);
             else wexit[i] = 1;
             rq_tgt[nrq] = coord[k]; rq_agent[nrq++] = i;
             continue;

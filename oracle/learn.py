@@ -143,7 +143,7 @@ class Learn:
         self.V = Table(1, log2_cap)
         # H rows: one value per move (neighbours + stay): 5, or 9 with the Moore neighbourhood
         moore = p.get("neighborhood", "neumann") == "moore"
-        self.n_actions = 9 if moore and variant in ("unified", "actor_only") else 5
+        self.n_actions = 9 if moore and variant in ("unified", "actor_only", "trained") else 5
         self.Ht = Table(self.n_actions, log2_cap)
         self.cfg = LearnCfg(
             self.H, self.W, self.map.ctypes.data,

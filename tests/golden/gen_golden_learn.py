@@ -134,6 +134,7 @@ def run_trained_case(name, cls, map_array, sff, params, N, seeds, n_ep, max_step
     """model/ffm_trained_core.py driven like run_trained_ffm.py:213-295: per episode
     model.N, model.positions = model.initialize_agents(), model.dff = zeros, run."""
     H, W = map_array.shape
+    width = 9 if params.get("neighborhood") == "moore" else 5
     init, nsteps, counts, cells, hashes, np_tail, py_tail = [], [], [], [], [], [], []
     with tempfile.TemporaryDirectory() as td:
         sff_path = os.path.join(td, "sff.npy")
@@ -172,10 +173,10 @@ def run_trained_case(name, cls, map_array, sff, params, N, seeds, n_ep, max_step
         nsteps=np.asarray(nsteps, np.int32), counts=np.asarray(counts, np.int16),
         cells=np.asarray(cells, np.int16), dff_hash=np.asarray(hashes, np.uint64),
         v_keys=np.zeros(0, np.uint64), v_vals=np.zeros(0, np.float64), v_n=np.zeros(len(seeds), np.int64),
-        h_keys=np.zeros(0, np.uint64), h_vals=np.zeros((0, 5), np.float64), h_n=np.zeros(len(seeds), np.int64),
+        h_keys=np.zeros(0, np.uint64), h_vals=np.zeros((0, width), np.float64), h_n=np.zeros(len(seeds), np.int64),
         np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
         pre_h_keys=np.asarray([K.from_rank_tuple(k) for k in h_table], np.uint64),
-        pre_h_vals=np.asarray([list(map(float, v)) for v in h_table.values()], np.float64).reshape(-1, 5),
+        pre_h_vals=np.asarray([list(map(float, v)) for v in h_table.values()], np.float64).reshape(-1, width),
     )
     path = os.path.join(HERE, f"learn_{name}.npz")
     np.savez_compressed(path, **out)
@@ -303,6 +304,25 @@ def main():
             run_trained_case("trained_12x12_N24", TR, m12, s12, tr_p, 24, [18, 19], 3, 300, tables[1])
         if not only or "trained_12x12_N40_bs5" in only:
             run_trained_case("trained_12x12_N40_bs5", TR, m12, s12, {}, 40, [20], 3, 300, tables[5])
+
+    # ffm_trained_core with the Moore neighbourhood (:76-85, nine-value rows :228-236), driven
+    # by the nine-value H of a Moore unified actor
+    if not only or "trained_moore_12x12_N20" in only:
+        np.random.seed(23)
+        random.seed(23)
+        with tempfile.TemporaryDirectory() as td, contextlib.redirect_stdout(io.StringIO()):
+            sp = os.path.join(td, "s.npy")
+            np.save(sp, s12)
+            ua = UNI(m12, sp, 20, learning_mode="both", params=dict(uni_p, block_size=1, neighborhood="moore"))
+            for ep in range(6):
+                ua.set_epsilon(0.2)
+                ua.reset()
+                ua.run(max_steps=200)
+            table_m = ua.get_h_table()
+        assert all(len(v) == 9 for v in table_m.values())
+        run_trained_case("trained_moore_12x12_N20", TR, m12, s12,
+                         {"k_D": 1, "k_A": 10, "neighborhood": "moore", "block_size": 1}, 20, [21, 22], 3, 300,
+                         table_m)
 
 
 if __name__ == "__main__":
