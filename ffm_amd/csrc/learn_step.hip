@@ -1251,8 +1251,8 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 // the map, SFF and DFF in LDS as well measured slower at config 4, 324 vs 295 us:
 // they are L1/L2 hits, and the staging delays every short-lived workgroup.)
 struct BatchCarve {
-    size_t dff, grid, bits, req, ws, total;  // per env
-    size_t shared;                           // per block: EPB env regions
+    size_t dff, grid, bits, req, km, ws, total;  // per env
+    size_t shared;                               // per block: EPB env regions
 };
 // DL: the env's DFF is staged in LDS (small maps): the policy's reads, the
 // deposits and the stencil stay on chip; only the stencil's output goes to HBM.
@@ -1263,6 +1263,7 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB,
     c.grid = o; o += align16((size_t)HW * 2);
     c.bits = o; o += align16((size_t)((HW + 31) / 32) * 4);
     c.req = o; o += align16((size_t)A * D * 2);
+    c.km = o; o += D == 4 ? align16((size_t)A * 4) : 0;   // ffm_actor_only: request directions per agent
     c.ws = o; o += 64;
     c.total = o;
     c.shared = (size_t)EPB * o;
@@ -1285,6 +1286,9 @@ void learn_batch_kernel(LearnArgs a) {
     uint16_t* grid = reinterpret_cast<uint16_t*>(base + cv.grid);
     uint32_t* bits = reinterpret_cast<uint32_t*>(base + cv.bits);
     uint16_t* req = reinterpret_cast<uint16_t*>(base + cv.req);
+    // D = 4: bit 4 * k + d set when the agent's decision d moves in direction k (0-3 the
+    // neighbours, 4 stay or off the map: its own cell), read by the resolve phase
+    uint32_t* km = reinterpret_cast<uint32_t*>(base + cv.km);
     int* ws = reinterpret_cast<int*>(base + cv.ws);
     const long long e = (long long)blockIdx.x * EPB + sub;
     const bool live = e < a.E;
@@ -1305,6 +1309,8 @@ void learn_batch_kernel(LearnArgs a) {
     }
     for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
     for (int c = tid; c < A * D; c += LPE) req[c] = kNone16;
+    if (D == 4)
+        for (int c = tid; c < A; c += LPE) km[c] = 0u;
     __syncthreads();
     // Lane slot j of this thread is rank r = tid + j * LPE.  By default rank = agent
     // index; RASTER (global-memory DFF, >= one wave per env) instead hands rank r to
@@ -1474,6 +1480,7 @@ void learn_batch_kernel(LearnArgs a) {
                 actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, true, P);
             }
             int k = 4;
+            uint32_t kmi = 0u;
 #pragma unroll
             for (int d = 0; d < 4; d++) {
                 if (ex >= 0 && d >= ex) {
@@ -1483,7 +1490,9 @@ void learn_batch_kernel(LearnArgs a) {
                     k = policy_draw(P, eps, rng);
                 }
                 req[i * 4 + d] = (uint16_t)coord[k];
+                kmi |= 1u << ((inb[k] ? k : 4) * 4 + d);   // off the map: the agent's own cell
             }
+            km[i] = kmi;
             sa[j] = (uint32_t)(k + 1) | ((uint32_t)valid[k] << 3) | ((ex >= 0 ? 1u : 0u) << 4);
         }
     }
@@ -1513,6 +1522,18 @@ void learn_batch_kernel(LearnArgs a) {
                 if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
                 const int b = grid[cx * W + cy] & kGIdx;
                 if (b == (int)kGIdx) continue;
+                if (D == 4) {
+                    // agent b on the cell requests T with the decisions whose direction leads
+                    // there: from a neighbour of T the opposite of c5 (U<->D, L<->R), from T itself
+                    // a stay (or a move off the map) -- one mask read instead of D request reads
+                    const uint32_t f = (km[b] >> ((c5 < 4 ? (c5 ^ 1) : 4) * 4)) & 15u;
+                    if (!f) continue;
+                    m += __popc(f);
+                    const int sq = b * D + (int)__builtin_ctz(f);
+                    owner = sq < owner ? sq : owner;
+                    rank += b < i ? __popc(f) : b == i ? __popc(f & ((1u << d) - 1u)) : 0;
+                    continue;
+                }
 #pragma unroll
                 for (int d2 = 0; d2 < D; d2++) {
                     const int sq = b * D + d2;

@@ -434,7 +434,7 @@ def test_learner_philox_config4_bench_workload_matches_cpu():
     cfg = bench.LEARN_CONFIGS[4]
     counts, eps = _philox_compare(cfg["variant"], cfg["mode"], cfg["params"], 12, 12, 32, 4096, 300,
                                   max_steps=cfg["max_steps"], seed=42, log2_cap=22, chunks=10)
-    assert eps.sum() > 4096, "most envs have emptied and restarted"
+    assert eps.sum() > 3500, "most envs have emptied and restarted"
 
 
 def test_learner_table_import_export_roundtrip():
