@@ -1939,11 +1939,13 @@ __device__ __forceinline__ int own_local(const LearnArgs& a, int t) {
 }
 
 // A launch's tiles: block -> (launch tile k, tile t); k >= the launch's tiles: nothing to do.
+template <bool TM>
 __device__ __forceinline__ void tile_of_launch(const LearnArgs& a, int& k, int& t) {
-    k = tile_of_block(a.thdr ? a.NTk : a.NT);
-    t = a.thdr ? own_tile(a, k) : k;
+    k = tile_of_block(TM ? a.NTk : a.NT);
+    t = TM ? own_tile(a, k) : k;
 }
-__device__ __forceinline__ int launch_tiles(const LearnArgs& a) { return a.thdr ? a.NTk : a.NT; }
+template <bool TM>
+__device__ __forceinline__ int launch_tiles(const LearnArgs& a) { return TM ? a.NTk : a.NT; }
 
 // Tile-major records: the ranges of launch tile k (wave 0, tR <= 64 lanes) -> rs[r] = records
 // of the ranges before r (rs[tR] = the tile's total), rb[r] = first record of range r (the
@@ -2079,31 +2081,26 @@ __device__ __forceinline__ void block_append_runs(unsigned long long* ctr, const
     __syncthreads();
 }
 
-// The nonzero H increments of J rows (p: a row applied here), each row's increments
-// adjacent in the output, so a receiver's updates of one row share its record's line.
+// The nonzero H increments of the rows a thread applies go out with a row's increments
+// adjacent (a receiver's updates of one row then share its record's line): the caller
+// counts each row's nonzero increments (n[j]), hout_reserve gives every row its first
+// output index (uniform call, block-aggregated), hout_row writes a row.  q is re-read
+// per row by the caller, so no thread holds all its rows' sums at once.
 template <int J>
-__device__ __forceinline__ void hout_push(const LearnArgs& a, const bool (&p)[J], const uint32_t (&slot)[J],
-                                          const long long (&q)[J][5], int* lw) {
+__device__ __forceinline__ void hout_reserve(const LearnArgs& a, const int (&n)[J], int (&base)[J], int* lw) {
     if (!a.hout_n) return;
-    int n[J], base[J];
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-        n[j] = 0;
-#pragma unroll
-        for (int k = 0; k < 5; k++) n[j] += (p[j] && q[j][k] != 0) ? 1 : 0;
-    }
     block_append_runs<J>(a.hout_n, n, base, lw);
+}
+
+__device__ __forceinline__ void hout_row(const LearnArgs& a, int base, uint32_t slot, const long long (&q)[5]) {
+    if (!a.hout_n) return;
 #pragma unroll
-    for (int j = 0; j < J; j++) {
-        int o = base[j];
-#pragma unroll
-        for (int k = 0; k < 5; k++)
-            if (p[j] && q[j][k] != 0) {
-                a.hout_key[o] = slot[j] | ((uint32_t)k << 28);
-                a.hout_q[o] = q[j][k];
-                o++;
-            }
-    }
+    for (int k = 0; k < 5; k++)
+        if (q[k] != 0) {
+            a.hout_key[base] = slot | ((uint32_t)k << 28);
+            a.hout_q[base] = q[k];
+            base++;
+        }
 }
 
 constexpr int kTileEnvChunk = 2 * kTileThreads;   // envs whose ranges one pass gathers
@@ -2164,11 +2161,11 @@ __device__ __forceinline__ void tile_fill(const LearnArgs& a, long long e0, cons
 
 // Calls f(g) for every record g of tile t's cells, dealt evenly over the threads: one
 // dependent chain (range, record, table reads) per record instead of one per env in turn.
-template <typename F>
+template <bool TM, typename F>
 __device__ __forceinline__ void tile_records(const LearnArgs& a, int t, int k, uint32_t* list, int* wsum,
                                              uint32_t* rs, uint32_t* rb, F f) {
     const int tid = (int)threadIdx.x;
-    if (a.thdr) {       // tile-major: the tile's records are the ranges' runs
+    if (TM) {       // tile-major: the tile's records are the ranges' runs
         const int total = tm_spans(a, k, rs, rb);
         for (int b = 0; b < total; b += kTileList) {
             const int m = total - b < kTileList ? total - b : kTileList;
@@ -2201,9 +2198,10 @@ __device__ __forceinline__ void tile_records(const LearnArgs& a, int t, int k, u
 // owed).
 constexpr int kTileJ = kTileList / kTileThreads;
 
+template <bool TM>
 __device__ __forceinline__ int tile_window(const LearnArgs& a, int t, int k, uint32_t* list, int* wsum, uint32_t* rs,
                                            uint32_t* rb) {
-    if (a.thdr) {       // tile-major: any number of envs, only the tile's record count matters
+    if (TM) {       // tile-major: any number of envs, only the tile's record count matters
         const int total = tm_spans(a, k, rs, rb);
         if (total > kTileList) return -1;
         for (int j = (int)threadIdx.x; j < total; j += kTileThreads) list[j] = tm_index(a, rs, rb, (uint32_t)j);
@@ -2241,6 +2239,7 @@ __device__ __forceinline__ unsigned long long dense_key(uint32_t slot, int qsh, 
 }
 
 // V: visit-averaged TD(0) of every touched state (learn_apply_dense_kernel's update).
+template <bool TM>
 __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
     __shared__ long long qs[NS];
@@ -2250,9 +2249,9 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     __shared__ uint32_t rs[kMaxOwners + 1], rb[kMaxOwners];
     const int tid = (int)threadIdx.x;
     int k, t;
-    tile_of_launch(a, k, t);
+    tile_of_launch<TM>(a, k, t);
     if (blockIdx.x == 0 && tid == 0) a.tcand[0] = 0;    // the H pass's queue of wide tiles
-    if (k >= launch_tiles(a)) return;
+    if (k >= launch_tiles<TM>(a)) return;
     for (int i = tid; i < NS; i += kTileThreads) { qs[i] = 0; ks[i] = 0u; }
     __syncthreads();
     const uint32_t Q = (a.V.mask + 1u) >> 8;
@@ -2265,7 +2264,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
             if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
         }
     };
-    const int m = tile_window(a, t, k, list, wsum, rs, rb);
+    const int m = tile_window<TM>(a, t, k, list, wsum, rs, rb);
     if (m >= 0) {
         TileRec rc[kTileJ];
 #pragma unroll
@@ -2296,10 +2295,10 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
                 tval(a.V, sl[j])[0] = nv[j];
             }
         }
-        vout_push<kTileJ>(a, own, sl, nv, wsum);
+        if (TM) vout_push<kTileJ>(a, own, sl, nv, wsum);
         return;
     }
-    if (a.thdr) {       // tile-major (tile_window left the spans in rs / rb)
+    if (TM) {           // tile-major (tile_window left the spans in rs / rb)
         const int total = (int)rs[a.tR];
         for (int b = 0; b < total; b += kTileList) {
             TileRec rc[kTileJ];
@@ -2315,7 +2314,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
         }
         __syncthreads();
     } else {
-        tile_records(a, t, k, list, wsum, rs, rb, [&](uint32_t g) {
+        tile_records<TM>(a, t, k, list, wsum, rs, rb, [&](uint32_t g) {
             const TileRec rc = a.trecs[g];
             const uint32_t sv = rc.svk & 0x0FFFFFFFu;
             const int idx = tile_idx(sv, qsh, Q, c0);
@@ -2345,7 +2344,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
             tval(a.V, sl[j])[0] = nv[j];
         }
     }
-    vout_push<kPer>(a, up, sl, nv, wsum);
+    if (TM) vout_push<kPer>(a, up, sl, nv, wsum);
 }
 
 // Exact min / max / non-finite of one tile's present H rows (a block-wide scan).
@@ -2510,6 +2509,7 @@ __device__ __forceinline__ void tile_h_end(const LearnArgs& a, int t, TileHCtx& 
 // learn_tile_v_kernel) for learn_tile_h_wide_kernel.
 constexpr int kTilePairs = 256 * kTileCells * 5;
 
+template <bool TM>
 __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
     __shared__ long long hq[kTileList];             // per touched (slot, action) pair
@@ -2524,8 +2524,8 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     __shared__ int npair;
     const int tid = (int)threadIdx.x, lane = tid & 63;
     int k, t;
-    tile_of_launch(a, k, t);
-    if (k >= launch_tiles(a)) return;
+    tile_of_launch<TM>(a, k, t);
+    if (k >= launch_tiles<TM>(a)) return;
     const uint32_t Q = (a.Ht.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
     for (int i = tid; i < kTileList; i += kTileThreads) hq[i] = 0;
@@ -2533,7 +2533,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     if (tid < NS / 32) touched[tid] = 0u;
     if (tid == 0) npair = 0;
     // (tile_window's barriers order these stores before any use)
-    const int m = tile_window(a, t, k, list, wsum, rs, rb);
+    const int m = tile_window<TM>(a, t, k, list, wsum, rs, rb);
     if (m < 0) {
         if (tid == 0) a.tcand[1 + atomicAdd(&a.tcand[0], 1)] = t;
         return;
@@ -2590,25 +2590,41 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
 #pragma unroll
         for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
     }
-    long long q[kTileJ][5];
-    uint32_t sl[kTileJ];
-#pragma unroll
-    for (int j = 0; j < kTileJ; j++) {
-        sl[j] = rc[j].svk & 0x0FFFFFFFu;
+    auto row_q = [&](int j, long long (&q)[5]) {
 #pragma unroll
         for (int kk = 0; kk < 5; kk++) {
             const int p = ix[j] * 5 + kk;
-            q[j][kk] = own[j] && ((pbit[p >> 5] >> (p & 31)) & 1u) ? hq[pid[p]] : 0;
+            q[kk] = ((pbit[p >> 5] >> (p & 31)) & 1u) ? hq[pid[p]] : 0;
         }
-        if (own[j]) tile_h_apply(tval(a.Ht, sl[j]), q[j], hv[j], c);
+    };
+    int hn[kTileJ], hb[kTileJ];
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++) {     // owner mode: each row's nonzero increments, reserved
+        hn[j] = 0;
+        if (TM && a.hout_n && own[j]) {
+            long long q[5];
+            row_q(j, q);
+#pragma unroll
+            for (int kk = 0; kk < 5; kk++) hn[j] += q[kk] != 0 ? 1 : 0;
+        }
     }
-    hout_push<kTileJ>(a, own, sl, q, wsum);
+    if (TM) hout_reserve<kTileJ>(a, hn, hb, wsum);
+#pragma unroll
+    for (int j = 0; j < kTileJ; j++) {
+        if (!own[j]) continue;
+        long long q[5];
+        row_q(j, q);
+        const uint32_t sl = rc[j].svk & 0x0FFFFFFFu;
+        tile_h_apply(tval(a.Ht, sl), q, hv[j], c);
+        if (TM) hout_row(a, hb[j], sl, q);
+    }
     tile_h_end(a, t, c, smn, smx, sfl);
 }
 
 // The general form, for the tiles the fast form queued (more than one window of
 // records: a crowded tile, or more than 512 envs): every (slot, action) pair of the
 // tile has its word (40 KB), records stream through windows, then the touched rows.
+template <bool TM>
 __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
     __shared__ long long hq[NS * 5];
@@ -2623,12 +2639,12 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
     const int qsh = __builtin_ctz(Q);
     const int n = a.tcand[0];
     for (int ci = (int)blockIdx.x; ci < n; ci += (int)gridDim.x) {
-        const int t = a.tcand[1 + ci], c0 = t * kTileCells, kt = a.thdr ? own_local(a, t) : t;
+        const int t = a.tcand[1 + ci], c0 = t * kTileCells, kt = TM ? own_local(a, t) : t;
         for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
         for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
         __syncthreads();
         TileHCtx c = tile_h_begin(a, t);
-        if (a.thdr) {       // tile-major: windows of kTileJ records per thread, the loads first
+        if (TM) {           // tile-major: windows of kTileJ records per thread, the loads first
             const int total = tm_spans(a, kt, rs, rb);
             for (int b = 0; b < total; b += kTileList) {
                 TileRec rc[kTileJ];
@@ -2650,7 +2666,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
             }
             __syncthreads();
         } else {
-            tile_records(a, t, kt, list, wsum, rs, rb, [&](uint32_t g) {
+            tile_records<TM>(a, t, kt, list, wsum, rs, rb, [&](uint32_t g) {
                 const TileRec rc = a.trecs[g];
                 const uint32_t sv = rc.svk & 0x0FFFFFFFu;
                 const int idx = tile_idx(sv, qsh, Q, c0);
@@ -2678,17 +2694,27 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
                 for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
             }
         }
-        long long q[kPer][5];
-        uint32_t sl[kPer];
+        int hn[kPer], hb[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const int i = tid + j * kTileThreads;
-            sl[j] = (uint32_t)((size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+            hn[j] = 0;
+            if (TM && a.hout_n && tch[j])
 #pragma unroll
-            for (int kk = 0; kk < 5; kk++) q[j][kk] = tch[j] ? hq[i * 5 + kk] : 0;
-            if (tch[j]) tile_h_apply(tval(a.Ht, sl[j]), q[j], hv[j], c);
+                for (int kk = 0; kk < 5; kk++) hn[j] += hq[i * 5 + kk] != 0 ? 1 : 0;
         }
-        hout_push<kPer>(a, tch, sl, q, wsum);
+        if (TM) hout_reserve<kPer>(a, hn, hb, wsum);
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            const int i = tid + j * kTileThreads;
+            if (!tch[j]) continue;
+            const uint32_t sl = (uint32_t)((size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
+            long long q[5];
+#pragma unroll
+            for (int kk = 0; kk < 5; kk++) q[kk] = hq[i * 5 + kk];
+            tile_h_apply(tval(a.Ht, sl), q, hv[j], c);
+            if (TM) hout_row(a, hb[j], sl, q);
+        }
         tile_h_end(a, t, c, smn, smx, sfl);
     }
 }
@@ -3567,10 +3593,16 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
         return hipGetLastError();
     }
     const unsigned tgrid = 8u * (unsigned)((a.NT + 7) / 8);
-    learn_tile_v_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    if (a.thdr) learn_tile_v_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    else learn_tile_v_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
     if (actor) {
-        learn_tile_h_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-        learn_tile_h_wide_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        if (a.thdr) {
+            learn_tile_h_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+            learn_tile_h_wide_kernel<true><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        } else {
+            learn_tile_h_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+            learn_tile_h_wide_kernel<false><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        }
         learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
@@ -3598,7 +3630,7 @@ hipError_t launch_learn_tile_pack(const LearnArgs& a, uint32_t* pe, uint32_t* tp
 hipError_t launch_learn_tiles_owner_v(const LearnArgs& a, hipStream_t s) {
     const unsigned tgrid = 8u * (unsigned)((a.NTk + 7) / 8);
     if (a.vout_n) (void)hipMemsetAsync(a.vout_n, 0, 8, s);
-    if (a.NTk > 0) learn_tile_v_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    if (a.NTk > 0) learn_tile_v_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
     return hipGetLastError();
 }
 
@@ -3607,8 +3639,8 @@ hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStrea
     const unsigned nresc = (unsigned)(a.NTk < 2048 ? (a.NTk > 0 ? a.NTk : 1) : 2048);
     if (a.hout_n) (void)hipMemsetAsync(a.hout_n, 0, 8, s);
     if (a.NTk > 0) {
-        learn_tile_h_kernel<<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-        learn_tile_h_wide_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        learn_tile_h_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+        learn_tile_h_wide_kernel<true><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tsum_pack_kernel<<<dim3((unsigned)((a.NTk + 255) / 256)), dim3(256), 0, s>>>(a, tsum);
     }
     return hipGetLastError();
