@@ -58,7 +58,10 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
         const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        // three-input xor in one v_bitop3_b32 (gfx950; truth table 0x96): the compiler
+        // otherwise issues two v_xor_b32 per word
+        c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+                       __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }

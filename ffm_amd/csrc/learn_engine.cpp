@@ -118,6 +118,7 @@ struct ffm_learner {
     unsigned long long* d_on = nullptr;      // [2] V / H output counts
     size_t ocap = 0;
     double* d_tsum = nullptr;                // [ths][5] this rank's tile summaries
+    unsigned char* d_bph = nullptr;          // the phase-split batch step's per-env state (learn_batch_phases)
     const ffm::TileRec* own_recs = nullptr;  // the received records of the current owner step
     const uint32_t* own_hdr = nullptr;
     DevTable V, H;
@@ -145,7 +146,7 @@ static void release(ffm_learner* l) {
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
                     l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand,
                     l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_pack, l->d_xcnt, l->d_newv, l->d_newh,
-                    l->d_vslot, l->d_vval, l->d_hkey, l->d_hq, l->d_on, l->d_tsum};
+                    l->d_vslot, l->d_vval, l->d_hkey, l->d_hq, l->d_on, l->d_tsum, l->d_bph};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
     free_traj(l);
@@ -236,6 +237,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.mBS = magic(a.bs);
     a.trecs = nullptr;       // the accumulator path unless a tiled step sets it
     a.tstart = l->d_tstart;
+    a.bph = l->d_bph;
     a.tstats = l->d_tstats;
     a.tdirty = l->d_tdirty;
     a.tcand = l->d_tcand;
@@ -443,6 +445,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
             hipMalloc((void**)&l->d_xcnt, (ffm::kMaxOwners + 2) * 8) != hipSuccess ||
             hipMalloc((void**)&l->d_on, 16) != hipSuccess)
             return cleanup(fail(FFM_E_NOMEM, "hipMalloc (tiled step)"));
+        const size_t pb = l->actor ? ffm::learn_batch_phase_bytes((long long)E, HW, (int)A) : 0;
+        if (pb && hipMalloc((void**)&l->d_bph, pb) != hipSuccess)
+            return cleanup(fail(FFM_E_NOMEM, "hipMalloc (phase-split batch step)"));
     }
     he = hipMemcpy(l->d_map, d.map, HW, hipMemcpyHostToDevice);
     if (he == hipSuccess) {

@@ -122,6 +122,10 @@ struct LearnArgs {
     uint32_t* hout_key;
     long long* hout_q;
     unsigned long long* hout_n;
+    // Phase-split batch step (learn_batch_phases): per env the 2-bit state
+    // maps of the current and next positions, the agents in raster order (cell, agent index)
+    // and the decide / resolve outputs per raster rank.  nullptr: the fused batch kernel.
+    unsigned char* bph;
     int* overflow;              // [1] table full / reset capacity exceeded
     uint32_t key0, key1, t;
     int auto_reset, max_steps;
@@ -183,6 +187,8 @@ hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s);
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
 bool learn_batch_raster(int HW, int A, int D);
+// Bytes of LearnArgs::bph for a tiled learner of E envs (0: the shape keeps the fused kernel).
+size_t learn_batch_phase_bytes(long long E, int HW, int A);
 hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s);
 // tile-major records: the column scan, the tile offsets in destination order (per-destination
 // headers, hdr row stride ths, and record counts xcnt[ow]) and the scatter of trecs into out.

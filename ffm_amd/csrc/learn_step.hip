@@ -18,6 +18,7 @@
 //    once per step by learn_apply_kernel.
 // All translation units are built with -ffp-contract=off.
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 #include "learn_kernels.h"
@@ -352,10 +353,14 @@ __device__ unsigned long long enc13(const SM& sm, int H, int W, int x, int y, ui
 }
 
 template <class SM>
-__device__ unsigned long long encode(const LearnArgs& a, const SM& sm, int x, int y) {
-    if (a.variant == kVarUnified || a.variant == kVarTrained) return enc_rank(sm, a.H, a.W, x, y, a.mBS);
-    if (a.variant == kVarAC) return enc13(sm, a.H, a.W, x, y, a.mBS, 2);
+__device__ unsigned long long encode_v(const LearnArgs& a, int variant, const SM& sm, int x, int y) {
+    if (variant == kVarUnified || variant == kVarTrained) return enc_rank(sm, a.H, a.W, x, y, a.mBS);
+    if (variant == kVarAC) return enc13(sm, a.H, a.W, x, y, a.mBS, 2);
     return enc13(sm, a.H, a.W, x, y, a.mBS, 0);                // block 5 hard-coded, :143 (a.bs = 5)
+}
+template <class SM>
+__device__ unsigned long long encode(const LearnArgs& a, const SM& sm, int x, int y) {
+    return encode_v(a, a.variant, sm, x, y);
 }
 
 // ---- random draws -----------------------------------------------------------
@@ -1274,7 +1279,11 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB,
 #define FFM_LBATCH_WAVES 1   // minimum waves per SIMD asked of the register allocator
 #endif
 
-template <int BS, int EPB, int APT, int D, bool DL>
+// VK = 1: the shape of BASELINE config 5 fixed at compile time -- ffm_unified in an actor
+// mode, dense V and H, tiled records (learn_batch_uni) -- so the unrolled agent slots carry
+// none of the other variants' paths (a fraction of the generic kernel's code: fewer
+// instruction-cache misses across 16 waves walking it)
+template <int BS, int EPB, int APT, int D, bool DL, int VK = 0>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(FFM_LBATCH_WAVES, 8)))
 void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1294,8 +1303,11 @@ void learn_batch_kernel(LearnArgs a) {
     const bool live = e < a.E;
     const uint32_t genv = (uint32_t)(a.env_base + e);
     const int n = live ? a.cnt[e] : 0;
-    const bool actor = a.variant == kVarActorOnly || (a.variant == kVarUnified && a.mode != kModeCritic);
-    const bool post_update = a.variant == kVarUnified && a.mode == kModeActor;
+    constexpr bool UNI = VK == 1;
+    const int variant = UNI ? (int)kVarUnified : a.variant;
+    const bool actor = UNI || variant == kVarActorOnly || (variant == kVarUnified && a.mode != kModeCritic);
+    const bool post_update = variant == kVarUnified && a.mode == kModeActor;
+    const bool vdense = UNI || a.V.dense_by, hdense = UNI || a.Ht.dense_by;
     float* dff = DL ? reinterpret_cast<float*>(base + cv.dff) : a.dff_in + (live ? e : 0) * (long long)HW;
 #if FFM_LSTAMP
     unsigned long long ts_[8];
@@ -1322,7 +1334,7 @@ void learn_batch_kernel(LearnArgs a) {
     constexpr bool RASTER = FFM_RASTER && !DL && LPE >= 64 && EPB == 1;
     // tiled step: records in raster order for the tile kernels, no
     // accumulator adds; set by the host for single-rank ffm_unified steps at block size 1
-    const bool TILED = RASTER && a.trecs != nullptr;
+    const bool TILED = UNI || (RASTER && a.trecs != nullptr);
     // Per-agent state, packed so the APT slots of a lane stay in registers (APT = 8 at
     // C5: unpacked, the kernel spilled to scratch).  pa: cell (bits 0-15) | agent index
     // (16-29).  sa, from decide on: act + 1 (0-2), avalid (3), wexit (4), and from
@@ -1386,7 +1398,7 @@ void learn_batch_kernel(LearnArgs a) {
         for (int c = tid; c < n; c += LPE) req[c] = kNone16;
         __syncthreads();
     }
-    const bool trained = a.variant == kVarTrained;
+    const bool trained = variant == kVarTrained;
     const double eps = live && actor ? env_epsilon(a, a.episodes[e], a.env_base + e) : 0.0;
     HStat hs{};
     if (actor || trained) {
@@ -1413,7 +1425,7 @@ void learn_batch_kernel(LearnArgs a) {
         if (KEYS) { skey[j] = 0; hsl[j] = -1; }
         if (tid + j * LPE >= n) continue;
         const int x = fdiv(BK_P(j), a.mW), y = BK_P(j) - x * W;
-        const unsigned long long sk = encode(a, smc, x, y);
+        const unsigned long long sk = encode_v(a, variant, smc, x, y);
         if (KEYS) skey[j] = sk;
         int coord[5], valid[5], inb[5];
         int cls[5];
@@ -1427,7 +1439,7 @@ void learn_batch_kernel(LearnArgs a) {
             sa[j] = 5u | 8u;
             continue;
         }
-        if (a.variant == kVarAC) {
+        if (variant == kVarAC) {
             // ffm_core candidates: free neighbours, then stay if any (:126-164)
             if ((valid[0] | valid[1] | valid[2] | valid[3]) == 0) continue;
             int exv = -1;
@@ -1454,7 +1466,7 @@ void learn_batch_kernel(LearnArgs a) {
                     trained_policy(a, tab_find(a.Ht, sk), coord, valid, dff, hs, P);
                 } else if (!actor) {
                     critic_policy(a, coord, valid, dff, P);
-                } else if (a.Ht.dense_by) {
+                } else if (hdense) {
                     const int h = (int)dense_slot(sk, a.Ht);
                     if (KEYS) hsl[j] = h;
                     actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, false, P);
@@ -1589,7 +1601,7 @@ void learn_batch_kernel(LearnArgs a) {
                 skj = skey[j];
             } else {
                 const int px = fdiv(BK_P(j), a.mW);
-                skj = encode(a, smc, px, BK_P(j) - px * W);
+                skj = encode_v(a, variant, smc, px, BK_P(j) - px * W);
             }
             double r = a.step_penalty;
             if (BK_WEXIT(j)) r = r + a.exit_reward;
@@ -1598,8 +1610,8 @@ void learn_batch_kernel(LearnArgs a) {
             double vn = 0.0;
             if (!BK_WEXIT(j)) {
                 const int nx = fdiv(BK_NXT(j), a.mW), ny = BK_NXT(j) - nx * W;
-                const unsigned long long nk = encode(a, smn, nx, ny);
-                if (a.V.dense_by) {
+                const unsigned long long nk = encode_v(a, variant, smn, nx, ny);
+                if (vdense) {
                     sn = (int)dense_slot(nk, a.V);
                     vn = tval(a.V, sn)[0];
                     dense_ensure(a.V, (uint32_t)sn, nk);
@@ -1609,7 +1621,7 @@ void learn_batch_kernel(LearnArgs a) {
                 }
             }
             int sv;
-            if (a.V.dense_by) {
+            if (vdense) {
                 sv = (int)dense_slot(skj, a.V);
                 dense_ensure(a.V, (uint32_t)sv, skj);
             } else {
@@ -1625,8 +1637,15 @@ void learn_batch_kernel(LearnArgs a) {
             if (BK_ACT(j) < 0) break;
             // the decide phase's H slot; without KEYS, dense tables recompute it (the decide
             // phase inserted it unless the agent was exit-forced) and hashed ones probe again
-            int hslj = KEYS ? hsl[j] : (a.Ht.dense_by && !BK_WEXIT(j) ? (int)dense_slot(skj, a.Ht) : -1);
-            if (hslj < 0) hslj = tab_get(a.Ht, skj, a.overflow);   // dense: slot + insert, no probe
+            int hslj = KEYS ? hsl[j] : (hdense && !BK_WEXIT(j) ? (int)dense_slot(skj, a.Ht) : -1);
+            if (hslj < 0) {     // dense: slot + insert, no probe
+                if (UNI) {
+                    hslj = (int)dense_slot(skj, a.Ht);
+                    dense_ensure(a.Ht, (uint32_t)hslj, skj);
+                } else {
+                    hslj = tab_get(a.Ht, skj, a.overflow);
+                }
+            }
             if (hslj < 0) break;
             if (TILED) {            // the tile kernels sum the increments (hsl == sv: one dense layout)
                 kk = BK_AVALID(j) ? BK_ACT(j) : (int)kTileNoAct;
@@ -1729,6 +1748,377 @@ void learn_batch_kernel(LearnArgs a) {
         slot[1] += (unsigned long long)(n - base_);
         slot[3] += 1;
     }
+}
+
+// ===========================================================================
+// The phase-split batch step: learn_batch_kernel's phases for the
+// VK = 1 shape (ffm_unified in an actor mode, dense tables, tiled records, one decision
+// per agent, maps of at most 65,536 cells) as four launches.  The fused kernel holds an
+// env's 128 KB agent grid in LDS, so one 1,024-lane workgroup per CU walks eight agents
+// per lane through dependent table reads; here the table-bound phases (decide: state
+// key -> H row -> policy; learn: next-state key -> V rows) run one agent per lane at
+// full occupancy from two 2-bit state maps in global memory (L2-resident), and only
+// the conflict resolution keeps a per-env LDS workgroup (68 KB: two per CU).
+//   prep    (env per workgroup): occupancy bits, the current state map, the agents in
+//           raster order (cell, agent index), the tile offsets of the records;
+//   decide  (agent per lane, raster order): target, action, validity, exit forcing;
+//   resolve (env per workgroup): requesters of each target, friction draw, deposits,
+//           the next state map, order-preserving exit removal, counters;
+//   learn   (agent per lane): the TD error and the record of learn_batch_kernel.
+// Every value is computed by the same expressions in the same order as the fused
+// kernel's, so the step is bit-identical to it (and to the oracle).
+// ===========================================================================
+constexpr int kPhBS = 1024;              // prep / resolve workgroup (one env)
+constexpr int kPhLanes = 256;            // decide / learn workgroup (256 consecutive raster ranks)
+constexpr int kPhWords = 65536 / 32;     // occupancy words of the largest map
+
+struct PhaseCarve {
+    uint32_t* sm;     // [E][mw] current state map: 2 bits per cell, occupied ? 1 : map class
+    uint32_t* nm;     // [E][mw] next state map (next cells that are not exits)
+    uint16_t* rc;     // [E][A] cell of raster rank r
+    uint16_t* ri;     // [E][A] agent index of raster rank r
+    uint32_t* dec;    // [E][A] decide: target (0-15), action + 1 (16-18), valid (19), exit-forced (20)
+    uint32_t* res;    // [E][A] resolve: next cell (0-15), collisions + 1 (16-20), decide bits 16-20 (21-25)
+};
+
+__host__ __device__ inline PhaseCarve phase_carve(unsigned char* b, long long E, int HW, int A) {
+    const size_t mw = (size_t)(HW + 15) / 16;
+    PhaseCarve c;
+    c.sm = reinterpret_cast<uint32_t*>(b);
+    c.nm = c.sm + (size_t)E * mw;
+    c.rc = reinterpret_cast<uint16_t*>(c.nm + (size_t)E * mw);
+    c.ri = c.rc + (size_t)E * A;
+    c.dec = reinterpret_cast<uint32_t*>(c.ri + (size_t)E * A);
+    c.res = c.dec + (size_t)E * A;
+    return c;
+}
+
+struct Sm2 {                     // a 2-bit state map in global memory
+    const uint32_t* m;
+    __device__ int operator()(int c) const { return (int)((m[c >> 4] >> ((c & 15) << 1)) & 3u); }
+};
+
+// 16 occupancy bits into a word of 16 2-bit map classes: occupied cells read 1.
+__device__ __forceinline__ uint32_t state2(uint32_t m2, uint32_t o16) {
+    uint32_t x = o16;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return (m2 & ~(x | (x << 1))) | x;
+}
+
+// Raster rank of cell c: the occupied cells before it.
+__device__ __forceinline__ int cell_rank(const uint32_t* occ, const uint16_t* pre, int c) {
+    return (int)pre[c >> 5] + __popc(occ[c >> 5] & ((1u << (c & 31)) - 1u));
+}
+
+// Exclusive block scan of one value per thread (BS threads); ends after a barrier.
+template <int BS>
+__device__ __forceinline__ int block_exscan(int v, int* ws, int& total) {
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) ws[wv] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BS / 64; w++) {
+        const int c = ws[w];
+        off += w < wv ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return off + incl - v;
+}
+
+// Occupancy words -> word prefix (pre) of the raster ranks; ends after a barrier.
+__device__ __forceinline__ void occ_prefix(const uint32_t* occ, uint16_t* pre, int nw, int* ws) {
+    constexpr int K = kPhWords / kPhBS;
+    const int tid = (int)threadIdx.x;
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const int w = tid * K + q;
+        cnt += w < nw ? __popc(occ[w]) : 0;
+    }
+    int tot;
+    int off = block_exscan<kPhBS>(cnt, ws, tot);
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const int w = tid * K + q;
+        if (w < nw) {
+            pre[w] = (uint16_t)off;
+            off += __popc(occ[w]);
+        }
+    }
+    __syncthreads();
+}
+
+// The 2-bit map of occupancy bits occ (16 cells per output word).
+__device__ __forceinline__ void write_state_map(const LearnArgs& a, const uint32_t* occ, uint32_t* out) {
+    const int mw = (a.HW + 15) >> 4;
+    for (int w = (int)threadIdx.x; w < mw; w += kPhBS)
+        out[w] = state2(a.map2[w], (occ[w >> 1] >> ((w & 1) * 16)) & 0xFFFFu);
+}
+
+__global__ __launch_bounds__(kPhBS) void learn_phase_prep_kernel(LearnArgs a) {
+    __shared__ uint32_t occ[kPhWords];
+    __shared__ uint16_t pre[kPhWords];
+    __shared__ int ws[kPhBS / 64];
+    const long long e = blockIdx.x;
+    const int tid = (int)threadIdx.x, HW = a.HW, A = a.A;
+    const int nw = (HW + 31) >> 5, mw = (HW + 15) >> 4;
+    const PhaseCarve pc = phase_carve(a.bph, a.E, HW, A);
+    const int n = a.cnt[e];
+    const uint16_t* pos = a.pos + e * A;
+    for (int w = tid; w < nw; w += kPhBS) occ[w] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += kPhBS) {
+        const int c = pos[i];
+        atomicOr(&occ[c >> 5], 1u << (c & 31));
+    }
+    __syncthreads();
+    write_state_map(a, occ, pc.sm + e * mw);
+    occ_prefix(occ, pre, nw, ws);
+    uint16_t* rc = pc.rc + e * A;
+    uint16_t* ri = pc.ri + e * A;
+    for (int i = tid; i < n; i += kPhBS) {
+        const int c = pos[i];
+        const int r = cell_rank(occ, pre, c);
+        rc[r] = (uint16_t)c;
+        ri[r] = (uint16_t)i;
+    }
+    // the raster rank of the first agent of every tile (learn_batch_kernel's RASTER pass)
+    uint16_t* ts = a.tstart + e * (a.NT + 1);
+    for (int t = tid; t <= a.NT; t += kPhBS) {
+        const int c = t * kTileCells;
+        ts[t] = (uint16_t)(c < HW ? cell_rank(occ, pre, c) : n);
+    }
+}
+
+// Decide / learn workgroups: logical block b (256 consecutive ranks of one env) from
+// the launch's block with XCD-contiguous numbering, so one env's blocks share an L2.
+__device__ __forceinline__ bool phase_block(const LearnArgs& a, long long& e, int& r) {
+    const int bpe = (a.A + kPhLanes - 1) / kPhLanes;
+    const unsigned G8 = gridDim.x >> 3;
+    const unsigned b = (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3);
+    e = (long long)(b / (unsigned)bpe);
+    r = (int)(b % (unsigned)bpe) * kPhLanes + (int)threadIdx.x;
+    return e < a.E;
+}
+
+__global__ __launch_bounds__(kPhLanes) void learn_phase_decide_kernel(LearnArgs a) {
+    long long e;
+    int r;
+    if (!phase_block(a, e, r)) return;
+    const int n = a.cnt[e];
+    if (r >= n) return;
+    const int H = a.H, W = a.W, A = a.A;
+    const PhaseCarve pc = phase_carve(a.bph, a.E, a.HW, A);
+    const Sm2 sm{pc.sm + e * ((a.HW + 15) >> 4)};
+    const uint32_t genv = (uint32_t)(a.env_base + e);
+    const int c = pc.rc[e * A + r], i = pc.ri[e * A + r];
+    const int x = fdiv(c, a.mW), y = c - x * W;
+    const unsigned long long sk = enc_rank(sm, H, W, x, y, a.mBS);
+    int coord[5], valid[5], inb[5], cls[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {      // moves5_grid on the state map and the class map
+        const int nx = k < 4 ? x + kNBx[k] : x, ny = k < 4 ? y + kNBy[k] : y;
+        inb[k] = nx >= 0 && nx < H && ny >= 0 && ny < W;
+        coord[k] = inb[k] ? nx * W + ny : c;
+        cls[k] = inb[k] ? map2_at(a.map2, coord[k]) : 2;
+        const bool occupied = sm(coord[k]) == 1 && cls[k] != 1;
+        valid[k] = inb[k] && (cls[k] == 0 || cls[k] == 3) && (k == 4 || !occupied);
+    }
+    valid[4] = 1;
+    int ex = -1;
+#pragma unroll
+    for (int k = 3; k >= 0; k--) ex = inb[k] && cls[k] == 3 ? k : ex;
+    int k;
+    if (ex >= 0) {
+        k = ex;
+    } else {
+        HStat hs;
+        hs.has = (int)a.hstat[0];
+        hs.nonfinite = (int)a.hstat[1];
+        hs.mn = a.hstat[2];
+        hs.mx = a.hstat[3];
+        const double eps = env_epsilon(a, a.episodes[e], a.env_base + e);
+        const int h = (int)dense_slot(sk, a.Ht);
+        Policy P;
+        actor_policy(a, tval(a.Ht, h), coord, valid, a.dff_in + e * (long long)a.HW, hs, false, P);
+        dense_ensure(a.Ht, (uint32_t)h, sk);
+        DrawPh rng(a, genv, (uint32_t)i);
+        k = policy_draw(P, eps, rng);
+    }
+    pc.dec[e * A + r] = (uint32_t)coord[k] | ((uint32_t)(k + 1) << 16) | ((uint32_t)valid[k] << 19) |
+                        ((ex >= 0 ? 1u : 0u) << 20);
+}
+
+// LDS of the resolve workgroup (dynamic): occupancy and next-cell bits, the word prefix,
+// targets and agent indices by rank, next cells by agent index, scan words.
+struct PhaseResolveCarve {
+    size_t occ, nb, pre, rq, rx, nx, ws, total;
+};
+__host__ __device__ inline PhaseResolveCarve phase_resolve_carve(int HW, int A) {
+    PhaseResolveCarve c;
+    const size_t nw = (size_t)(HW + 31) / 32;
+    size_t o = 0;
+    c.occ = o; o += align16(nw * 4);
+    c.nb = o; o += align16(nw * 4);
+    c.pre = o; o += align16(nw * 2);
+    c.rq = o; o += align16((size_t)A * 2);
+    c.rx = o; o += align16((size_t)A * 2);
+    c.nx = o; o += align16((size_t)A * 2);
+    c.ws = o; o += 64;
+    c.total = o;
+    return c;
+}
+
+__global__ __launch_bounds__(kPhBS) void learn_phase_resolve_kernel(LearnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const PhaseResolveCarve cv = phase_resolve_carve(a.HW, a.A);
+    uint32_t* occ = reinterpret_cast<uint32_t*>(smem + cv.occ);
+    uint32_t* nb = reinterpret_cast<uint32_t*>(smem + cv.nb);
+    uint16_t* pre = reinterpret_cast<uint16_t*>(smem + cv.pre);
+    uint16_t* rq = reinterpret_cast<uint16_t*>(smem + cv.rq);
+    uint16_t* rx = reinterpret_cast<uint16_t*>(smem + cv.rx);
+    uint16_t* nx = reinterpret_cast<uint16_t*>(smem + cv.nx);
+    int* ws = reinterpret_cast<int*>(smem + cv.ws);
+    const long long e = blockIdx.x;
+    const int tid = (int)threadIdx.x, H = a.H, W = a.W, HW = a.HW, A = a.A;
+    const int nw = (HW + 31) >> 5, mw = (HW + 15) >> 4;
+    const PhaseCarve pc = phase_carve(a.bph, a.E, HW, A);
+    const uint32_t genv = (uint32_t)(a.env_base + e);
+    const int n = a.cnt[e];
+    const uint16_t* rc = pc.rc + e * A;
+    const uint32_t* dec = pc.dec + e * A;
+    for (int w = tid; w < nw; w += kPhBS) { occ[w] = 0u; nb[w] = 0u; }
+    __syncthreads();
+    for (int r = tid; r < n; r += kPhBS) {
+        const int c = rc[r];
+        atomicOr(&occ[c >> 5], 1u << (c & 31));
+        rq[r] = (uint16_t)(dec[r] & 0xFFFFu);
+        rx[r] = pc.ri[e * A + r];
+    }
+    __syncthreads();
+    occ_prefix(occ, pre, nw, ws);
+    // learn_batch_kernel's resolve (D = 1): the requesters of T stand on it or next to it;
+    // its owner is the smallest requesting agent index, whose stream draws the winner rank
+    float* dff = a.dff_in + e * (long long)HW;
+    for (int r = tid; r < n; r += kPhBS) {
+        const int c = rc[r], i = rx[r];
+        const uint32_t d = dec[r];
+        const int T = (int)(d & 0xFFFFu);
+        const int tx = fdiv(T, a.mW), ty = T - tx * W;
+        int m = 0, owner = 0x7FFFFFFF, rank = 0;
+#pragma unroll
+        for (int c5 = 0; c5 < 5; c5++) {
+            const int cx = c5 < 4 ? tx + kNBx[c5] : tx, cy = c5 < 4 ? ty + kNBy[c5] : ty;
+            if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
+            const int cc = cx * W + cy;
+            if (!((occ[cc >> 5] >> (cc & 31)) & 1u)) continue;
+            const int b = cell_rank(occ, pre, cc);
+            if (rq[b] != T) continue;
+            const int ib = rx[b];
+            m++;
+            owner = ib < owner ? ib : owner;
+            rank += ib < i ? 1 : 0;
+        }
+        int w = 0;
+        if (m > 1) {
+            PhiloxStream ps(a.key0, a.key1, a.t, genv, (uint32_t)owner, kPurFriction);
+            w = (int)ps.randbelow((uint32_t)m);
+        }
+        const int clj = m == 1 ? 0 : m - 1;
+        const bool won = rank == w;
+        const int nxt = won ? T : c;
+        if (won) {             // the winner's deposit on its own cell (distinct per agent)
+            float v = dff[c];
+            v = v + 1.0f;
+            dff[c] = v;
+        }
+        const bool stays = map2_at(a.map2, nxt) != 3;
+        if (stays) atomicOr(&nb[nxt >> 5], 1u << (nxt & 31));
+        nx[i] = stays ? (uint16_t)nxt : kNone16;
+        pc.res[e * A + r] = (uint32_t)nxt | ((uint32_t)(clj + 1) << 16) | (((d >> 16) & 31u) << 21);
+    }
+    __syncthreads();
+    write_state_map(a, nb, pc.nm + e * mw);
+    // exit removal in agent order (order preserving)
+    int base_ = 0;
+    for (int j = 0; j < (A + kPhBS - 1) / kPhBS; j++) {
+        const int i = tid + j * kPhBS;
+        const int c = i < n ? nx[i] : kNone16;
+        const bool keep = c != kNone16;
+        int tot;
+        const int off = env_scan_flag<kPhBS, kPhBS>(keep, ws, tot);
+        if (keep) a.pos[e * A + base_ + off] = (uint16_t)c;
+        base_ += tot;
+    }
+    if (tid == 0) {
+        a.cnt[e] = base_;
+        a.nstart[e] = n;
+        const int st = a.ep_steps[e] + 1;
+        a.ep_steps[e] = st;
+        a.done[e] = a.auto_reset && (base_ == 0 || (a.max_steps > 0 && st >= a.max_steps)) ? 1 : 0;
+        unsigned long long* slot = a.counters + 4 * e;
+        slot[0] += (unsigned long long)n;
+        slot[1] += (unsigned long long)(n - base_);
+        slot[3] += 1;
+    }
+}
+
+__global__ __launch_bounds__(kPhLanes) void learn_phase_learn_kernel(LearnArgs a) {
+    long long e;
+    int r;
+    if (!phase_block(a, e, r)) return;
+    const int n = a.nstart[e];
+    if (r >= n) return;
+    const int H = a.H, W = a.W, A = a.A;
+    const PhaseCarve pc = phase_carve(a.bph, a.E, a.HW, A);
+    const size_t mo = (size_t)e * ((a.HW + 15) >> 4);
+    const Sm2 smc{pc.sm + mo}, smn{pc.nm + mo};
+    const int c = pc.rc[e * A + r];
+    const uint32_t rs = pc.res[e * A + r];
+    const int nxt = (int)(rs & 0xFFFFu), coll = (int)((rs >> 16) & 31u) - 1;
+    const int act = (int)((rs >> 21) & 7u) - 1, avalid = (int)((rs >> 24) & 1u), wexit = (int)((rs >> 25) & 1u);
+    const int x = fdiv(c, a.mW);
+    const unsigned long long skj = enc_rank(smc, H, W, x, c - x * W, a.mBS);
+    double rw = a.step_penalty;
+    if (wexit) rw = rw + a.exit_reward;
+    if (coll >= 0) rw = rw + (double)coll * a.collision_penalty;
+    int sn = -1;
+    double vn = 0.0;
+    if (!wexit) {
+        const int qx = fdiv(nxt, a.mW);
+        const unsigned long long nk = enc_rank(smn, H, W, qx, nxt - qx * W, a.mBS);
+        sn = (int)dense_slot(nk, a.V);
+        vn = tval(a.V, sn)[0];
+        dense_ensure(a.V, (uint32_t)sn, nk);
+    }
+    const int sv = (int)dense_slot(skj, a.V);
+    dense_ensure(a.V, (uint32_t)sv, skj);
+    const double td = (rw + a.gamma * vn) - tval(a.V, sv)[0];
+    int kk = (int)kTileNoAct;
+    if (act >= 0) {
+        if (wexit) {           // exit-forced: decide made no H lookup, the learn step inserts s
+            const uint32_t h = dense_slot(skj, a.Ht);
+            dense_ensure(a.Ht, h, skj);
+        }
+        kk = avalid ? act : (int)kTileNoAct;
+    }
+    TileRec rc;
+    rc.svk = (uint32_t)sv | ((uint32_t)kk << 28);
+    rc.snf = (sn >= 0 ? (uint32_t)sn : kTileTerminal) | ((uint32_t)wexit << 28) | ((uint32_t)(coll + 1) << 29);
+    rc.td = td;
+    a.trecs[e * A + r] = rc;
 }
 
 // ===========================================================================
@@ -3469,7 +3859,21 @@ __global__ __launch_bounds__(256) void learn_stencil_col_kernel(LearnArgs a, int
 
 constexpr int kSepStencilHW = 16384;
 
-template <int BS, int EPB, int APT, int D, bool DL>
+// The DFF stencil of large maps as its own all-cells launch (learn_stencil*_kernel).
+void launch_sep_stencil(const LearnArgs& a, hipStream_t s) {
+    const int tiles = (a.HW + 255) / 256;
+    if (a.W % 256 == 0 && !(FFM_LABLATE & 16)) {
+        const int segs = a.W / 256, strips = (a.H + 4 * kColRows - 1) / (4 * kColRows);
+        learn_stencil_col_kernel<<<dim3((unsigned)(strips * segs * a.E)), dim3(256), 0, s>>>(a, strips, segs);
+    } else if (a.W % 4 == 0) {
+        const int tiles4 = (a.HW / 4 + 255) / 256;
+        learn_stencil4_kernel<<<dim3((unsigned)(tiles4 * a.E)), dim3(256), 0, s>>>(a, tiles4);
+    } else {
+        learn_stencil_kernel<<<dim3((unsigned)(tiles * a.E)), dim3(256), 0, s>>>(a, tiles);
+    }
+}
+
+template <int BS, int EPB, int APT, int D, bool DL, int VK = 0>
 hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     LearnArgs a = a0;
     // the DFF lives in global memory (not DL) and the map is large: stencil apart
@@ -3477,25 +3881,47 @@ hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D, DL>),
+            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D, DL, VK>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
     const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
-    learn_batch_kernel<BS, EPB, APT, D, DL><<<dim3(blocks), dim3(BS), smem, s>>>(a);
-    if (a.sep_stencil) {
-        const int tiles = (a.HW + 255) / 256;
-        if (a.W % 256 == 0 && !(FFM_LABLATE & 16)) {
-            const int segs = a.W / 256, strips = (a.H + 4 * kColRows - 1) / (4 * kColRows);
-            learn_stencil_col_kernel<<<dim3((unsigned)(strips * segs * a.E)), dim3(256), 0, s>>>(a, strips, segs);
-        } else if (a.W % 4 == 0) {
-            const int tiles4 = (a.HW / 4 + 255) / 256;
-            learn_stencil4_kernel<<<dim3((unsigned)(tiles4 * a.E)), dim3(256), 0, s>>>(a, tiles4);
-        } else {
-            learn_stencil_kernel<<<dim3((unsigned)(tiles * a.E)), dim3(256), 0, s>>>(a, tiles);
-        }
-    }
+    learn_batch_kernel<BS, EPB, APT, D, DL, VK><<<dim3(blocks), dim3(BS), smem, s>>>(a);
+    if (a.sep_stencil) launch_sep_stencil(a, s);
     return hipGetLastError();
+}
+
+// The phase-split step (learn_phase_*_kernel); the DFF stencil always runs apart.
+hipError_t launch_batch_phases(const LearnArgs& a, hipStream_t s) {
+    const size_t smem = phase_resolve_carve(a.HW, a.A).total;
+    if (smem > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&learn_phase_resolve_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    const unsigned E = (unsigned)a.E;
+    const unsigned bpe = (unsigned)((a.A + kPhLanes - 1) / kPhLanes);
+    const unsigned G = (E * bpe + 7u) & ~7u;          // phase_block: a multiple of the 8 XCDs
+    learn_phase_prep_kernel<<<dim3(E), dim3(kPhBS), 0, s>>>(a);
+    learn_phase_decide_kernel<<<dim3(G), dim3(kPhLanes), 0, s>>>(a);
+    learn_phase_resolve_kernel<<<dim3(E), dim3(kPhBS), smem, s>>>(a);
+    learn_phase_learn_kernel<<<dim3(G), dim3(kPhLanes), 0, s>>>(a);
+    launch_sep_stencil(a, s);
+    return hipGetLastError();
+}
+
+// The kernel's VK = 1 shape: ffm_unified in an actor mode on dense tables with tiled
+// records (RASTER holds for every 1024-lane shape).  FFM_BATCH_UNI=0 keeps the generic kernel.
+bool learn_batch_uni(const LearnArgs& a) {
+    static const bool off = [] { const char* v = getenv("FFM_BATCH_UNI"); return v && v[0] == '0'; }();
+    return !off && FFM_RASTER && a.variant == kVarUnified && a.mode != kModeCritic && a.V.dense_by && a.Ht.dense_by &&
+           a.trecs != nullptr && !(FFM_LABLATE & 2);
+}
+
+// FFM_BATCH_PHASES=0 keeps the fused kernel for the phase-split shapes (A/B).
+bool learn_batch_phases_on() {
+    static const bool off = [] { const char* v = getenv("FFM_BATCH_PHASES"); return v && v[0] == '0'; }();
+    return !off;
 }
 
 // One agent per lane when A <= 1024; beyond that APT agents per lane of a
@@ -3523,9 +3949,13 @@ hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
         return launch_batch_t<256, 1, 1, D, false>(a, s);
     }
     if (A <= 1024) return launch_batch_t<1024, 1, 1, D, false>(a, s);
+    if (D == 1 && a.bph && learn_batch_uni(a) && learn_batch_phases_on()) return launch_batch_phases(a, s);
     if (A <= 2048) return launch_batch_t<1024, 1, 2, D, false>(a, s);
     if (A <= 4096) return launch_batch_t<1024, 1, 4, D, false>(a, s);
-    if (A <= 8192) return launch_batch_t<1024, 1, 8, D, false>(a, s);
+    if (A <= 8192) {
+        if (D == 1 && learn_batch_uni(a)) return launch_batch_t<1024, 1, 8, 1, false, 1>(a, s);
+        return launch_batch_t<1024, 1, 8, D, false>(a, s);
+    }
     return launch_batch_t<1024, 1, 16, D, false>(a, s);
 }
 
@@ -3536,6 +3966,11 @@ size_t learn_exact_scratch_bytes(int HW, int A) { return exact_carve(nullptr, HW
 int learn_batch_block_size(int A) { return A <= 64 ? 64 : A <= 256 ? 256 : 1024; }
 
 size_t learn_batch_smem_bytes(int HW, int A, int D) { return batch_carve(HW, A, D, 1).shared; }
+
+size_t learn_batch_phase_bytes(long long E, int HW, int A) {
+    if (A <= 1024 || A > 16383 || HW > 65536) return 0;
+    return (size_t)E * ((size_t)(HW + 15) / 16 * 8 + (size_t)A * 12);
+}
 
 bool learn_batch_supported(int HW, int A, int D) {
     return A <= 16383 && learn_batch_smem_bytes(HW, A, D) <= 160 * 1024;

@@ -235,6 +235,19 @@ def test_learner_philox_tiled_step_matches_cpu(mode):
                     max_steps=25, seed=6, env_base=77)
 
 
+@pytest.mark.parametrize("mode", ["actor_only", "both"])
+def test_learner_philox_phase_split_step_matches_cpu(mode):
+    """The phase-split batch step (prep / decide / resolve / learn launches,
+    taken by ffm_unified's actor modes above 1,024 agents per env with tiled records):
+    positions, DFF, V and H equal the CPU restatement bit for bit -- a square room, then an
+    odd width (state-map words across rows), spare agent capacity, env ids offset, episodes
+    through max_steps."""
+    p = {"epsilon": 0.1, "block_size": 1}
+    _philox_compare("unified", mode, p, 64, 64, 1500, 12, 30, max_steps=20, seed=4)
+    _philox_compare("unified", mode, dict(p, k_A=3.0, step_penalty=-1.0), 50, 77, 1300, 10, 26, A=2000,
+                    max_steps=12, seed=6, env_base=77)
+
+
 @pytest.mark.parametrize("H,W", [(70, 256), (40, 512)])
 def test_learner_philox_column_stencil_shapes(H, W):
     """The separate DFF stencil in row-segment strips (learn_stencil_col_kernel, W % 256 ==
@@ -334,8 +347,9 @@ def test_learner_tiled_shards_equal_one_learner(mode):
         L.close()
 
 
-@pytest.mark.parametrize("mode,world", [("actor_only", 3), ("both", 2), ("critic_only", 3), ("actor_only", 1)])
-def test_learner_owner_shards_equal_one_learner(mode, world):
+@pytest.mark.parametrize("mode,world,N", [("actor_only", 3, 600), ("both", 2, 600), ("critic_only", 3, 600),
+                                          ("actor_only", 1, 600), ("both", 3, 1500)])
+def test_learner_owner_shards_equal_one_learner(mode, world, N):
     """The owner-sharded tiled step (TableSync's exchange for tiled learners,
     coupled in one process): the 1,024 tiles of a 64x64 room are dealt to the shards in
     chunks of 64, each shard sums only its own tiles' records from every shard (all-to-all),
@@ -348,7 +362,7 @@ def test_learner_owner_shards_equal_one_learner(mode, world):
     s = l1_sff(m)
     p = {"epsilon": 0.1, "block_size": 1}
     sizes = {1: [16], 2: [9, 7], 3: [7, 5, 4]}[world]
-    n, N, T = sum(sizes), 600, 30
+    n, T = sum(sizes), 30
     kw = dict(mode=mode, params=p, rng="philox", seed=8, auto_reset=True, max_steps=20)
     one = _learner(m, s, "unified", n_envs=n, n_agents=N, **kw)
     assert one.tiled and one.tile_major
