@@ -27,7 +27,8 @@ struct LearnRec {
 struct TileRec {
     uint32_t svk;               // V / H slot of s (bits 0-27), action k (28-31; 15 = no H increment)
     uint32_t snf;               // V slot of s' (bits 0-27; 0x0FFFFFFF = terminal), wexit (28), coll + 1 (29-31)
-    double td;                  // TD error with the step-start V (ffm_unified both: the actor's td)
+    double td;                  // ffm_unified both: the TD error with the step-start V (the actor's td);
+                                // otherwise the TD target r + gamma V(s') (the V pass subtracts V(s))
 };
 constexpr int kTileCells = 4;   // cells per tile: a tile's slots are 256 rank patterns x 4 cells
 constexpr uint32_t kTileNoAct = 15u, kTileTerminal = 0x0FFFFFFFu;

@@ -1210,6 +1210,11 @@ __device__ __forceinline__ double env_epsilon(const LearnArgs& a, int k, long lo
     return e < 0.0 ? 0.0 : e > 1.0 ? 1.0 : e;
 }
 
+// Tiled records (TileRec::td) carry the TD target r + gamma V(s') instead of the TD error
+// unless the H pass needs the step-start error (ffm_unified both): the V pass reads V(s)
+// anyway and subtracts it there (record_td), with the same operands and rounding.
+__device__ __forceinline__ bool rec_target(const LearnArgs& a) { return a.mode != kModeBoth; }
+
 // One record per ended episode (ffm_learner_drain_episodes).
 __device__ __forceinline__ void log_episode(const LearnArgs& a, long long e) {
     const unsigned long long r = atomicAdd(a.eplog_n, 1ull);
@@ -1628,10 +1633,15 @@ void learn_batch_kernel(LearnArgs a) {
                 sv = tab_get(a.V, skj, a.overflow);
             }
             if (sv < 0) break;
-            const double td = (r + a.gamma * vn) - tval(a.V, sv)[0];
+            const double y = r + a.gamma * vn;
             vsl = sv;
-            vq = fx(td);
-            tdv = td;
+            if (TILED && rec_target(a)) {
+                tdv = y;           // the V pass subtracts V(s) (record_td): one table read less here
+            } else {
+                const double td = y - tval(a.V, sv)[0];
+                vq = fx(td);
+                tdv = td;
+            }
             snv = sn;
             if (!actor) break;
             if (BK_ACT(j) < 0) break;
@@ -1656,7 +1666,7 @@ void learn_batch_kernel(LearnArgs a) {
                 rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hslj; rc.k = BK_AVALID(j) ? BK_ACT(j) : -1;
                 a.recs[e * A + i] = rc;
             } else if (BK_AVALID(j) && !(FFM_LABLATE & 1)) {
-                acc_add(acc_at(a.Ht, (size_t)hslj * 5 + BK_ACT(j)), fx(a.alpha_h * td));
+                acc_add(acc_at(a.Ht, (size_t)hslj * 5 + BK_ACT(j)), fx(a.alpha_h * tdv));
             }
         } while (false);
         if (TILED) {
@@ -1902,23 +1912,53 @@ __global__ __launch_bounds__(kPhBS) void learn_phase_prep_kernel(LearnArgs a) {
     }
 }
 
-// Decide / learn workgroups: logical block b (256 consecutive ranks of one env) from
-// the launch's block with XCD-contiguous numbering, so one env's blocks share an L2.
-__device__ __forceinline__ bool phase_block(const LearnArgs& a, long long& e, int& r) {
-    const int bpe = (a.A + kPhLanes - 1) / kPhLanes;
-    const unsigned G8 = gridDim.x >> 3;
-    const unsigned b = (blockIdx.x & 7u) * G8 + (blockIdx.x >> 3);
-    e = (long long)(b / (unsigned)bpe);
-    r = (int)(b % (unsigned)bpe) * kPhLanes + (int)threadIdx.x;
-    return e < a.E;
+// Decide / learn work units: the agents of one env in one row-chunk of kPhUnitTiles tiles
+// (ranks from the records' tile offsets), one wave each, kPhWaves envs per workgroup.
+// Unit u runs on XCD u % 8 for all envs back to back, so the table rows of its cells
+// (slot = pattern * Q + cell) that many envs' agents read stay in that XCD's L2 -- in env
+// order they were fetched from HBM once per env (C5: L2 hit rate 0.3).
+constexpr int kPhUnitTiles = 64;      // 256 cells: one row at W = 256
+constexpr int kPhWaves = kPhLanes / 64;
+
+__device__ __forceinline__ bool phase_unit(const LearnArgs& a, long long& e, int& r0, int& r1) {
+    const int NU = (a.NT + kPhUnitTiles - 1) / kPhUnitTiles;
+    const unsigned EB = (unsigned)((a.E + kPhWaves - 1) / kPhWaves);
+    const unsigned x = blockIdx.x & 7u, k = blockIdx.x >> 3;
+    const int u = (int)(x + 8u * (k / EB));
+    e = (long long)(k % EB) * kPhWaves + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    if (u >= NU || e >= a.E) return false;
+    const int t0 = u * kPhUnitTiles, t1 = t0 + kPhUnitTiles < a.NT ? t0 + kPhUnitTiles : a.NT;
+    const uint16_t* ts = a.tstart + e * (a.NT + 1);
+    r0 = ts[t0];
+    r1 = ts[t1];
+    return true;
 }
+
+unsigned phase_unit_grid(const LearnArgs& a) {
+    const unsigned NU = (unsigned)((a.NT + kPhUnitTiles - 1) / kPhUnitTiles);
+    const unsigned EB = (unsigned)((a.E + kPhWaves - 1) / kPhWaves);
+    return 8u * ((NU + 7u) / 8u) * EB;
+}
+
+__device__ __forceinline__ void phase_decide_one(const LearnArgs& a, long long e, int r);
+__device__ __forceinline__ void phase_learn_one(const LearnArgs& a, long long e, int r);
 
 __global__ __launch_bounds__(kPhLanes) void learn_phase_decide_kernel(LearnArgs a) {
     long long e;
-    int r;
-    if (!phase_block(a, e, r)) return;
-    const int n = a.cnt[e];
-    if (r >= n) return;
+    int r0, r1;
+    if (!phase_unit(a, e, r0, r1)) return;
+    for (int r = r0 + (int)(threadIdx.x & 63); r < r1; r += 64) phase_decide_one(a, e, r);
+}
+
+__global__ __launch_bounds__(kPhLanes) void learn_phase_learn_kernel(LearnArgs a) {
+    long long e;
+    int r0, r1;
+    if (!phase_unit(a, e, r0, r1)) return;
+    for (int r = r0 + (int)(threadIdx.x & 63); r < r1; r += 64) phase_learn_one(a, e, r);
+}
+
+// One agent (raster rank r of env e): learn_batch_kernel's decide phase (D = 1, UNI).
+__device__ __forceinline__ void phase_decide_one(const LearnArgs& a, long long e, int r) {
     const int H = a.H, W = a.W, A = a.A;
     const PhaseCarve pc = phase_carve(a.bph, a.E, a.HW, A);
     const Sm2 sm{pc.sm + e * ((a.HW + 15) >> 4)};
@@ -2075,12 +2115,8 @@ __global__ __launch_bounds__(kPhBS) void learn_phase_resolve_kernel(LearnArgs a)
     }
 }
 
-__global__ __launch_bounds__(kPhLanes) void learn_phase_learn_kernel(LearnArgs a) {
-    long long e;
-    int r;
-    if (!phase_block(a, e, r)) return;
-    const int n = a.nstart[e];
-    if (r >= n) return;
+// One agent: learn_batch_kernel's learn phase (TD error, record).
+__device__ __forceinline__ void phase_learn_one(const LearnArgs& a, long long e, int r) {
     const int H = a.H, W = a.W, A = a.A;
     const PhaseCarve pc = phase_carve(a.bph, a.E, a.HW, A);
     const size_t mo = (size_t)e * ((a.HW + 15) >> 4);
@@ -2105,7 +2141,8 @@ __global__ __launch_bounds__(kPhLanes) void learn_phase_learn_kernel(LearnArgs a
     }
     const int sv = (int)dense_slot(skj, a.V);
     dense_ensure(a.V, (uint32_t)sv, skj);
-    const double td = (rw + a.gamma * vn) - tval(a.V, sv)[0];
+    const double y = rw + a.gamma * vn;
+    const double td = rec_target(a) ? y : y - tval(a.V, sv)[0];
     int kk = (int)kTileNoAct;
     if (act >= 0) {
         if (wexit) {           // exit-forced: decide made no H lookup, the learn step inserts s
@@ -2646,8 +2683,12 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     __syncthreads();
     const uint32_t Q = (a.V.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
-    auto add = [&](const TileRec& rc, uint32_t sv, int idx) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(rc.td));
+    // the record's td (rec_target: the target, minus V(s) at step start, read before any
+    // store of this pass)
+    const bool tgt = rec_target(a);
+    auto add = [&](const TileRec& rc, uint32_t sv, int idx, double vs) {
+        const double td = tgt ? rc.td - vs : rc.td;
+        atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(td));
         if (a.tile_ensure) {     // another rank's agent: its s and s' join this rank's V
             dense_ensure(a.V, sv, dense_key(sv, qsh, Q, a.V.dense_by));
             const uint32_t sn = rc.snf & 0x0FFFFFFFu;
@@ -2670,8 +2711,9 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
             const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
             ix[j] = tile_idx(sv, qsh, Q, c0);
             own[j] = atomicAdd(&ks[ix[j]], 1u) == 0u;
-            if (own[j]) vv[j] = tval(a.V, sv)[0];
-            add(rc[j], sv, ix[j]);
+            const double vs = tgt || own[j] ? tval(a.V, sv)[0] : 0.0;
+            if (own[j]) vv[j] = vs;
+            add(rc[j], sv, ix[j], vs);
         }
         __syncthreads();
         double nv[kTileJ];
@@ -2699,7 +2741,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
                 const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
                 const int idx = tile_idx(sv, qsh, Q, c0);
                 atomicAdd(&ks[idx], 1u);
-                add(rc[j], sv, idx);
+                add(rc[j], sv, idx, tgt ? tval(a.V, sv)[0] : 0.0);
             }
         }
         __syncthreads();
@@ -2709,7 +2751,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
             const uint32_t sv = rc.svk & 0x0FFFFFFFu;
             const int idx = tile_idx(sv, qsh, Q, c0);
             atomicAdd(&ks[idx], 1u);
-            add(rc, sv, idx);
+            add(rc, sv, idx, tgt ? tval(a.V, sv)[0] : 0.0);
         });
     }
     constexpr int kPer = NS / kTileThreads;
@@ -3900,8 +3942,7 @@ hipError_t launch_batch_phases(const LearnArgs& a, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     const unsigned E = (unsigned)a.E;
-    const unsigned bpe = (unsigned)((a.A + kPhLanes - 1) / kPhLanes);
-    const unsigned G = (E * bpe + 7u) & ~7u;          // phase_block: a multiple of the 8 XCDs
+    const unsigned G = phase_unit_grid(a);
     learn_phase_prep_kernel<<<dim3(E), dim3(kPhBS), 0, s>>>(a);
     learn_phase_decide_kernel<<<dim3(G), dim3(kPhLanes), 0, s>>>(a);
     learn_phase_resolve_kernel<<<dim3(E), dim3(kPhBS), smem, s>>>(a);
@@ -3918,10 +3959,11 @@ bool learn_batch_uni(const LearnArgs& a) {
            a.trecs != nullptr && !(FFM_LABLATE & 2);
 }
 
-// FFM_BATCH_PHASES=0 keeps the fused kernel for the phase-split shapes (A/B).
+// FFM_BATCH_PHASES=1 takes the phase-split step for its shapes (measured
+// slower than the fused VK = 1 kernel, so off by default); read at every launch.
 bool learn_batch_phases_on() {
-    static const bool off = [] { const char* v = getenv("FFM_BATCH_PHASES"); return v && v[0] == '0'; }();
-    return !off;
+    const char* v = getenv("FFM_BATCH_PHASES");
+    return v && v[0] == '1';
 }
 
 // One agent per lane when A <= 1024; beyond that APT agents per lane of a

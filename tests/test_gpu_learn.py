@@ -236,13 +236,19 @@ def test_learner_philox_tiled_step_matches_cpu(mode):
 
 
 @pytest.mark.parametrize("mode", ["actor_only", "both"])
-def test_learner_philox_phase_split_step_matches_cpu(mode):
+def test_learner_philox_phase_split_step_matches_cpu(monkeypatch, mode):
     """The phase-split batch step (prep / decide / resolve / learn launches,
     taken by ffm_unified's actor modes above 1,024 agents per env with tiled records):
     positions, DFF, V and H equal the CPU restatement bit for bit -- a square room, then an
     odd width (state-map words across rows), spare agent capacity, env ids offset, episodes
-    through max_steps."""
+    through max_steps.  Then the fused kernel's compile-time ffm_unified form (the default
+    for these shapes) on the same cases."""
     p = {"epsilon": 0.1, "block_size": 1}
+    monkeypatch.setenv("FFM_BATCH_PHASES", "1")
+    _philox_compare("unified", mode, p, 64, 64, 1500, 12, 30, max_steps=20, seed=4)
+    _philox_compare("unified", mode, dict(p, k_A=3.0, step_penalty=-1.0), 50, 77, 1300, 10, 26, A=2000,
+                    max_steps=12, seed=6, env_base=77)
+    monkeypatch.delenv("FFM_BATCH_PHASES")
     _philox_compare("unified", mode, p, 64, 64, 1500, 12, 30, max_steps=20, seed=4)
     _philox_compare("unified", mode, dict(p, k_A=3.0, step_penalty=-1.0), 50, 77, 1300, 10, 26, A=2000,
                     max_steps=12, seed=6, env_base=77)
