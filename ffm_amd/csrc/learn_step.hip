@@ -200,6 +200,38 @@ __device__ int tab_get(const LearnTable& T, unsigned long long key, int* overflo
     return -1;
 }
 
+// Home-slot look of a hashed table, free of side effects: the key and the first W values
+// of the key's home slot in one round trip (a record is one line).  True when the key sits
+// there -- the common case -- and v then holds its values (values never change during a
+// step; an empty slot already holds the default).  Otherwise the caller takes tab_get
+// (probe, insert), so a lookup costs one dependent round trip instead of two (key, then
+// values), and independent lookups issue together.
+template <int W>
+__device__ __forceinline__ bool tab_peek(const LearnTable& T, unsigned long long key, uint32_t& h, double (&v)[W]) {
+    h = (uint32_t)mix64(key) & T.mask;
+    const unsigned long long* r = T.rec + (size_t)h * T.stride;
+    const unsigned long long k = r[0];
+#pragma unroll
+    for (int i = 0; i < W; i++) v[i] = __longlong_as_double((long long)r[1 + i]);
+    return k == key;
+}
+
+// tab_peek, then tab_get when the key is not at its home slot: the slot (-1: table full)
+// with the W values loaded.
+template <int W>
+__device__ __forceinline__ int tab_get_row(const LearnTable& T, unsigned long long key, int* overflow,
+                                           double (&v)[W]) {
+    uint32_t h;
+    if (tab_peek<W>(T, key, h, v)) return (int)h;
+    const int s = tab_get(T, key, overflow);
+    if (s >= 0) {
+        const double* p = tval(T, s);
+#pragma unroll
+        for (int i = 0; i < W; i++) v[i] = p[i];
+    }
+    return s;
+}
+
 // Slot of `key`, or -1 when absent (read-only tables: ffm_trained_core).
 __device__ int tab_find(const LearnTable& T, unsigned long long key) {
     if (T.dense_by) {
@@ -1477,10 +1509,11 @@ void learn_batch_kernel(LearnArgs a) {
                     actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, false, P);
                     dense_ensure(a.Ht, (uint32_t)h, sk);
                 } else {
-                    const int h = tab_get(a.Ht, sk, a.overflow);
+                    double hr[5];
+                    const int h = tab_get_row<5>(a.Ht, sk, a.overflow, hr);
                     if (KEYS) hsl[j] = h;
                     if (h < 0) continue;
-                    actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, false, P);
+                    actor_policy(a, hr, coord, valid, dff, hs, false, P);
                 }
                 DrawPh rng(a, genv, (uint32_t)i);
                 k = policy_draw(P, eps, rng);
@@ -1491,10 +1524,11 @@ void learn_batch_kernel(LearnArgs a) {
             // model/ffm_actor_only.py:214-355: decisions for the neighbours before the
             // first exit, then the exit for the rest; the last one is the agent's action.
             if (ex != 0) {
-                const int h = tab_get(a.Ht, sk, a.overflow);
+                double hr[5];
+                const int h = tab_get_row<5>(a.Ht, sk, a.overflow, hr);
                 if (KEYS) hsl[j] = h;
                 if (h < 0) continue;
-                actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, true, P);
+                actor_policy(a, hr, coord, valid, dff, hs, true, P);
             }
             int k = 4;
             uint32_t kmi = 0u;
@@ -1611,26 +1645,45 @@ void learn_batch_kernel(LearnArgs a) {
             double r = a.step_penalty;
             if (BK_WEXIT(j)) r = r + a.exit_reward;
             if (BK_COLL(j) >= 0) r = r + (double)BK_COLL(j) * a.collision_penalty;
-            int sn = -1;
-            double vn = 0.0;
+            int sn = -1, sv;
+            double vn = 0.0, vs = 0.0;
+            unsigned long long nk = 0;
             if (!BK_WEXIT(j)) {
                 const int nx = fdiv(BK_NXT(j), a.mW), ny = BK_NXT(j) - nx * W;
-                const unsigned long long nk = encode_v(a, variant, smn, nx, ny);
-                if (vdense) {
+                nk = encode_v(a, variant, smn, nx, ny);
+            }
+            if (vdense) {
+                if (!BK_WEXIT(j)) {
                     sn = (int)dense_slot(nk, a.V);
                     vn = tval(a.V, sn)[0];
                     dense_ensure(a.V, (uint32_t)sn, nk);
-                } else {
-                    sn = tab_get(a.V, nk, a.overflow);
-                    vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
                 }
-            }
-            int sv;
-            if (vdense) {
                 sv = (int)dense_slot(skj, a.V);
                 dense_ensure(a.V, (uint32_t)sv, skj);
+                if (!(TILED && rec_target(a))) vs = tval(a.V, sv)[0];
             } else {
-                sv = tab_get(a.V, skj, a.overflow);
+                // both home slots in one round trip; the probing / inserting path only for
+                // keys away from home, s' before s as before
+                uint32_t hn, hv;
+                double pn[1], pv[1];
+                const bool okn = tab_peek<1>(a.V, nk, hn, pn);
+                const bool okv = tab_peek<1>(a.V, skj, hv, pv);
+                if (!BK_WEXIT(j)) {
+                    if (okn) {
+                        sn = (int)hn;
+                        vn = pn[0];
+                    } else {
+                        sn = tab_get(a.V, nk, a.overflow);
+                        vn = sn >= 0 ? tval(a.V, sn)[0] : 0.0;
+                    }
+                }
+                if (okv) {
+                    sv = (int)hv;
+                    vs = pv[0];
+                } else {
+                    sv = tab_get(a.V, skj, a.overflow);
+                    if (sv >= 0) vs = tval(a.V, sv)[0];
+                }
             }
             if (sv < 0) break;
             const double y = r + a.gamma * vn;
@@ -1638,7 +1691,7 @@ void learn_batch_kernel(LearnArgs a) {
             if (TILED && rec_target(a)) {
                 tdv = y;           // the V pass subtracts V(s) (record_td): one table read less here
             } else {
-                const double td = y - tval(a.V, sv)[0];
+                const double td = y - vs;
                 vq = fx(td);
                 tdv = td;
             }
