@@ -119,10 +119,17 @@ struct ffm_learner {
     size_t ocap = 0;
     double* d_tsum = nullptr;                // [ths][5] this rank's tile summaries
     unsigned char* d_bph = nullptr;          // the phase-split batch step's per-env state (learn_batch_phases)
+    uint16_t* d_tstartT = nullptr;           // [NT + 1][E] transposed tile offsets (one-device env-major passes)
     const ffm::TileRec* own_recs = nullptr;  // the received records of the current owner step
     const uint32_t* own_hdr = nullptr;
     DevTable V, H;
 };
+
+// FFM_TSTART_T=0: the env-major tile passes read the [E][NT + 1] offsets (A/B).
+static bool tstart_t_off() {
+    const char* v = getenv("FFM_TSTART_T");
+    return v && v[0] == '0';
+}
 
 static void free_traj(ffm_learner* l) {
     void* bufs[] = {(void*)l->traj.envs, (void*)l->traj.phase, l->traj.meta, l->traj.cells, l->traj.n};
@@ -146,7 +153,7 @@ static void release(ffm_learner* l) {
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
                     l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand,
                     l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_pack, l->d_xcnt, l->d_newv, l->d_newh,
-                    l->d_vslot, l->d_vval, l->d_hkey, l->d_hq, l->d_on, l->d_tsum, l->d_bph};
+                    l->d_vslot, l->d_vval, l->d_hkey, l->d_hq, l->d_on, l->d_tsum, l->d_bph, l->d_tstartT};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
     free_traj(l);
@@ -237,6 +244,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.mBS = magic(a.bs);
     a.trecs = nullptr;       // the accumulator path unless a tiled step sets it
     a.tstart = l->d_tstart;
+    a.tstartT = nullptr;     // set by the one-device tiled step after its transpose
     a.bph = l->d_bph;
     a.tstats = l->d_tstats;
     a.tdirty = l->d_tdirty;
@@ -433,6 +441,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         l->ths = l->NT + 1;
         if (hipMalloc((void**)&l->d_trecs, E * A * sizeof(ffm::TileRec)) != hipSuccess ||
             hipMalloc((void**)&l->d_tstart, E * (size_t)(l->NT + 1) * 2) != hipSuccess ||
+            hipMalloc((void**)&l->d_tstartT, E * (size_t)(l->NT + 1) * 2) != hipSuccess ||
             hipMalloc((void**)&l->d_tstats, (size_t)l->NT * 32) != hipSuccess ||
             hipMalloc((void**)&l->d_tdirty, (size_t)l->NT * 4) != hipSuccess ||
             hipMalloc((void**)&l->d_tcand, (size_t)(l->NT + 1) * 4) != hipSuccess ||
@@ -612,6 +621,9 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
                 a.thdr = l->d_hdr;
                 a.tR = 1;
                 a.NTk = l->NT;
+            } else if (!tstart_t_off()) {   // env-major passes read the tile offsets transposed
+                HIP_TRY(ffm::launch_learn_tstart_transpose(a, l->d_tstartT, s));
+                a.tstartT = l->d_tstartT;
             }
             HIP_TRY(ffm::launch_learn_tiles(a, false, s));
             if (int rc = phase_end(l, s)) return rc;

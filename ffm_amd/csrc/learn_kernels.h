@@ -100,6 +100,9 @@ struct LearnArgs {
     LearnRec* recs;             // [E][A]
     TileRec* trecs;             // [E][A] tiled step: per-agent records in raster order (nullptr: off)
     uint16_t* tstart;           // [E][NT + 1] tiled step: agents of env e in cells < kTileCells * t (A <= 16384)
+    // the same transposed, [NT + 1][E] (one device, env-major passes): a tile's ranges of
+    // all envs are contiguous, so a pass loads them coalesced.  nullptr: read tstart.
+    const uint16_t* tstartT;
     double* tstats;             // [NT][4] tiled step: per-tile H summary (present, non-finite, min, max)
     int* tdirty;                // [NT] tiled step: bit 0 max, 1 min, 2 non-finite flag only a bound (stale)
     int* tcand;                 // [NT + 1] tiled step: tiles to rescan ([0] = count, then the tiles)
@@ -191,6 +194,8 @@ bool learn_batch_raster(int HW, int A, int D);
 // Bytes of LearnArgs::bph for a tiled learner of E envs (0: the shape keeps the fused kernel).
 size_t learn_batch_phase_bytes(long long E, int HW, int A);
 hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s);
+// tstart [E][NT + 1] -> out [NT + 1][E] (LearnArgs::tstartT)
+hipError_t launch_learn_tstart_transpose(const LearnArgs& a, uint16_t* out, hipStream_t s);
 // tile-major records: the column scan, the tile offsets in destination order (per-destination
 // headers, hdr row stride ths, and record counts xcnt[ow]) and the scatter of trecs into out.
 // pe [E][NT], tpre [NT], toff [NT + 2 * ceil(NT / kOwnChunk)] words.

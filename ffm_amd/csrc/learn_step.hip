@@ -2602,9 +2602,14 @@ __device__ __forceinline__ TileRanges tile_ranges(const LearnArgs& a, int t, lon
         r.lo[j] = 0;
         r.n[j] = 0;
         if (e < a.E) {
-            const uint16_t* ts = a.tstart + e * (a.NT + 1) + t;
-            r.lo[j] = ts[0];
-            r.n[j] = ts[1] - r.lo[j];
+            if (a.tstartT) {       // tile-major offsets: the block's loads are contiguous
+                r.lo[j] = a.tstartT[(long long)t * a.E + e];
+                r.n[j] = a.tstartT[(long long)(t + 1) * a.E + e] - r.lo[j];
+            } else {
+                const uint16_t* ts = a.tstart + e * (a.NT + 1) + t;
+                r.lo[j] = ts[0];
+                r.n[j] = ts[1] - r.lo[j];
+            }
         }
     }
     const int c = r.n[0] + r.n[1];
@@ -3952,6 +3957,26 @@ __global__ __launch_bounds__(256) void learn_stencil_col_kernel(LearnArgs a, int
     }
 }
 
+// tstart [E][NT + 1] -> [NT + 1][E] through a 64 x 64 LDS tile (both sides coalesced).
+__global__ __launch_bounds__(256) void learn_tstart_transpose_kernel(const uint16_t* in, uint16_t* out, long long E,
+                                                                     int NT1) {
+    __shared__ uint16_t tl[64][66];
+    const int t0 = (int)blockIdx.x * 64;
+    const long long e0 = (long long)blockIdx.y * 64;
+    const int lx = (int)threadIdx.x & 63, ly = (int)threadIdx.x >> 6;
+    for (int i = ly; i < 64; i += 4) {
+        const long long e = e0 + i;
+        const int t = t0 + lx;
+        tl[i][lx] = e < E && t < NT1 ? in[e * NT1 + t] : (uint16_t)0;
+    }
+    __syncthreads();
+    for (int i = ly; i < 64; i += 4) {
+        const int t = t0 + i;
+        const long long e = e0 + lx;
+        if (t < NT1 && e < E) out[(long long)t * E + e] = tl[lx][i];
+    }
+}
+
 constexpr int kSepStencilHW = 16384;
 
 // The DFF stencil of large maps as its own all-cells launch (learn_stencil*_kernel).
@@ -4137,6 +4162,13 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_tstart_transpose(const LearnArgs& a, uint16_t* out, hipStream_t s) {
+    const int NT1 = a.NT + 1;
+    learn_tstart_transpose_kernel<<<dim3((unsigned)((NT1 + 63) / 64), (unsigned)((a.E + 63) / 64)), dim3(256), 0, s>>>(
+        a.tstart, out, a.E, NT1);
     return hipGetLastError();
 }
 
