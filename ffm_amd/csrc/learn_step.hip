@@ -3964,12 +3964,17 @@ __global__ __launch_bounds__(256) void learn_tstart_transpose_kernel(const uint1
     const int t0 = (int)blockIdx.x * 64;
     const long long e0 = (long long)blockIdx.y * 64;
     const int lx = (int)threadIdx.x & 63, ly = (int)threadIdx.x >> 6;
-    for (int i = ly; i < 64; i += 4) {
-        const long long e = e0 + i;
+    uint16_t v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {     // every load in flight before the first LDS store
+        const long long e = e0 + ly + 4 * q;
         const int t = t0 + lx;
-        tl[i][lx] = e < E && t < NT1 ? in[e * NT1 + t] : (uint16_t)0;
+        v[q] = e < E && t < NT1 ? in[e * NT1 + t] : (uint16_t)0;
     }
+#pragma unroll
+    for (int q = 0; q < 16; q++) tl[ly + 4 * q][lx] = v[q];
     __syncthreads();
+#pragma unroll
     for (int i = ly; i < 64; i += 4) {
         const int t = t0 + i;
         const long long e = e0 + lx;
