@@ -3224,13 +3224,116 @@ __device__ __forceinline__ void tile_summary(const LearnArgs& a, int t, double4&
     d = a.tdirty[t];
 }
 
+// The candidates' non-finite word beside the partials (hpart[6..7]): learn_tile_final_kernel
+// ORs it into the statistics.
+__device__ __forceinline__ int* cand_nf(const LearnArgs& a) { return reinterpret_cast<int*>(a.hpart + 6); }
+
+// The candidate scan on the whole chip (learn_tile_cand_kernel's two passes as two launches):
+// per-block min / max over the clean tiles, then every block reduces those partials and lists
+// its stale tiles that could still hold the table's extreme.  One workgroup took 21 us at
+// C5 (16,384 tiles), mostly its own load latency.
+constexpr int kCandPartThreads = 256, kCandPartTiles = 4;   // tiles per thread
+constexpr int kCandPartMax = 512;                            // partial blocks (hpart[8 ..))
+
+__global__ __launch_bounds__(kCandPartThreads) void learn_tile_cand_part_kernel(LearnArgs a) {
+    __shared__ double smn[kCandPartThreads / 64], smx[kCandPartThreads / 64];
+    const int tid = (int)threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0) {
+        a.tcand[0] = 0;
+        cand_nf(a)[0] = 0;
+    }
+    double cmn = __builtin_inf(), cmx = -__builtin_inf();
+    double4 ts[kCandPartTiles];
+    int d[kCandPartTiles];
+#pragma unroll
+    for (int u = 0; u < kCandPartTiles; u++) {
+        const int t = ((int)blockIdx.x * kCandPartTiles + u) * kCandPartThreads + tid;
+        d[u] = 3;
+        if (t < a.NT) tile_summary(a, t, ts[u], d[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kCandPartTiles; u++) {
+        if (d[u] == 3 || ts[u].x == 0.0) continue;
+        if (!(d[u] & 1)) cmx = ts[u].w > cmx ? ts[u].w : cmx;
+        if (!(d[u] & 2)) cmn = ts[u].z < cmn ? ts[u].z : cmn;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(cmn, o), b2 = __shfl_xor(cmx, o);
+        cmn = a2 < cmn ? a2 : cmn;
+        cmx = b2 > cmx ? b2 : cmx;
+    }
+    if ((tid & 63) == 0) { smn[tid >> 6] = cmn; smx[tid >> 6] = cmx; }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kCandPartThreads / 64; w++) {
+            cmn = smn[w] < cmn ? smn[w] : cmn;
+            cmx = smx[w] > cmx ? smx[w] : cmx;
+        }
+        a.hpart[8 + 2 * blockIdx.x] = cmn;
+        a.hpart[9 + 2 * blockIdx.x] = cmx;
+    }
+}
+
+__global__ __launch_bounds__(kCandPartThreads) void learn_tile_cand_list_kernel(LearnArgs a) {
+    __shared__ int sfl[kCandPartThreads / 64];
+    const int tid = (int)threadIdx.x, lane = tid & 63;
+    // every block reduces the partials (a few hundred words, L2-resident)
+    double cmn = __builtin_inf(), cmx = -__builtin_inf();
+    for (int b = lane; b < (int)gridDim.x; b += 64) {
+        const double x = a.hpart[8 + 2 * b], y = a.hpart[9 + 2 * b];
+        cmn = x < cmn ? x : cmn;
+        cmx = y > cmx ? y : cmx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_xor(cmn, o), b2 = __shfl_xor(cmx, o);
+        cmn = a2 < cmn ? a2 : cmn;
+        cmx = b2 > cmx ? b2 : cmx;
+    }
+    int nf = 0;
+#pragma unroll
+    for (int u = 0; u < kCandPartTiles; u++) {
+        const int t = ((int)blockIdx.x * kCandPartTiles + u) * kCandPartThreads + tid;
+        double4 ts;
+        int d = -1;
+        if (t < a.NT) tile_summary(a, t, ts, d);
+        bool c = false;
+        if (d >= 0) {
+            c = ts.x != 0.0 && (((d & 1) && ts.w >= cmx) || ((d & 2) && ts.z <= cmn) || ((d & 4) && ts.y != 0.0));
+            if (!c) nf |= ts.x != 0.0 && ts.y != 0.0;
+        }
+        const unsigned long long m = __ballot(c);
+        if (m) {             // wave-aggregated append
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&a.tcand[0], __popcll(m));
+            base = __shfl(base, 0);
+            if (c) a.tcand[1 + base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = t;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) nf |= __shfl_xor(nf, o);
+    if (lane == 0) sfl[tid >> 6] = nf;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kCandPartThreads / 64; w++) nf |= sfl[w];
+        if (nf) atomicOr(cand_nf(a), 1);
+        if (blockIdx.x == 0) {
+            a.hpart[0] = cmn;
+            a.hpart[1] = cmx;
+            a.hpart[2] = 0.0;    // the non-finite flags: cand_nf
+        }
+    }
+}
+
 __global__ __launch_bounds__(kCandThreads) void learn_tile_cand_kernel(LearnArgs a, int all) {
     constexpr int NW = kCandThreads / 64;
     __shared__ double smn[NW], smx[NW];
     __shared__ int sfl[NW];
     __shared__ int ncand;
     const int tid = (int)threadIdx.x;
-    if (tid == 0) ncand = 0;
+    if (tid == 0) {
+        ncand = 0;
+        cand_nf(a)[0] = 0;
+    }
     double cmn = __builtin_inf(), cmx = -__builtin_inf();   // over exact (clean) tiles
     if (!all) {
         for (int t0 = tid; t0 < a.NT; t0 += kCandUnroll * kCandThreads) {
@@ -3296,6 +3399,19 @@ __global__ __launch_bounds__(kCandThreads) void learn_tile_cand_kernel(LearnArgs
     }
 }
 
+// The candidates of this step's statistics (every tile when `all`) on the whole chip, or
+// in one workgroup (FFM_CAND_ONE=1 for A/B).
+void launch_tile_cands(const LearnArgs& a, hipStream_t s) {
+    const char* v = getenv("FFM_CAND_ONE");
+    const unsigned nb = (unsigned)((a.NT + kCandPartThreads * kCandPartTiles - 1) / (kCandPartThreads * kCandPartTiles));
+    if ((v && v[0] == '1') || nb > kCandPartMax) {
+        learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
+        return;
+    }
+    learn_tile_cand_part_kernel<<<dim3(nb), dim3(kCandPartThreads), 0, s>>>(a);
+    learn_tile_cand_list_kernel<<<dim3(nb), dim3(kCandPartThreads), 0, s>>>(a);
+}
+
 __global__ __launch_bounds__(kTileThreads) void learn_tile_rescan_kernel(LearnArgs a) {
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
@@ -3310,7 +3426,7 @@ __global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
     __shared__ double smn[4], smx[4];
     __shared__ int snf[4];
     double mn = a.hpart[0], mx = a.hpart[1];
-    int nf = a.hpart[2] != 0.0;
+    int nf = a.hpart[2] != 0.0 || cand_nf(a)[0] != 0;
     const int n = a.tcand[0];
     for (int c = threadIdx.x; c < n; c += 256) {
         const double* ts = a.tstats + 4 * (size_t)a.tcand[1 + c];
@@ -4163,7 +4279,7 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
             learn_tile_h_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
             learn_tile_h_wide_kernel<false><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         }
-        learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
+        launch_tile_cands(a, s);
         learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
@@ -4215,7 +4331,7 @@ hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStrea
 
 hipError_t launch_learn_tile_stats(const LearnArgs& a, hipStream_t s) {
     const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
-    learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 0);
+    launch_tile_cands(a, s);
     learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
     learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     return hipGetLastError();
