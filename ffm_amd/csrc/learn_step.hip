@@ -1351,7 +1351,14 @@ void learn_batch_kernel(LearnArgs a) {
 #endif
     LSTAMP(0);
 
-    for (int c = tid; c < HW; c += LPE) grid[c] = (uint16_t)((map2_at(a.map2, c) << 14) | kGIdx);
+    {   // map classes into the grid two cells per dword (one map word covers eight pairs)
+        uint32_t* g32 = reinterpret_cast<uint32_t*>(grid);
+        for (int c2 = tid; c2 < HW / 2; c2 += LPE) {
+            const uint32_t m = a.map2[c2 >> 3] >> ((c2 & 7) << 2);
+            g32[c2] = (((m & 3u) << 14) | kGIdx) | ((((m >> 2) & 3u) << 14 | kGIdx) << 16);
+        }
+        if ((HW & 1) && tid == 0) grid[HW - 1] = (uint16_t)((map2_at(a.map2, HW - 1) << 14) | kGIdx);
+    }
     if (DL) {
         const float* src = a.dff_in + (live ? e : 0) * (long long)HW;
         for (int c = tid; c < HW; c += LPE) dff[c] = src[c];
@@ -1391,37 +1398,52 @@ void learn_batch_kernel(LearnArgs a) {
         const int pj = i < n ? a.pos[e * A + i] : 0;
         pa[j] = (uint32_t)pj | ((uint32_t)i << 16);
         sa[j] = 0u;
-        if (i < n) grid[pj] = (uint16_t)((grid[pj] & ~kGIdx) | (uint32_t)i);
+        if (i < n) {
+            grid[pj] = (uint16_t)((grid[pj] & ~kGIdx) | (uint32_t)i);
+            if (RASTER) atomicOr(&bits[pj >> 5], 1u << (pj & 31));   // occupancy, for the raster pass
+        }
     }
     if (RASTER) {
         __syncthreads();
-        // wave w of the env lists cells [w * cpw, (w + 1) * cpw) in two passes
-        // (count, then place) of 64 consecutive cells per round; the list lives in req
-        // (A * D >= n entries) until decide overwrites it.
+        // the occupied cells in raster order from the occupancy words (held in `bits` until
+        // the resolve phase needs it): lane l of wave w owns K consecutive words, a scan of
+        // the lanes' counts gives each its first rank, and its set bits are listed in order;
+        // the list lives in req (A * D >= n entries) until decide overwrites it.
         constexpr int NW = LPE / 64;
         const int w = tid >> 6, lane = tid & 63;
-        const int cpw = ((HW + NW * 64 - 1) / (NW * 64)) * 64;
-        const int c0 = w * cpw, c1 = min(c0 + cpw, HW);
-        int cnt = 0;
-        for (int c = c0 + lane; c - lane < c1; c += 64)
-            cnt += __popcll(__ballot(c < c1 && (grid[c] & kGIdx) != kGIdx));
-        if (lane == 0) ws[w] = cnt;
-        __syncthreads();
-        int base = 0;
+        const int nwords = (HW + 31) / 32;
+        const int wpw = (nwords + NW - 1) / NW, K = (wpw + 63) / 64;
+        const int lw0 = w * wpw + lane * K;
+        const int lw1 = min(min(lw0 + K, (w + 1) * wpw), nwords);
+        int lc = 0;
+        for (int q = lw0; q < lw1; q++) lc += __popc(bits[q]);
+        int incl = lc;
 #pragma unroll
-        for (int q = 0; q < NW; q++) base += q < w ? ws[q] : 0;
-        for (int c = c0 + lane; c - lane < c1; c += 64) {
-            const bool f = c < c1 && (grid[c] & kGIdx) != kGIdx;
-            const unsigned long long m = __ballot(f);
-            if (f) req[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)c;
-            if (a.trecs && lane < 64 / kTileCells) {
-                // tiled step: the raster rank of the first agent of each tile of this 64-cell chunk
-                const int tc = c - lane + kTileCells * lane;
-                if (tc < c1)
-                    a.tstart[e * (a.NT + 1) + tc / kTileCells] =
-                        (uint16_t)(base + __popcll(m & ((1ull << (kTileCells * lane)) - 1ull)));
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) ws[w] = incl;
+        __syncthreads();
+        int off = incl - lc;
+#pragma unroll
+        for (int q = 0; q < NW; q++) off += q < w ? ws[q] : 0;
+        for (int q = lw0; q < lw1; q++) {
+            uint32_t m = bits[q];
+            if (a.trecs) {      // tiled step: the raster rank of the first agent of each tile
+#pragma unroll
+                for (int tt = 0; tt < 32 / kTileCells; tt++) {
+                    const int tc = q * 32 + tt * kTileCells;
+                    if (tc < HW)
+                        a.tstart[e * (a.NT + 1) + tc / kTileCells] =
+                            (uint16_t)(off + __popc(m & ((1u << (tt * kTileCells)) - 1u)));
+                }
             }
-            base += __popcll(m);
+            while (m) {
+                const int b = __builtin_ctz(m);
+                m &= m - 1u;
+                req[off++] = (uint16_t)(q * 32 + b);
+            }
         }
         if (a.trecs && tid == 0) a.tstart[e * (a.NT + 1) + a.NT] = (uint16_t)n;
         __syncthreads();
@@ -1433,6 +1455,7 @@ void learn_batch_kernel(LearnArgs a) {
         }
         __syncthreads();   // the list is read: decide may write req
         for (int c = tid; c < n; c += LPE) req[c] = kNone16;
+        for (int c = tid; c < nwords; c += LPE) bits[c] = 0u;   // the next-state bits start empty
         __syncthreads();
     }
     const bool trained = variant == kVarTrained;
