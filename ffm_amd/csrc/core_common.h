@@ -240,6 +240,20 @@ __device__ __forceinline__ uint32_t slot_cell(uint32_t slot, int pp, int PW) {
     return slot <= (uint32_t)NB ? (uint32_t)(pp + off) : slot;
 }
 
+// slot_cell with the padded row stride known at compile time: the four Neumann offsets
+// (U, D, L, R: -PW, +PW, -1, +1; stay 0) as 6-bit fields of one constant, read by one
+// signed bit-field extract instead of a compare-and-select per direction.
+template <int NB, int PW>
+__device__ __forceinline__ uint32_t slot_cell_k(uint32_t slot, int pp) {
+    if constexpr (NB == 4 && PW <= 31) {
+        constexpr uint32_t K = ((uint32_t)(-PW) & 63u) | (((uint32_t)PW & 63u) << 6) | (63u << 12) | (1u << 18);
+        const int off = __builtin_amdgcn_sbfe((int)K, slot * 6u, 6u);
+        return slot <= 4u ? (uint32_t)(pp + off) : slot;
+    } else {
+        return slot_cell<NB>(slot, pp, PW);
+    }
+}
+
 // The requesters of target r (padded): agents adjacent to r whose request is r.
 // who[s] = agent index at r - off(s) (or 0xFFFF), is[s] = it requests r.
 template <int NB, class GT, class RT = uint16_t>

@@ -293,7 +293,7 @@ void core_group_kernel(CoreStepArgs a) {
                 const bool to_exit = (cr[c] & 16u) != 0u;
                 const uint32_t slot = sd == DirCodes::kNoDir ? (uint32_t)kNoReq : sd;
                 const uint16_t* gk = grid + s * PHW;
-                const int r = (int)slot_cell<NB>(slot, pp, PW);
+                const int r = (int)slot_cell_k<NB, PW>(slot, pp);
                 const bool req = slot <= (uint32_t)NB;
                 const bool moving = req && r != pp;
                 bool granted = req && !moving;   // a stay is always granted

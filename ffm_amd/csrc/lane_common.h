@@ -115,11 +115,12 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
     }
     bool v[NB + 1];
     v[NB] = true;
-    int nvalid = 0, exit_slot = -1;
+    bool anyv = false;     // a valid neighbour (a lane-mask OR, not a per-lane count)
+    int exit_slot = -1;
 #pragma unroll
     for (int s = NB - 1; s >= 0; s--) {
         v[s] = g[s] == 0u || g[s] == 3u;                                 // :52-60
-        nvalid += v[s] ? 1 : 0;
+        anyv = anyv || v[s];
         exit_slot = g[s] == 3u ? s : exit_slot;                          // :66-72
     }
     float scm[NB + 1];
@@ -135,7 +136,8 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k <= NB; k++) {
-        acc += __builtin_amdgcn_exp2f((scm[k] - mx) * 1.44269504088896341f);
+        const float x = __builtin_amdgcn_exp2f((scm[k] - mx) * 1.44269504088896341f);
+        acc = k == 0 ? x : acc + x;      // exp2 is never -0: 0 + x == x, one add fewer
         cum[k] = acc;
     }
     const float uf = (float)(wx >> 8) * 0x1p-24f;
@@ -150,7 +152,7 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
         cs = ge ? cum[k] : cs;
     }
     to_exit = exit_slot >= 0;
-    return nvalid == 0 ? (uint32_t)kNoReq                                // :63
+    return !anyv ? (uint32_t)kNoReq                                      // :63
            : exit_slot >= 0 ? (uint32_t)exit_slot                        // :66-72, no draw
            : cs > t + d ? (uint32_t)slot : (uint32_t)kPending;
 }
