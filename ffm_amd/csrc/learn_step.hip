@@ -3899,12 +3899,20 @@ __global__ __launch_bounds__(256) void learn_dense_adopt_kernel(LearnTable T, co
 // ranks F/64 keys against all F in LDS), instead of one workgroup per env.
 constexpr int kResetSmallF = 256;
 
+// Envs per reset wave: the wave re-places its ended envs one after the other, so the
+// launch lasts as long as the wave with the most (C4: ~2 % of 65,536 envs end per step;
+// 64 envs per wave left the slowest wave ~6 placements; reset kernel 12.6 -> 10.6 us at 8).
+#ifndef FFM_RESET_ENVS
+#define FFM_RESET_ENVS 8
+#endif
+constexpr int kResetSmallEnvs = FFM_RESET_ENVS;
+
 __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int all) {
     __shared__ __attribute__((aligned(16))) unsigned long long keys[kResetSmallF + 2];
     const int lane = threadIdx.x;
-    const long long e0 = (long long)blockIdx.x * 64;
+    const long long e0 = (long long)blockIdx.x * kResetSmallEnvs;
     const long long me = e0 + lane;
-    const bool want = me < a.E && (all || a.done[me]);
+    const bool want = lane < kResetSmallEnvs && me < a.E && (all || a.done[me]);
     unsigned long long m = __ballot(want);
     const int F = a.F, N = a.N, HW = a.HW;
     while (m) {
@@ -4411,7 +4419,8 @@ hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s) {
 
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
     if (a.F <= kResetSmallF && a.N <= a.F) {
-        learn_reset_small_kernel<<<dim3((unsigned)((a.E + 63) / 64)), dim3(64), 0, s>>>(a, all ? 1 : 0);
+        learn_reset_small_kernel<<<dim3((unsigned)((a.E + kResetSmallEnvs - 1) / kResetSmallEnvs)), dim3(64), 0, s>>>(
+            a, all ? 1 : 0);
         return hipGetLastError();
     }
     int P = 1;
