@@ -245,6 +245,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.trecs = nullptr;       // the accumulator path unless a tiled step sets it
     a.tstart = l->d_tstart;
     a.tstartT = nullptr;     // set by the one-device tiled step after its transpose
+    a.tstart_out = nullptr;
     a.bph = l->d_bph;
     a.tstats = l->d_tstats;
     a.tdirty = l->d_tdirty;
@@ -610,7 +611,11 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             }
             ffm::LearnArgs a = make_args(l);
             a.trecs = l->d_trecs;
+            // env-major passes read the tile offsets transposed, written by the stencil launch
+            const bool tt = !l->single_tm && !tstart_t_off();
+            if (tt) a.tstart_out = l->d_tstartT;
             HIP_TRY(ffm::launch_learn_batch(a, s));
+            a.tstart_out = nullptr;
             if (l->single_tm) {      // records reordered tile-major, then the passes
                 a.ow = 1;
                 a.orank = 0;
@@ -621,8 +626,7 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
                 a.thdr = l->d_hdr;
                 a.tR = 1;
                 a.NTk = l->NT;
-            } else if (!tstart_t_off()) {   // env-major passes read the tile offsets transposed
-                HIP_TRY(ffm::launch_learn_tstart_transpose(a, l->d_tstartT, s));
+            } else if (tt) {
                 a.tstartT = l->d_tstartT;
             }
             HIP_TRY(ffm::launch_learn_tiles(a, false, s));

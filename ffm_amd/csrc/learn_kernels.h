@@ -103,6 +103,7 @@ struct LearnArgs {
     // the same transposed, [NT + 1][E] (one device, env-major passes): a tile's ranges of
     // all envs are contiguous, so a pass loads them coalesced.  nullptr: read tstart.
     const uint16_t* tstartT;
+    uint16_t* tstart_out;       // non-null: the batch step's stencil launch also writes tstartT here
     double* tstats;             // [NT][4] tiled step: per-tile H summary (present, non-finite, min, max)
     int* tdirty;                // [NT] tiled step: bit 0 max, 1 min, 2 non-finite flag only a bound (stale)
     int* tcand;                 // [NT + 1] tiled step: tiles to rescan ([0] = count, then the tiles)

@@ -3982,6 +3982,37 @@ __global__ __launch_bounds__(64) void learn_import_kernel(LearnTable T, int widt
 // XCD-aware: hardware deals consecutive workgroups round-robin over the 8 XCDs, so
 // workgroup b takes logical tile (b % 8) * (B / 8) + b / 8; each XCD then sweeps a
 // contiguous run of rows and finds the rows above and below in its own L2.
+// tstart [E][NT + 1] -> [NT + 1][E] through a 64 x 64 LDS tile (both sides coalesced);
+// tile (bx, by) covers offsets [64 bx, 64 bx + 64) of envs [64 by, 64 by + 64).
+__device__ __forceinline__ void tstart_transpose_tile(const uint16_t* in, uint16_t* out, long long E, int NT1,
+                                                      int bx, int by) {
+    __shared__ uint16_t tl[64][66];
+    const int t0 = bx * 64;
+    const long long e0 = (long long)by * 64;
+    const int lx = (int)threadIdx.x & 63, ly = (int)threadIdx.x >> 6;
+    uint16_t v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {     // every load in flight before the first LDS store
+        const long long e = e0 + ly + 4 * q;
+        const int t = t0 + lx;
+        v[q] = e < E && t < NT1 ? in[e * NT1 + t] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) tl[ly + 4 * q][lx] = v[q];
+    __syncthreads();
+#pragma unroll
+    for (int i = ly; i < 64; i += 4) {
+        const int t = t0 + i;
+        const long long e = e0 + lx;
+        if (t < NT1 && e < E) out[(long long)t * E + e] = tl[lx][i];
+    }
+}
+
+__global__ __launch_bounds__(256) void learn_tstart_transpose_kernel(const uint16_t* in, uint16_t* out, long long E,
+                                                                     int NT1) {
+    tstart_transpose_tile(in, out, E, NT1, (int)blockIdx.x, (int)blockIdx.y);
+}
+
 __global__ __launch_bounds__(256) void learn_stencil_kernel(LearnArgs a, int tiles_per_env) {
     const unsigned B = gridDim.x, b = blockIdx.x;
     const unsigned lt = (B & 7u) ? b : (b & 7u) * (B >> 3) + (b >> 3);
@@ -4047,8 +4078,17 @@ __global__ __launch_bounds__(256) void learn_stencil4_kernel(LearnArgs a, int ti
 // operation sequence (U, D, L, R).
 constexpr int kColRows = 8;
 
-__global__ __launch_bounds__(256) void learn_stencil_col_kernel(LearnArgs a, int strips, int segs) {
-    const unsigned B = gridDim.x, b = blockIdx.x;
+// tblocks > 0: the launch's first tblocks workgroups transpose the tile offsets
+// (a.tstart -> a.tstart_out, independent of the stencil: one dispatch instead of two);
+// tblocks is a multiple of 8, so the stencil's XCD-aware numbering is unchanged.
+__global__ __launch_bounds__(256) void learn_stencil_col_kernel(LearnArgs a, int strips, int segs, int tblocks) {
+    if ((int)blockIdx.x < tblocks) {
+        const int NT1 = a.NT + 1, nbx = (NT1 + 63) / 64, nby = (int)((a.E + 63) / 64);
+        const int k = (int)blockIdx.x;
+        if (k < nbx * nby) tstart_transpose_tile(a.tstart, a.tstart_out, a.E, NT1, k % nbx, k / nbx);
+        return;
+    }
+    const unsigned B = gridDim.x - (unsigned)tblocks, b = blockIdx.x - (unsigned)tblocks;
     const unsigned lt = (B & 7u) ? b : (b & 7u) * (B >> 3) + (b >> 3);
     const int per_env = strips * segs;
     const long long e = lt / (unsigned)per_env;
@@ -4104,30 +4144,6 @@ __global__ __launch_bounds__(256) void learn_stencil_col_kernel(LearnArgs a, int
     }
 }
 
-// tstart [E][NT + 1] -> [NT + 1][E] through a 64 x 64 LDS tile (both sides coalesced).
-__global__ __launch_bounds__(256) void learn_tstart_transpose_kernel(const uint16_t* in, uint16_t* out, long long E,
-                                                                     int NT1) {
-    __shared__ uint16_t tl[64][66];
-    const int t0 = (int)blockIdx.x * 64;
-    const long long e0 = (long long)blockIdx.y * 64;
-    const int lx = (int)threadIdx.x & 63, ly = (int)threadIdx.x >> 6;
-    uint16_t v[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) {     // every load in flight before the first LDS store
-        const long long e = e0 + ly + 4 * q;
-        const int t = t0 + lx;
-        v[q] = e < E && t < NT1 ? in[e * NT1 + t] : (uint16_t)0;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; q++) tl[ly + 4 * q][lx] = v[q];
-    __syncthreads();
-#pragma unroll
-    for (int i = ly; i < 64; i += 4) {
-        const int t = t0 + i;
-        const long long e = e0 + lx;
-        if (t < NT1 && e < E) out[(long long)t * E + e] = tl[lx][i];
-    }
-}
 
 constexpr int kSepStencilHW = 16384;
 
@@ -4136,8 +4152,17 @@ void launch_sep_stencil(const LearnArgs& a, hipStream_t s) {
     const int tiles = (a.HW + 255) / 256;
     if (a.W % 256 == 0 && !(FFM_LABLATE & 16)) {
         const int segs = a.W / 256, strips = (a.H + 4 * kColRows - 1) / (4 * kColRows);
-        learn_stencil_col_kernel<<<dim3((unsigned)(strips * segs * a.E)), dim3(256), 0, s>>>(a, strips, segs);
-    } else if (a.W % 4 == 0) {
+        int tb = 0;
+        if (a.tstart_out) {
+            const int NT1 = a.NT + 1;
+            tb = ((NT1 + 63) / 64) * (int)((a.E + 63) / 64);
+            tb = (tb + 7) & ~7;
+        }
+        learn_stencil_col_kernel<<<dim3((unsigned)(strips * segs * a.E + tb)), dim3(256), 0, s>>>(a, strips, segs, tb);
+        return;
+    }
+    if (a.tstart_out) (void)launch_learn_tstart_transpose(a, a.tstart_out, s);
+    if (a.W % 4 == 0) {
         const int tiles4 = (a.HW / 4 + 255) / 256;
         learn_stencil4_kernel<<<dim3((unsigned)(tiles4 * a.E)), dim3(256), 0, s>>>(a, tiles4);
     } else {
@@ -4160,6 +4185,7 @@ hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
     learn_batch_kernel<BS, EPB, APT, D, DL, VK><<<dim3(blocks), dim3(BS), smem, s>>>(a);
     if (a.sep_stencil) launch_sep_stencil(a, s);
+    else if (a.tstart_out) (void)launch_learn_tstart_transpose(a, a.tstart_out, s);   // stencil fused: its own launch
     return hipGetLastError();
 }
 
