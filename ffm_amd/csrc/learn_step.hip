@@ -4001,7 +4001,8 @@ __device__ __forceinline__ void tstart_transpose_tile(const uint16_t* in, uint16
     for (int q = 0; q < 16; q++) tl[ly + 4 * q][lx] = v[q];
     __syncthreads();
 #pragma unroll
-    for (int i = ly; i < 64; i += 4) {
+    for (int q = 0; q < 16; q++) {
+        const int i = ly + 4 * q;
         const int t = t0 + i;
         const long long e = e0 + lx;
         if (t < NT1 && e < E) out[(long long)t * E + e] = tl[lx][i];
