@@ -634,8 +634,16 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             continue;
         }
         int rc = phase_local(l, s);
-        if (!rc) rc = phase_apply(l, FFM_TABLE_V, s);
-        if (!rc && l->actor) rc = phase_apply(l, FFM_TABLE_H, s);
+        if (!rc && l->actor && !l->trained && !l->post_update && apply_due(l)) {
+            // one device, nothing exchanged between the tables: both applies in one launch
+            HIP_TRY(ffm::launch_learn_apply(make_args(l), true, true, s));
+            l->hstat_valid = true;
+            l->tstats_valid = false;
+            l->phase = 3;
+        } else {
+            if (!rc) rc = phase_apply(l, FFM_TABLE_V, s);
+            if (!rc && l->actor) rc = phase_apply(l, FFM_TABLE_H, s);
+        }
         if (!rc) rc = phase_end(l, s);
         if (rc) return rc;
     }

@@ -2239,7 +2239,8 @@ __device__ __forceinline__ void phase_learn_one(const LearnArgs& a, long long e,
 // ===========================================================================
 // Min / max / non-finite flag of the H values (the actor's global normalisation,
 // model/ffm_unified.py:413-426), reduced per block into hpart[block][4].
-__device__ __forceinline__ void hstat_block_reduce(double mn, double mx, int nf, uint32_t n, double* hpart) {
+__device__ __forceinline__ void hstat_block_reduce(double mn, double mx, int nf, uint32_t n, double* hpart,
+                                                   unsigned bid = blockIdx.x) {
     __shared__ double smn[4], smx[4];
     __shared__ int snf[4];
     for (int o = 32; o > 0; o >>= 1) {
@@ -2257,7 +2258,7 @@ __device__ __forceinline__ void hstat_block_reduce(double mn, double mx, int nf,
             mx = smx[w] > mx ? smx[w] : mx;
             nf |= snf[w];
         }
-        double* o = hpart + blockIdx.x * 4;
+        double* o = hpart + bid * 4;
         o[0] = n > 0 ? 1.0 : 0.0;
         o[1] = (double)nf;
         o[2] = mn;
@@ -2306,14 +2307,16 @@ __global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a, int nb) {
 
 // Apply the step's fixed-point increments once; for H also reduce the statistics
 // the next step's actor reads (fusing the separate statistics pass).
+// One table's apply as workgroup `bid` of `nblk` (learn_apply_kernel; learn_apply_vh_kernel
+// runs V's and H's in one launch).
 template <int WIDTH, bool STATS>
-__global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* hpart) {
+__device__ __forceinline__ void apply_hashed(const LearnTable& T, double* hpart, unsigned bid, unsigned nblk) {
     const uint32_t n = *T.n;
     // the next step's delta export reports entries inserted after this point
-    if (blockIdx.x == 0 && threadIdx.x == 0) *T.mark = n;
+    if (bid == 0 && threadIdx.x == 0) *T.mark = n;
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    for (uint32_t i = bid * 256 + threadIdx.x; i < n; i += nblk * 256) {
         const uint32_t slot = T.order[i];
         double* vp = tval(T, slot);
         if (WIDTH == 1) {   // V: visit-averaged
@@ -2340,7 +2343,19 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
             }
         }
     }
-    if (STATS) hstat_block_reduce(mn, mx, nf, n, hpart);
+    if (STATS) hstat_block_reduce(mn, mx, nf, n, hpart, bid);
+}
+
+template <int WIDTH, bool STATS>
+__global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* hpart) {
+    apply_hashed<WIDTH, STATS>(T, hpart, blockIdx.x, gridDim.x);
+}
+
+// Both hashed tables in one launch (their increments are independent): workgroups
+// [0, nbv) apply V, the rest H with the statistics partials -- one dispatch fewer per step.
+__global__ __launch_bounds__(256) void learn_apply_vh_kernel(LearnTable V, LearnTable Ht, double* hpart, unsigned nbv) {
+    if (blockIdx.x < nbv) apply_hashed<1, false>(V, nullptr, blockIdx.x, nbv);
+    else apply_hashed<5, true>(Ht, hpart, blockIdx.x - nbv, gridDim.x - nbv);
 }
 
 // Dense tables: the same pass in slot order over the presence bitmap.  Most
@@ -4291,6 +4306,12 @@ hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s) {
+    if (v && h && !a.V.dense_by && !a.Ht.dense_by) {     // hashed V and H together
+        const unsigned nb = kHstatBlocks / 4;
+        learn_apply_vh_kernel<<<dim3(512 + nb), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u);
+        learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, (int)nb);
+        return hipGetLastError();
+    }
     if (v) {
         if (a.V.dense_by) learn_apply_dense_kernel<1, false><<<dim3(2048), dim3(256), 0, s>>>(a.V, nullptr);
         else learn_apply_kernel<1, false><<<dim3(512), dim3(256), 0, s>>>(a.V, nullptr);
