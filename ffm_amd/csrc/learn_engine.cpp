@@ -551,11 +551,11 @@ static int phase_apply(ffm_learner* l, int32_t which, hipStream_t s) {
     return FFM_OK;
 }
 
-static int phase_end(ffm_learner* l, hipStream_t s) {
+static int phase_end(ffm_learner* l, hipStream_t s, bool reset_done = false) {
     l->since_apply = apply_due(l) ? 0 : l->since_apply + 1;
     HIP_TRY(ffm::launch_learn_capture(make_args(l), l->traj, s));   // before the reset re-places
     l->cur ^= 1;
-    if (l->d.auto_reset) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
+    if (l->d.auto_reset && !reset_done) HIP_TRY(ffm::launch_learn_reset(make_args(l), false, s));
     l->t++;
     l->phase = 0;
     return FFM_OK;
@@ -634,9 +634,22 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             continue;
         }
         int rc = phase_local(l, s);
+        bool reset_done = false;
         if (!rc && l->actor && !l->trained && !l->post_update && apply_due(l)) {
-            // one device, nothing exchanged between the tables: both applies in one launch
-            HIP_TRY(ffm::launch_learn_apply(make_args(l), true, true, s));
+            // one device, nothing exchanged between the tables: both applies in one launch,
+            // and the ended envs re-placed in it too when no trajectory capture must see
+            // them first (the reset's arguments are those after the step's DFF swap)
+            ffm::LearnArgs a = make_args(l);
+            if (l->d.auto_reset && l->traj.n_sel <= 0 && ffm::learn_reset_small(a) && !a.V.dense_by &&
+                !a.Ht.dense_by) {
+                l->cur ^= 1;
+                const ffm::LearnArgs ra = make_args(l);
+                l->cur ^= 1;
+                HIP_TRY(ffm::launch_learn_apply_reset(a, ra, s));
+                reset_done = true;
+            } else {
+                HIP_TRY(ffm::launch_learn_apply(a, true, true, s));
+            }
             l->hstat_valid = true;
             l->tstats_valid = false;
             l->phase = 3;
@@ -644,7 +657,7 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             if (!rc) rc = phase_apply(l, FFM_TABLE_V, s);
             if (!rc && l->actor) rc = phase_apply(l, FFM_TABLE_H, s);
         }
-        if (!rc) rc = phase_end(l, s);
+        if (!rc) rc = phase_end(l, s, reset_done);
         if (rc) return rc;
     }
     if (l->h_overflow && n_steps > 0 && !l->mt)

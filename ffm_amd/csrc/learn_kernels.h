@@ -190,6 +190,9 @@ hipError_t launch_learn_hstat(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_exact(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s);
+// hashed V + H applies and the small-map reset (ra: the arguments after the step's DFF swap)
+bool learn_reset_small(const LearnArgs& a);
+hipError_t launch_learn_apply_reset(const LearnArgs& a, const LearnArgs& ra, hipStream_t s);
 hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s);
 bool learn_batch_raster(int HW, int A, int D);
 // Bytes of LearnArgs::bph for a tiled learner of E envs (0: the shape keeps the fused kernel).

@@ -2353,11 +2353,6 @@ __global__ __launch_bounds__(256) void learn_apply_kernel(LearnTable T, double* 
 
 // Both hashed tables in one launch (their increments are independent): workgroups
 // [0, nbv) apply V, the rest H with the statistics partials -- one dispatch fewer per step.
-__global__ __launch_bounds__(256) void learn_apply_vh_kernel(LearnTable V, LearnTable Ht, double* hpart, unsigned nbv) {
-    if (blockIdx.x < nbv) apply_hashed<1, false>(V, nullptr, blockIdx.x, nbv);
-    else apply_hashed<5, true>(Ht, hpart, blockIdx.x - nbv, gridDim.x - nbv);
-}
-
 // Dense tables: the same pass in slot order over the presence bitmap.  Most
 // slots of a long run are present, so streaming the records beats gathering
 // them through the insertion order; min / max / non-finite do not depend on order.
@@ -3922,10 +3917,17 @@ constexpr int kResetSmallF = 256;
 #endif
 constexpr int kResetSmallEnvs = FFM_RESET_ENVS;
 
-__global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int all) {
-    __shared__ __attribute__((aligned(16))) unsigned long long keys[kResetSmallF + 2];
-    const int lane = threadIdx.x;
-    const long long e0 = (long long)blockIdx.x * kResetSmallEnvs;
+__device__ __forceinline__ void lwave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One wave re-places its ended envs among [e0, e0 + kResetSmallEnvs), keys in its own LDS
+// row.  WAVE: the wave shares its workgroup with others (learn_apply_vh_kernel), so it
+// synchronises itself only.
+template <bool WAVE>
+__device__ __forceinline__ void reset_small_wave(const LearnArgs& a, int all, long long e0, unsigned long long* keys) {
+    const int lane = (int)(threadIdx.x & 63);
     const long long me = e0 + lane;
     const bool want = lane < kResetSmallEnvs && me < a.E && (all || a.done[me]);
     unsigned long long m = __ballot(want);
@@ -3939,10 +3941,10 @@ __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int 
             const uint32_t k = philox(make_uint4(a.t, genv, (uint32_t)j, kPurReset << 28), a.key0, a.key1).x;
             keys[j] = ((unsigned long long)k << 32) | (unsigned)j;
         }
-        __syncthreads();
+        if (WAVE) lwave_sync(); else __syncthreads();
         // each lane ranks its (up to four) keys in one pass over 16-B broadcast reads
         if (lane == 0 && (F & 1)) keys[F] = ~0ull;   // pad to pairs: ~0 is never below a key
-        __syncthreads();
+        if (WAVE) lwave_sync(); else __syncthreads();
         unsigned long long kj[kResetSmallF / 64];
         int rank[kResetSmallF / 64];
 #pragma unroll
@@ -3973,7 +3975,29 @@ __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int 
                 a.counters[4 * e + 2] += 1;
             }
         }
-        __syncthreads();
+        if (WAVE) lwave_sync(); else __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int all) {
+    __shared__ __attribute__((aligned(16))) unsigned long long keys[kResetSmallF + 2];
+    reset_small_wave<false>(a, all, (long long)blockIdx.x * kResetSmallEnvs, keys);
+}
+
+// nbr > 0: the last nbr workgroups re-place the ended envs as well (ra: the step's
+// arguments after the DFF swap; independent of the tables), four waves of
+// kResetSmallEnvs envs each -- the reset launch's work without its dispatch.
+__global__ __launch_bounds__(256) void learn_apply_vh_kernel(LearnTable V, LearnTable Ht, double* hpart, unsigned nbv,
+                                                             unsigned nbh, LearnArgs ra) {
+    if (blockIdx.x < nbv) {
+        apply_hashed<1, false>(V, nullptr, blockIdx.x, nbv);
+    } else if (blockIdx.x < nbv + nbh) {
+        apply_hashed<5, true>(Ht, hpart, blockIdx.x - nbv, nbh);
+    } else {
+        __shared__ __attribute__((aligned(16))) unsigned long long keys[4][kResetSmallF + 2];
+        const unsigned w = threadIdx.x >> 6;
+        const long long e0 = ((long long)(blockIdx.x - nbv - nbh) * 4 + w) * kResetSmallEnvs;
+        if (e0 < ra.E) reset_small_wave<true>(ra, 0, e0, keys[w]);
     }
 }
 
@@ -4305,10 +4329,21 @@ hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s) {
     return a.D == 4 ? launch_batch_d<4>(a, s) : launch_batch_d<1>(a, s);
 }
 
+bool learn_reset_small(const LearnArgs& a) { return a.F <= kResetSmallF && a.N <= a.F; }
+
+// Hashed V and H applies and the small-map reset of the ended envs (ra) in one launch.
+hipError_t launch_learn_apply_reset(const LearnArgs& a, const LearnArgs& ra, hipStream_t s) {
+    const unsigned nb = kHstatBlocks / 4;
+    const unsigned nbr = (unsigned)((ra.E + 4 * kResetSmallEnvs - 1) / (4 * kResetSmallEnvs));
+    learn_apply_vh_kernel<<<dim3(512 + nb + nbr), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, ra);
+    learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, (int)nb);
+    return hipGetLastError();
+}
+
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s) {
     if (v && h && !a.V.dense_by && !a.Ht.dense_by) {     // hashed V and H together
         const unsigned nb = kHstatBlocks / 4;
-        learn_apply_vh_kernel<<<dim3(512 + nb), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u);
+        learn_apply_vh_kernel<<<dim3(512 + nb), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, a);
         learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, (int)nb);
         return hipGetLastError();
     }
