@@ -629,8 +629,17 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             } else if (tt) {
                 a.tstartT = l->d_tstartT;
             }
-            HIP_TRY(ffm::launch_learn_tiles(a, false, s));
-            if (int rc = phase_end(l, s)) return rc;
+            bool reset_done = false;
+            if (l->actor && !l->single_tm && l->d.auto_reset && l->traj.n_sel <= 0 && !ffm::learn_reset_small(a)) {
+                l->cur ^= 1;     // the reset's arguments are those after the step's DFF swap
+                const ffm::LearnArgs ra = make_args(l);
+                l->cur ^= 1;
+                HIP_TRY(ffm::launch_learn_tiles_reset(a, ra, s));
+                reset_done = true;
+            } else {
+                HIP_TRY(ffm::launch_learn_tiles(a, false, s));
+            }
+            if (int rc = phase_end(l, s, reset_done)) return rc;
             continue;
         }
         int rc = phase_local(l, s);

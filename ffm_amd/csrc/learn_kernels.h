@@ -198,6 +198,9 @@ bool learn_batch_raster(int HW, int A, int D);
 // Bytes of LearnArgs::bph for a tiled learner of E envs (0: the shape keeps the fused kernel).
 size_t learn_batch_phase_bytes(long long E, int HW, int A);
 hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s);
+// launch_learn_tiles' env-major actor passes with the re-placement of the ended envs (ra:
+// the arguments after the step's DFF swap) fused into the statistics' final launch
+hipError_t launch_learn_tiles_reset(const LearnArgs& a, const LearnArgs& ra, hipStream_t s);
 // tstart [E][NT + 1] -> out [NT + 1][E] (LearnArgs::tstartT)
 hipError_t launch_learn_tstart_transpose(const LearnArgs& a, uint16_t* out, hipStream_t s);
 // tile-major records: the column scan, the tile offsets in destination order (per-destination

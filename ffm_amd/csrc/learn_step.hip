@@ -3455,7 +3455,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_rescan_kernel(LearnAr
 // The tiles' summaries -> the statistics the next step's actor reads (hstat): the
 // exact extremes of the tiles learn_tile_cand_kernel kept (hpart) and the rescanned
 // tiles'.  After learn_tile_rescan_kernel a stale tile's bound is never the extreme.
-__global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
+__device__ __forceinline__ void tile_final(const LearnArgs& a) {
     __shared__ double smn[4], smx[4];
     __shared__ int snf[4];
     double mn = a.hpart[0], mx = a.hpart[1];
@@ -3491,6 +3491,8 @@ __global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) {
         *a.V.mark = *a.V.n;
     }
 }
+
+__global__ __launch_bounds__(256) void learn_tile_final_kernel(LearnArgs a) { tile_final(a); }
 
 // ===========================================================================
 // Tile-major records.  The batch kernel leaves each env's records in
@@ -3776,11 +3778,10 @@ __global__ __launch_bounds__(256) void learn_capture_kernel(LearnArgs a, TrajCap
 constexpr int kResetBS = 256;
 constexpr int kResetCap = 16384;
 
-__global__ __launch_bounds__(kResetBS) void learn_reset_kernel(LearnArgs a, int all) {
+__device__ __forceinline__ void reset_env(const LearnArgs& a, int all, long long e) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     __shared__ int cnt;
-    const long long e = blockIdx.x;
     if (!all && !a.done[e]) return;
     const int tid = threadIdx.x, F = a.F, N = a.N;
     const uint32_t genv = (uint32_t)(a.env_base + e);
@@ -3837,6 +3838,19 @@ __global__ __launch_bounds__(kResetBS) void learn_reset_kernel(LearnArgs a, int 
             a.counters[4 * e + 2] += 1;
         }
     }
+}
+
+__global__ __launch_bounds__(kResetBS) void learn_reset_kernel(LearnArgs a, int all) {
+    reset_env(a, all, (long long)blockIdx.x);
+}
+
+// The H statistics' final reduction (workgroup 0) and the re-placement of the ended envs
+// (workgroup 1 + e; ra: the arguments after the step's DFF swap) in one launch: the two are
+// independent, and the step saves a dispatch.
+static_assert(kResetBS == 256, "the final reduction's workgroup shape");
+__global__ __launch_bounds__(kResetBS) void learn_tile_final_reset_kernel(LearnArgs a, LearnArgs ra) {
+    if (blockIdx.x == 0) tile_final(a);
+    else reset_env(ra, 0, (long long)blockIdx.x - 1);
 }
 
 // ---- delta exchange of the batched step (multi-rank) ----
@@ -4404,6 +4418,26 @@ hipError_t launch_learn_tstart_transpose(const LearnArgs& a, uint16_t* out, hipS
     const int NT1 = a.NT + 1;
     learn_tstart_transpose_kernel<<<dim3((unsigned)((NT1 + 63) / 64), (unsigned)((a.E + 63) / 64)), dim3(256), 0, s>>>(
         a.tstart, out, a.E, NT1);
+    return hipGetLastError();
+}
+
+hipError_t launch_learn_tiles_reset(const LearnArgs& a, const LearnArgs& ra, hipStream_t s) {
+    const unsigned tgrid = 8u * (unsigned)((a.NT + 7) / 8);
+    const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
+    int P = 1;
+    while (P < (ra.F < kResetCap ? ra.F : kResetCap)) P <<= 1;
+    const size_t smem = (size_t)P * 8;
+    if (smem > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&learn_tile_final_reset_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    learn_tile_v_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    learn_tile_h_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    learn_tile_h_wide_kernel<false><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    launch_tile_cands(a, s);
+    learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    learn_tile_final_reset_kernel<<<dim3((unsigned)(1 + ra.E)), dim3(kResetBS), smem, s>>>(a, ra);
     return hipGetLastError();
 }
 
