@@ -4130,7 +4130,10 @@ __global__ __launch_bounds__(256) void learn_stencil4_kernel(LearnArgs a, int ti
 // neighbours come from the adjacent lanes (a scalar load only at a segment's inner
 // edges).  A workgroup's four waves take consecutive strips.  Per cell the identical
 // operation sequence (U, D, L, R).
-constexpr int kColRows = 8;
+#ifndef FFM_COL_ROWS
+#define FFM_COL_ROWS 8
+#endif
+constexpr int kColRows = FFM_COL_ROWS;
 
 // tblocks > 0: the launch's first tblocks workgroups transpose the tile offsets
 // (a.tstart -> a.tstart_out, independent of the stencil: one dispatch instead of two);
