@@ -48,12 +48,15 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
-    ap.add_argument("--steps", type=int, default=None, help="default 500 (config 2), 1500 (config 3: one episode), 300 (config 4), 50 (config 5)")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="default 500 (config 2), 1500 (config 3: one episode), 300 (config 4), "
+                         "300 (config 5: one whole max_steps episode per window)")
     ap.add_argument("--warmup", type=int, default=None, help="default 50 (config 2), 20 (config 3), 30 (config 4), 5 (config 5)")
     ap.add_argument("--burn-in", type=int, default=None,
                     help="untimed steps after reset before the warmup, so the timed envs are desynchronised "
                          "(steady state) instead of all starting their first episode together; default 1000 "
-                         "(config 2), else 0")
+                         "(config 2), 300 (config 5: one whole episode, so the timed episodes start on "
+                         "populated tables), else 0")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
     ap.add_argument("--size", type=int, default=None)
     ap.add_argument("--agents", type=int, default=None)
@@ -82,13 +85,13 @@ def parse():
     # config 3: an episode takes 1,491 +- 31 steps (oracle, 64 envs), so its envs stay in
     # phase; every timed window spans one episode and averages a whole evacuation
     size, agents, envs, steps, warmup = {2: (12, 32, 65536, 500, 50), 3: (64, 512, 8192, 1500, 20),
-                                         4: (12, 32, 65536, 300, 30), 5: (256, 8192, 512, 50, 5)}[a.config]
+                                         4: (12, 32, 65536, 300, 30), 5: (256, 8192, 512, 300, 5)}[a.config]
     a.size = a.size or size
     a.agents = a.agents or agents
     a.envs = a.envs or envs
     a.steps = a.steps if a.steps is not None else steps
     a.warmup = a.warmup if a.warmup is not None else warmup
-    a.burn_in = a.burn_in if a.burn_in is not None else {2: 1000}.get(a.config, 0)
+    a.burn_in = a.burn_in if a.burn_in is not None else {2: 1000, 5: 300}.get(a.config, 0)
     return a
 
 
@@ -350,9 +353,9 @@ def bench_learner(args, world, rank, torch, dist):
     else:
         L.set_sync_period(args.sync_period)
         run = lambda k: L.step(k, stream)  # noqa: E731
-    run(args.warmup)
+    run(args.burn_in + args.warmup)
     torch.cuda.synchronize()
-    print(f"[bench] config {args.config}: warmup done", file=sys.stderr, flush=True)
+    print(f"[bench] config {args.config}: burn-in + warmup done", file=sys.stderr, flush=True)
     sent0 = sync.bytes_sent if world > 1 else 0
     recv0 = getattr(sync, "received_bytes", 0) if world > 1 else 0
     reps = timed_repeats(args, world, dist, torch, lambda: run(args.steps), lambda: L.counters(stream))
@@ -360,7 +363,9 @@ def bench_learner(args, world, rank, torch, dist):
     recv_timed = (getattr(sync, "received_bytes", 0) - recv0) if world > 1 else 0
     elapsed, agent_steps = reps["elapsed"], reps["agent_steps"]
     print(f"[bench] timed regions {reps['summary']['elapsed_s']} s", file=sys.stderr, flush=True)
-    nk = min(args.steps, 100)
+    # the event pass spans a whole timed window (config 5: one episode, its lockstep
+    # truncation and reset included), so the roofline averages what `value` averages
+    nk = min(args.steps, 300)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
@@ -391,7 +396,13 @@ def bench_learner(args, world, rank, torch, dist):
                              f"{'/' + cfg['mode'] if cfg['mode'] else ''} learning step, {H}x{W} room, "
                              f"{A} agents/env, {E} envs/GPU, epsilon {cfg['params']['epsilon']}, "
                              f"max_steps {cfg['max_steps']}, Philox seed {args.seed}, on-device auto-reset"
+                             + (f", {args.burn_in}-step untimed burn-in" if args.burn_in else "")
+                             + (f"; every {args.steps}-step timed window is one whole episode of every env (the "
+                                f"envs run in lockstep: each episode truncates at max_steps), its start on the "
+                                f"tables the previous episodes built and its lockstep reset included"
+                                if args.config == 5 and args.steps == cfg["max_steps"] else "")
                              + (f", tables applied every {args.sync_period} steps" if args.sync_period > 1 else "")),
+                "burn_in_steps": args.burn_in,
                 "map": f"{H}x{W}", "agents_per_env": A, "envs_per_gpu": E, "global_envs": E * world,
                 "parallelism": f"env-sharded x{world}",
             },

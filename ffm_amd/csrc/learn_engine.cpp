@@ -64,6 +64,7 @@ struct ffm_learner {
     int32_t* d_ep_steps = nullptr;
     int32_t* d_done = nullptr;
     int32_t* d_nstart = nullptr;
+    int32_t* d_epcap = nullptr;              // ffm_learner_set_episode_caps (nullptr: no quota)
     unsigned long long* d_ctr = nullptr;
     double* d_hstat = nullptr;
     double* d_hpart = nullptr;
@@ -149,7 +150,7 @@ static void free_table(DevTable& T) {
 static void release(ffm_learner* l) {
     if (!l) return;
     void* bufs[] = {l->d_map, l->d_map2, l->d_sff, l->d_free_cells, l->d_pos, l->d_cnt, l->d_dff[0], l->d_dff[1],
-                    l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_ctr, l->d_hstat, l->d_hpart,
+                    l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_epcap, l->d_ctr, l->d_hstat, l->d_hpart,
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
                     l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand,
                     l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_pack, l->d_xcnt, l->d_newv, l->d_newh,
@@ -227,6 +228,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.pos = l->d_pos; a.cnt = l->d_cnt;
     a.dff_in = l->d_dff[l->cur]; a.dff_out = l->d_dff[l->cur ^ 1];
     a.episodes = l->d_eps; a.ep_steps = l->d_ep_steps; a.done = l->d_done; a.nstart = l->d_nstart;
+    a.ep_cap = l->d_epcap;
     a.counters = l->d_ctr;
     a.V = l->V.t; a.Ht = l->H.t;
     a.hstat = l->d_hstat; a.hpart = l->d_hpart; a.recs = l->d_recs; a.overflow = l->d_overflow;
@@ -1043,21 +1045,24 @@ int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank) {
     int mx = 0;
     for (int q = 0; q < world; q++) mx = std::max(mx, ffm::owner_tiles(l->NT, world, ffm::kOwnChunk, q));
     const size_t E = (size_t)l->d.n_envs, A = (size_t)l->d.agent_capacity;
+    const int ths = mx + 1;
+    // the new buffers first: a failed allocation leaves the learner as it was
+    uint32_t* hdr = nullptr; double* tsum = nullptr; uint32_t* newv = nullptr; uint32_t* newh = nullptr;
+    if (hipMalloc((void**)&hdr, (size_t)world * ths * 4) != hipSuccess ||
+        hipMalloc((void**)&tsum, (size_t)ths * 5 * 8) != hipSuccess ||
+        hipMalloc((void**)&newv, 2 * E * A * 4) != hipSuccess ||
+        hipMalloc((void**)&newh, 2 * E * A * 4) != hipSuccess) {
+        (void)hipFree(hdr); (void)hipFree(tsum); (void)hipFree(newv); (void)hipFree(newh);
+        return fail(FFM_E_NOMEM, "hipMalloc (owner exchange)");
+    }
     (void)hipFree(l->d_hdr);
     (void)hipFree(l->d_tsum);
     (void)hipFree(l->d_newv);
     (void)hipFree(l->d_newh);
-    l->d_hdr = nullptr; l->d_tsum = nullptr; l->d_newv = nullptr; l->d_newh = nullptr;
+    l->d_hdr = hdr; l->d_tsum = tsum; l->d_newv = newv; l->d_newh = newh;
     l->ow = world;
     l->orank = rank;
-    l->ths = mx + 1;
-    if (hipMalloc((void**)&l->d_hdr, (size_t)world * l->ths * 4) != hipSuccess ||
-        hipMalloc((void**)&l->d_tsum, (size_t)l->ths * 5 * 8) != hipSuccess ||
-        hipMalloc((void**)&l->d_newv, 2 * E * A * 4) != hipSuccess ||
-        hipMalloc((void**)&l->d_newh, 2 * E * A * 4) != hipSuccess) {
-        l->ow = 1;
-        return fail(FFM_E_NOMEM, "hipMalloc (owner exchange)");
-    }
+    l->ths = ths;
     HIP_TRY(hipMemset(l->d_hdr, 0, (size_t)world * l->ths * 4));
     return FFM_OK;
 }
@@ -1225,6 +1230,27 @@ int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period) {
 int ffm_learner_set_epsilon_stride(ffm_learner* l, int64_t stride) {
     if (!l || stride < 1) return fail(FFM_E_INVALID, "epsilon stride must be >= 1");
     l->eps_stride = stride;
+    return FFM_OK;
+}
+
+int ffm_learner_set_episode_caps(ffm_learner* l, const int32_t* caps, int64_t n) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (n != 0 && (n != l->d.n_envs || !caps)) return fail(FFM_E_INVALID, "episode caps: n must be n_envs (or 0)");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    HIP_TRY(hipDeviceSynchronize());        // queued steps may still read the old quotas
+    if (n == 0) {
+        (void)hipFree(l->d_epcap);
+        l->d_epcap = nullptr;
+        return FFM_OK;
+    }
+    if (!l->d_epcap) {
+        hipError_t he = hipMalloc((void**)&l->d_epcap, (size_t)n * 4);
+        if (he != hipSuccess) {
+            l->d_epcap = nullptr;
+            return fail(FFM_E_NOMEM, std::string("hipMalloc (episode caps): ") + hipGetErrorString(he));
+        }
+    }
+    HIP_TRY(hipMemcpy(l->d_epcap, caps, (size_t)n * 4, hipMemcpyHostToDevice));
     return FFM_OK;
 }
 

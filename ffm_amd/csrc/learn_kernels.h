@@ -92,6 +92,7 @@ struct LearnArgs {
     int* episodes;              // [E]
     int* ep_steps;              // [E]
     int* done;                  // [E] re-place at the end of this step
+    const int* ep_cap;          // [E] episodes env e runs before it stays empty (nullptr: no quota)
     int* nstart;                // [E] live agents at step start
     unsigned long long* counters;  // [E][4] agent_steps, exits, resets, steps
     LearnTable V, Ht;

@@ -3783,7 +3783,14 @@ __device__ __forceinline__ void reset_env(const LearnArgs& a, int all, long long
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     __shared__ int cnt;
     if (!all && !a.done[e]) return;
-    const int tid = threadIdx.x, F = a.F, N = a.N;
+    const int tid = threadIdx.x, F = a.F;
+    // episode quota (ffm_learner_set_episode_caps): an env past it stays empty; the episode
+    // that reaches it ends with no re-placement (logged and counted like any other)
+    if (a.ep_cap && !all && a.episodes[e] >= a.ep_cap[e]) {
+        if (tid == 0) a.done[e] = 0;
+        return;
+    }
+    const int N = (a.ep_cap && a.episodes[e] + (all ? 0 : 1) >= a.ep_cap[e]) ? 0 : a.N;
     const uint32_t genv = (uint32_t)(a.env_base + e);
     const bool take_all = F <= kResetCap;
     unsigned long long T = 0xFFFFFFFFull;
@@ -3943,14 +3950,19 @@ template <bool WAVE>
 __device__ __forceinline__ void reset_small_wave(const LearnArgs& a, int all, long long e0, unsigned long long* keys) {
     const int lane = (int)(threadIdx.x & 63);
     const long long me = e0 + lane;
-    const bool want = lane < kResetSmallEnvs && me < a.E && (all || a.done[me]);
+    bool want = lane < kResetSmallEnvs && me < a.E && (all || a.done[me]);
+    if (want && a.ep_cap && !all && a.episodes[me] >= a.ep_cap[me]) {   // past its quota: stays empty
+        a.done[me] = 0;
+        want = false;
+    }
     unsigned long long m = __ballot(want);
-    const int F = a.F, N = a.N, HW = a.HW;
+    const int F = a.F, HW = a.HW;
     while (m) {
         const int b = __builtin_ctzll(m);
         m &= m - 1ull;
         const long long e = e0 + b;
         const uint32_t genv = (uint32_t)(a.env_base + e);
+        const int N = (a.ep_cap && a.episodes[e] + (all ? 0 : 1) >= a.ep_cap[e]) ? 0 : a.N;
         for (int j = lane; j < F; j += 64) {
             const uint32_t k = philox(make_uint4(a.t, genv, (uint32_t)j, kPurReset << 28), a.key0, a.key1).x;
             keys[j] = ((unsigned long long)k << 32) | (unsigned)j;

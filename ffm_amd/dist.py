@@ -206,6 +206,18 @@ class TableSync:
         self.caps[which] = cap
         self.capacity = max(self.caps.values())
 
+    def rescale(self, factor: float):
+        """The workload is about to grow by `factor` (e.g. a per-N driver raising N): scale the
+        adaptive record capacities up front, since the observed counts lag the change by the
+        adaptation window (a touched count jumping past the capacity is an error).  Every rank
+        calls it with the same factor at the same step; it never shrinks a capacity."""
+        if not self.adaptive or self.dense or self.tiled or factor <= 1.0:
+            return
+        for w in self.caps:
+            self.caps[w] = min(self.max_capacity, -(-int(self.caps[w] * factor) // 4096) * 4096)
+            self.max_count[w] = max(self.max_count[w], int(self.caps[w] / self.headroom))
+        self.capacity = max(self.caps.values())
+
     def _exchange_dense(self, which: str):
         acc, present = self.shard.dense_buffers(which)
         dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)

@@ -44,7 +44,7 @@ EXPORTED = [
     "ffm_learner_set_external_sync", "ffm_learner_flush_begin", "ffm_learner_flush_end",
     "ffm_learner_set_tile_owners", "ffm_learner_owner_buffers", "ffm_learner_step_owner_local",
     "ffm_learner_step_owner_v", "ffm_learner_step_owner_h", "ffm_learner_step_owner_end",
-    "ffm_learner_set_epsilon_stride",
+    "ffm_learner_set_epsilon_stride", "ffm_learner_set_episode_caps",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -158,6 +158,7 @@ def load_library():
     L.ffm_learner_set_epsilon_schedule.argtypes = [P, C.c_double, C.c_double, C.c_double, C.c_double]
     L.ffm_learner_set_epsilon_phase.argtypes = [P, i32]
     L.ffm_learner_set_epsilon_stride.argtypes = [P, i64]
+    L.ffm_learner_set_episode_caps.argtypes = [P, P, i64]
     L.ffm_learner_drain_episodes.argtypes = [P, P, i64, C.POINTER(i64), C.POINTER(i64), P]
     L.ffm_learner_set_trajectory_capture.argtypes = [P, P, P, i32, i32, i64, P]
     L.ffm_learner_delta_export_async.argtypes = [P, i32, P, P, i64, P, P]
@@ -597,6 +598,17 @@ class Learner:
         """Env g starts the epsilon schedule at its ((g % period) * stride)-th episode (0 = off)."""
         _check(self._L.ffm_learner_set_epsilon_phase(self._h, int(period)))
         _check(self._L.ffm_learner_set_epsilon_stride(self._h, int(stride)))
+
+    def set_episode_caps(self, caps=None):
+        """Env e ends at most caps[e] episodes after a reset, then stays empty (its quota of
+        the driver's episode count); None removes the quotas."""
+        if caps is None:
+            _check(self._L.ffm_learner_set_episode_caps(self._h, None, 0))
+            return
+        c = np.ascontiguousarray(caps, np.int32).reshape(-1)
+        if len(c) != self.n_envs:
+            raise ValueError("episode caps: one entry per env")
+        _check(self._L.ffm_learner_set_episode_caps(self._h, _ptr(c), len(c)))
 
     def drain_episodes(self, stream=None) -> np.ndarray:
         """Ended episodes since the last drain: int32 [n, 4] rows {global env, episode index,

@@ -75,13 +75,32 @@ def to_rank_tuple(key: int):
     return (tuple(int(r) for r in ranks), (int(blk[0]), int(blk[1])))
 
 
-def from_cells_bytes(b: bytes) -> int:
-    """pickle.dumps((cells13, (bx, by))) -> packed key (model/ffm_ac_core.py:109).
+class KeyUnpickler(pickle.Unpickler):
+    """Decodes key bytes (and table pickles) with every global refused except NumPy's scalar
+    reconstruction: a key is a pickled tuple of NumPy integer scalars (model/ffm_ac_core.py:109),
+    and nothing in it may run code."""
 
-    The bytes are produced by the caller's own process (a table it built or
-    exported); they are decoded with the standard unpickler like the
-    reference's own loaders do (model/ffm_actor_only.py:59-61)."""
-    cells, (bx, by) = pickle.loads(b)
+    _NUMPY = {("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"), ("numpy", "dtype")}
+
+    def __init__(self, f, numpy_scalars: bool = True):
+        super().__init__(f)
+        self.numpy_scalars = numpy_scalars
+
+    def find_class(self, module, name):
+        if self.numpy_scalars and (module, name) in self._NUMPY:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"pickle refers to {module}.{name}: refused")
+
+
+def loads_key(b: bytes):
+    import io
+    return KeyUnpickler(io.BytesIO(b)).load()
+
+
+def from_cells_bytes(b: bytes) -> int:
+    """pickle.dumps((cells13, (bx, by))) -> packed key (model/ffm_ac_core.py:109), decoded
+    with KeyUnpickler (NumPy scalars only)."""
+    cells, (bx, by) = loads_key(b)
     return pack(cells, bx, by)
 
 

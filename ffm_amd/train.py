@@ -46,10 +46,19 @@ def available_cells(map_array, exit_pos, radius) -> int:
     return int((np.abs(free[:, 0] - exit_pos[0]) + np.abs(free[:, 1] - exit_pos[1]) <= radius).sum())
 
 
+def _load_table(path: str) -> dict:
+    """A table pickle write_outputs / run_per_n wrote: a dict of bytes / tuple keys and float
+    values, read with every global refused (the file runs no code)."""
+    with open(path, "rb") as f:
+        table = K.KeyUnpickler(f, numpy_scalars=False).load()
+    if not isinstance(table, dict):
+        raise ValueError(f"{path}: not a table (dict)")
+    return table
+
+
 def load_critic(L: Learner, path: str):
     """Import a V table pickled by write_outputs (a dict keyed like the reference's V)."""
-    with open(path, "rb") as f:
-        table = pickle.load(f)   # written by this tool (write_outputs), never a reference file
+    table = _load_table(path)
     conv = K.from_rank_tuple if L.variant in ("unified", "trained") else K.from_cells_bytes
     keys = np.array([conv(k) for k in table], np.uint64)
     vals = np.array(list(table.values()), np.float64)
@@ -60,16 +69,17 @@ def _key_obj(variant, k):
     return K.to_rank_tuple(k) if variant in ("unified", "trained") else K.to_cells_bytes(k)
 
 
-def trajectory_selection(E: int, per_env: int, every: int):
+def trajectory_selection(E: int, per_env: int, every: int, env_base: int = 0):
     """Envs and capture phases for the trajectories of every `every`-th episode.
 
-    Within a configuration the reported episodes are numbered env-major, episode
-    n = e * per_env + k + 1 for env e's k-th episode (k < per_env); the reference keeps
-    the trajectory of every episode with n % every == 0 (run_actor_only_training.py:199-218),
-    i.e. (k + phase_e) % every == 0 with phase_e = (e * per_env + 1) % every."""
+    Within a configuration the reported episodes are numbered env-major over the global
+    envs, episode n = g * per_env + k + 1 for global env g's k-th episode (k < per_env); the
+    reference keeps the trajectory of every episode with n % every == 0
+    (run_actor_only_training.py:199-218), i.e. (k + phase_g) % every == 0 with
+    phase_g = (g * per_env + 1) % every.  Returns local env indices (g = env_base + e)."""
     envs, phases = [], []
     for e in range(E):
-        ph = (e * per_env + 1) % every
+        ph = ((env_base + e) * per_env + 1) % every
         if (-ph) % every < per_env:
             envs.append(e)
             phases.append(ph)
@@ -89,35 +99,52 @@ def save_trajectory(out_dir: str, N: int, episode: int, total: int, positions: l
 def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per_config: int,
                    eps_start: float | None = None, eps_end: float | None = None, out_dir: str | None = None,
                    log_every: int = 16, verbose: bool = True, trajectory_every: int = 0,
-                   eps_phase: bool = True) -> dict:
+                   eps_phase: bool = True, group: "_Group | None" = None, global_envs: int | None = None) -> dict:
     """Run every (radius, N) configuration; return per-configuration statistics and
     (when `out_dir` is given) write the reference's output files there, with the
     trajectory of every `trajectory_every`-th episode under out_dir/trajectories.
 
+    A radius of None places over every free cell (the full room: the C5 workload,
+    256x256 with 8,192 agents).  Sharded (`group` holds a TableSync): every rank steps its
+    own global envs [env_base, env_base + E) of G = `global_envs`, the tables are shared,
+    the episode rows of all ranks are merged and rank 0 writes the outputs -- the files a
+    single process stepping all G envs writes.
+
     Epsilon (actor modes) decays linearly over the P = episodes_per_config episodes of a
     configuration (run_unified_actor_training.py:253-259: episode j of P explores with
-    start + (end - start) * j / P).  With fewer envs than P, env e runs ceil(P / E)
-    episodes and decays over its own; with E >= P (one episode per env) and eps_phase,
-    env g plays episode 1 + g % P of the schedule, so the E episodes cover it."""
+    start + (end - start) * j / P).  With fewer envs than P, env g runs ceil(P / G) episodes
+    and decays over its own; with G >= P (one episode per env) and eps_phase, env g plays
+    episode 1 + g % P of the schedule, so the G episodes cover it.  Every env runs exactly
+    ceil(P / G) episodes per configuration (ffm_learner_set_episode_caps): no episode trains
+    the tables without being reported."""
     L = learner
+    g = group or _Group()
     E = L.n_envs
-    per_env = max(1, math.ceil(episodes_per_config / E))
-    phased = bool(eps_phase) and per_env == 1 and E >= episodes_per_config > 1
+    G = int(global_envs or E * g.world)
+    env_base = L.env_base
+    per_env = max(1, math.ceil(episodes_per_config / G))
+    phased = bool(eps_phase) and per_env == 1 and G >= episodes_per_config > 1
     chunk = max(1, min(int(log_every), 16))      # the episode log holds 16 steps of episode ends
     rows, configs = [], []
     episode_num = 0
     n_traj = 0
     t_start = time.time()
-    tsel, tph = (trajectory_selection(E, per_env, trajectory_every) if trajectory_every > 0
+    tsel, tph = (trajectory_selection(E, per_env, trajectory_every, env_base) if trajectory_every > 0
                  else (np.zeros(0, np.int32), None))
     if len(tsel):
         L.set_trajectory_capture(tsel, period=trajectory_every, phases=tph, capacity_rows=len(tsel) * chunk * 2)
+    L.set_episode_caps(np.full(E, per_env, np.int32))
+    if out_dir and g.rank == 0:
+        os.makedirs(out_dir, exist_ok=True)
     for radius in radius_list:
-        avail = available_cells(L.map, exit_pos, radius)
+        avail = available_cells(L.map, exit_pos, radius) if radius is not None else int((L.map == 0).sum())
         for N in n_list:
             if N > avail:                                # run_unified_critic_training.py:190-197
                 continue
-            L.set_radius_placement(exit_pos, radius, N)
+            if radius is None:
+                L.set_placement(None, n_agents=N)        # every free cell: the full-room reset
+            else:
+                L.set_radius_placement(exit_pos, radius, N)
             if eps_start is not None and L.actor:
                 # local linear decay per configuration (run_unified_actor_training.py:253-259)
                 if phased:
@@ -129,7 +156,7 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
             L.reset()
             done, trajs = [], {}
             while True:
-                L.step(chunk)
+                g.step(L, chunk)
                 d = L.drain_episodes()
                 if len(d):
                     done.append(d)
@@ -138,70 +165,81 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
                         st, ps = trajs.setdefault(key, ([], []))
                         st.extend(val[0])
                         ps.extend(val[1])
-                if L.episodes()[0].min() >= per_env:
+                if g.min_int(int(L.episodes()[0].min())) >= per_env:
                     break
-            ended = np.concatenate(done)
+            ended = np.concatenate(done) if done else np.zeros((0, 4), np.int32)
             ended = ended[ended[:, 1] < per_env]
-            ended = ended[np.lexsort((ended[:, 1], ended[:, 0]))]   # env-major: episode e * per_env + k + 1
             v1 = L.table_size("V")
             h1 = L.table_size("H") if L.actor else 0
             base = episode_num
-            for idx, (env, k, steps, emptied) in enumerate(ended.tolist()):
-                episode_num += 1
-                j, span = ((k + 1 + env % episodes_per_config, episodes_per_config) if phased   # env: global id
-                           else (k + 1, per_env))
-                eps = (min(max(eps_start + (eps_end - eps_start) * (j / span), 0.0), 1.0)
-                       if eps_start is not None and L.actor else 0.0)
-                rows.append([episode_num, len(configs) + 1, radius, N, steps, v1, h1, f"{eps:.6f}"])
+            for env, k, steps, emptied in ended.tolist():
+                idx = env * per_env + k                  # env-major position among all G * per_env episodes
                 tr = trajs.get((env, k))
                 if tr is not None and out_dir and (idx + 1) % trajectory_every == 0:
                     assert len(tr[0]) == steps and tr[0] == list(range(1, steps + 1)), "trajectory rows"
                     save_trajectory(os.path.join(out_dir, "trajectories"), N, idx + 1, base + idx + 1, tr[1],
                                     steps)
                     n_traj += 1
+            ended = np.concatenate(g.gather(ended))
+            ended = ended[np.lexsort((ended[:, 1], ended[:, 0]))]   # env-major: episode g * per_env + k + 1
+            for env, k, steps, emptied in ended.tolist():
+                episode_num += 1
+                j, span = ((k + 1 + env % episodes_per_config, episodes_per_config) if phased   # env: global id
+                           else (k + 1, per_env))
+                eps = (min(max(eps_start + (eps_end - eps_start) * (j / span), 0.0), 1.0)
+                       if eps_start is not None and L.actor else 0.0)
+                rows.append([episode_num, len(configs) + 1, "full" if radius is None else radius, N, steps, v1, h1,
+                             f"{eps:.6f}"])
             mean = float(ended[:, 2].mean())
             configs.append({"radius": radius, "N": N, "episodes": len(ended), "mean_steps": mean,
                             "std_steps": float(ended[:, 2].std()), "emptied": int(ended[:, 3].sum()),
                             "v_before": v0, "v_after": v1})
-            if verbose:
-                print(f"radius={radius:2d}, N={N:3d}: mean steps={mean:7.2f} over {len(ended)} episodes, "
-                      f"V {v0} -> {v1}", flush=True)
+            if verbose and g.rank == 0:
+                print(f"radius={'full' if radius is None else radius}, N={N:3d}: mean steps={mean:7.2f} over "
+                      f"{len(ended)} episodes, V {v0} -> {v1}", flush=True)
     if len(tsel):
         L.set_trajectory_capture([])
-    result = {"configs": configs, "rows": rows, "seconds": time.time() - t_start, "trajectories": n_traj}
+    L.set_episode_caps(None)
+    n_traj = int(sum(g.gather(n_traj)))
+    result = {"configs": configs, "rows": rows, "seconds": time.time() - t_start, "trajectories": n_traj,
+              "global_envs": G}
     if out_dir:
-        write_outputs(L, result, out_dir, exit_pos, radius_list, n_list, episodes_per_config)
+        g.flush()
+        if g.rank == 0:
+            tables = {w: _pickle_table(L, w) for w in (("V", "H") if L.actor else ("V",))}
+            write_outputs(L, result, out_dir, exit_pos, radius_list, n_list, episodes_per_config, tables)
     return result
 
 
-def write_outputs(L: Learner, result: dict, out_dir: str, exit_pos, radius_list, n_list, episodes_per_config):
+def write_outputs(L: Learner, result: dict, out_dir: str, exit_pos, radius_list, n_list, episodes_per_config,
+                  tables: dict | None = None):
     """steps_per_episode.csv (run_unified_actor_training.py:407-431), summary.txt, V / H
-    tables pickled as the reference's get_v_table / get_h_table dicts."""
+    tables pickled as the reference's get_v_table / get_h_table dicts (`tables`: those dicts,
+    exported beforehand; default: exported here)."""
+    tables = tables or {w: _pickle_table(L, w) for w in (("V", "H") if L.actor else ("V",))}
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, "steps_per_episode.csv"), "w", newline="", encoding="utf-8") as f:
         w = csv.writer(f)
         w.writerow(["episode_num", "config_idx", "radius", "N", "steps", "v_table_size", "h_table_size",
                     "epsilon"])
         w.writerows(result["rows"])
-    vk, vv = L.export_table("V")
     with open(os.path.join(out_dir, "V_table.pkl"), "wb") as f:
-        pickle.dump({_key_obj(L.variant, k): float(v) for k, v in zip(vk.tolist(), vv.tolist())}, f)
+        pickle.dump(tables["V"], f)
     if L.actor:
-        hk, hv = L.export_table("H")
         with open(os.path.join(out_dir, "H_table.pkl"), "wb") as f:
-            pickle.dump({_key_obj(L.variant, k): [float(x) for x in r] for k, r in zip(hk.tolist(), hv.tolist())},
-                        f)
+            pickle.dump(tables["H"], f)
     with open(os.path.join(out_dir, "summary.txt"), "w", encoding="utf-8") as f:
         f.write("=" * 80 + "\n")
         f.write(f"batched curriculum ({L.variant}{'/' + L.mode if L.variant == 'unified' else ''}), "
-                f"{L.n_envs} envs, seed-keyed Philox streams\n")
+                f"{result.get('global_envs', L.n_envs)} envs, seed-keyed Philox streams\n")
         f.write("=" * 80 + "\n")
         f.write(f"exit: {tuple(exit_pos)}\nradius list: {list(radius_list)}\nN list: {list(n_list)}\n")
         f.write(f"episodes per configuration: {episodes_per_config}\nparams: {L.params}\n")
-        f.write(f"final V states: {L.table_size('V')}\n")
+        f.write(f"final V states: {len(tables['V'])}\n")
         f.write(f"seconds: {result['seconds']:.1f}\n\nper configuration:\n" + "-" * 80 + "\n")
         for c in result["configs"]:
-            f.write(f"radius={c['radius']:2d}, N={c['N']:3d}: mean steps={c['mean_steps']:7.2f}, "
+            rad = "full" if c["radius"] is None else f"{c['radius']:2d}"
+            f.write(f"radius={rad}, N={c['N']:3d}: mean steps={c['mean_steps']:7.2f}, "
                     f"V states {c['v_before']:6d} -> {c['v_after']:6d} (+{c['v_after'] - c['v_before']:5d})\n")
 
 
@@ -291,8 +329,10 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
 
     Episodes are numbered env-major over the global envs: env g's k-th episode of pattern
     i is pattern episode g * per_env + k + 1 (per_env = ceil(P / G) for G global envs) and
-    run episode i * P + that; the first P of every pattern are reported (the envs past them
-    run on, unreported, until every env has ended per_env episodes).  With `eps`, the
+    run episode i * P + that.  Env g runs exactly the min(per_env, P - g * per_env) episodes
+    numbered <= P (ffm_learner_set_episode_caps; the envs past their quota stay empty until
+    the pattern ends), so the tables learn from exactly the P episodes of a pattern the
+    reference's driver runs, every one of them reported.  With `eps`, the
     explore rate follows the drivers' one linear schedule over all episodes of the run
     (run_actor_only_training.py:190-196: start + (end - start) * (j - 1) / (total - 1) for
     run episode j).  Trajectories of pattern episodes that are multiples of
@@ -327,7 +367,14 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
         tsel, tph = np.asarray(envs, np.int32), np.asarray(phases, np.int32)
         if len(tsel):
             L.set_trajectory_capture(tsel, period=trajectory_every, phases=tph, capacity_rows=len(tsel) * chunk * 2)
+    gids = env_base + np.arange(E, dtype=np.int64)
+    caps = np.clip(P - gids * per_env, 0, per_env).astype(np.int32)   # this rank's envs' episode quotas
+    L.set_episode_caps(caps)
+    prev_n = None
     for pi, N in enumerate(n_list):
+        if g.sync is not None and prev_n:
+            g.sync.rescale(N / prev_n)                     # the touched records grow with N
+        prev_n = N
         L.set_placement(None, n_agents=N)                  # every free cell: the full-room reset
         base = pi * P                                      # run episodes before this pattern
         if eps is not None and actor:
@@ -353,7 +400,7 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
                     st, ps = trajs.setdefault(key, ([], []))
                     st.extend(val[0])
                     ps.extend(val[1])
-            if g.min_int(int(L.episodes()[0].min())) >= per_env:
+            if g.min_int(int((L.episodes()[0] - caps).min())) >= 0:
                 break
         ended = np.concatenate(done) if done else np.zeros((0, 5), np.int64)
         ended = ended[ended[:, 1] < per_env]
@@ -396,6 +443,7 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
             print(f"N={N:3d}: mean steps={np.mean(pattern['avg_steps']):7.2f} over {len(rows)} episodes, "
                   f"V {L.table_size('V')}, H {L.table_size('H') if actor else 0}", flush=True)
     g.flush()
+    L.set_episode_caps(None)
     result = {"n_list": list(n_list), "episodes_per_n": P, "model_params": dict(params or {}),
               "results_by_n": all_results, "all_episodes": episode_results, "total_time": time.time() - t_start,
               "trajectories": n_traj}
@@ -502,7 +550,9 @@ def main(argv=None):
     ap.add_argument("--map", default=None, help="map .npy (default: the synthetic --size room)")
     ap.add_argument("--sff", default=None, help="SFF .npy (default: the L1 distance field of the map)")
     ap.add_argument("--envs", type=int, default=4096, help="envs per rank")
-    ap.add_argument("--radius", default="3,5,7,9,11,13,15")
+    ap.add_argument("--radius", default="3,5,7,9,11,13,15",
+                    help="radius list of the curriculum, or 'full' for full-room placement over every free cell "
+                         "(the C5 workload: --size 256 --n 8192 --mode actor_only)")
     ap.add_argument("--n", default=None, help="N list (default: the driver's)")
     ap.add_argument("--episodes", type=int, default=None, help="episodes per configuration / per N")
     ap.add_argument("--max-steps", type=int, default=None)
@@ -536,22 +586,26 @@ def main(argv=None):
     if a.critic and a.variant == "actor_only":
         # model/ffm_actor_only.py:55-66 re-keys the pretrained critic by tuples of ints, which never
         # equal the step's pickled-bytes keys: the entries only count (the drop-in class does the same)
-        with open(a.critic, "rb") as f:
-            table = pickle.load(f)   # a V table this tool wrote (never a reference file)
-        inert = {tuple(tuple(int(x) for x in sub) for sub in pickle.loads(k)): v for k, v in table.items()}
+        table = _load_table(a.critic)
+        inert = {tuple(tuple(int(x) for x in sub) for sub in K.loads_key(k)): v for k, v in table.items()}
     elif a.critic:
         load_critic(L, a.critic)
-    if a.variant == "unified":
-        if dev is not None:
-            raise SystemExit("the radius curriculum runs on one device (use --variant actor_only / ac to shard)")
-        es, ee = d["eps"]
-        run_curriculum(L, (0, m.shape[1] // 2), [int(x) for x in a.radius.split(",")], n_list, d["episodes"], es, ee,
-                       a.out, trajectory_every=d["trajectory_every"] if L.actor else 0, eps_phase=not a.no_eps_phase)
-        return
     group = _Group()
     if dev is not None:
         from .dist import TableSync
+        # ffm_unified's tables: the owner-sharded tiled exchange on large maps at block size 1
+        # (C5), the dense all-reduce otherwise; the 13-cell tables: record all-gathers
         group = _Group(TableSync(L, device="cuda", capacity=None))
+    if a.variant == "unified":
+        es, ee = d["eps"]
+        radius = [None] if a.radius == "full" else [int(x) for x in a.radius.split(",")]
+        run_curriculum(L, (0, m.shape[1] // 2), radius, n_list, d["episodes"], es, ee, a.out,
+                       trajectory_every=d["trajectory_every"] if L.actor else 0, eps_phase=not a.no_eps_phase,
+                       group=group, global_envs=a.envs * group.world)
+        if dev is not None:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
     run_per_n(L, n_list, d["episodes"], d["eps"], a.out, d["trajectory_every"] if L.actor else 0, group,
               params=d["params"], inert_v=inert)
     if dev is not None:

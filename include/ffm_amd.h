@@ -387,6 +387,13 @@ int ffm_learner_set_epsilon_phase(ffm_learner* l, int32_t period);
  * run `stride` episodes cover a run-wide schedule with episodes numbered env-major (the single
  * linear schedule over all episodes of run_actor_only_training.py:186-196). */
 int ffm_learner_set_epsilon_stride(ffm_learner* l, int64_t stride);
+/* Per-env episode quota of the auto-reset (the drivers' episode counts,
+ * run_actor_only_training.py:186-188 / run_unified_actor_training.py:247-252: the run stops
+ * after P episodes): env e is re-placed until it has ended caps[e] episodes since the last
+ * ffm_learner_reset, then stays empty (no agents, no table reads or increments) until the
+ * next reset; caps[e] <= 0 leaves env e empty from the reset on.  n = n_envs (host array)
+ * sets the quotas, n = 0 removes them (every env re-placed forever, the default). */
+int ffm_learner_set_episode_caps(ffm_learner* l, const int32_t* caps, int64_t n);
 /* Ended episodes since the last drain, in no particular order: records of 4 int32
  * {global env, episode index, steps, 1 = emptied / 0 = truncated at max_steps}
  * (the per-episode rows of run_*_training.py's steps_per_episode.csv).  *dropped counts

@@ -1110,3 +1110,124 @@ def test_gloo_world2_owner_table_sync_equals_one_learner(mode, tmp_path):
             o0, o = np.argsort(k0), np.argsort(k)
             assert np.array_equal(k[o], k0[o0]), w
             assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), w
+
+
+def test_learner_episode_caps_stop_envs_after_their_quota():
+    """ffm_learner_set_episode_caps: env e ends exactly caps[e] episodes after the reset and
+    then stays empty (a zero quota: empty from the reset).  critic_only's policy does not read
+    the tables, so every env's first caps[e] episodes are those of an uncapped run, step for
+    step (placement and decision streams are keyed by step, env and agent)."""
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    E, N, maxs = 64, 20, 40
+    caps = (np.arange(E) % 4).astype(np.int32)
+    logs = []
+    for capped in (False, True):
+        L = _learner(m, s, "unified", n_envs=E, n_agents=N, mode="critic_only", params={"block_size": 1}, seed=5,
+                     max_steps=maxs)
+        if capped:
+            L.set_episode_caps(caps)
+        L.reset()
+        done = []
+        for _ in range(20):
+            L.step(16)
+            done.append(L.drain_episodes())
+        log = np.concatenate(done)
+        eps, _ = L.episodes()
+        _, cnt, _ = L.get_state()
+        if capped:
+            assert np.array_equal(eps, caps)
+            assert (cnt == 0).all()
+            assert np.array_equal(np.bincount(log[:, 0], minlength=E), caps)
+            L.set_episode_caps(None)
+            L.reset()
+            _, cnt, _ = L.get_state()
+            assert (cnt == N).all()                        # quotas removed: every env placed again
+        L.close()
+        logs.append(log)
+    full, capped_log = logs
+    keep = full[full[:, 1] < caps[full[:, 0]]]
+    assert np.array_equal(keep[np.lexsort((keep[:, 1], keep[:, 0]))],
+                          capped_log[np.lexsort((capped_log[:, 1], capped_log[:, 0]))])
+
+
+def _c5_curriculum_run(tmp, world=1, rank=0, sync=None, envs=4):
+    """The C5 workload through ffm_amd.train.run_curriculum's full-room mode: 256x256 room,
+    8,192 agents, ffm_unified actor_only with run_unified_actor_training.py's MODEL_PARAMS,
+    max_steps 300, epsilon 0.2 -> 0.01, one episode per env, a trajectory every 2nd."""
+    from ffm_amd import train as T
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(256, 256)
+    d = T.driver_settings("unified")
+    E = envs // world
+    L = _learner(m, l1_sff(m), "unified", n_envs=E, n_agents=8192, mode="actor_only", params=d["params"], seed=13,
+                 max_steps=d["max_steps"], env_base=rank * E)
+    g = T._Group(sync(L) if sync else None)
+    res = T.run_curriculum(L, (0, 128), [None], [8192], envs, *d["eps"], tmp, verbose=False, trajectory_every=2,
+                           group=g, global_envs=envs)
+    L.close()
+    return res
+
+
+def _c5_curriculum_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ffm_amd.dist import TableSync
+
+        def sync(L):
+            ts = TableSync(L, device="cuda", capacity=None)
+            assert ts.owner                     # C5 shards through the owner-sharded tile exchange
+            return ts
+
+        _c5_curriculum_run(out, world, rank, sync=sync)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c5_curriculum_sharded_gloo_world2_equals_single(tmp_path):
+    """Row R3: the C5 learning loop (full-room ffm_unified actor_only, 256x256, 8,192 agents)
+    sharded over two ranks on one GPU (gloo; TableSync's owner-sharded tile exchange; global
+    env ids) writes the files of one process stepping the same 4 global envs:
+    steps_per_episode.csv and the trajectories identical, the V / H pickles equal as dicts
+    (keys and value bits; dict order is insertion order, which the ranks' exchange changes)."""
+    import csv
+    import pickle
+    import socket
+    import torch.multiprocessing as mp
+    one = tmp_path / "one"
+    res = _c5_curriculum_run(str(one))
+    assert res["configs"][0]["episodes"] == 4 and res["trajectories"] == 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    two = tmp_path / "two"
+    mp.spawn(_c5_curriculum_worker, args=(2, port, str(two)), nprocs=2, join=True)
+    with open(one / "steps_per_episode.csv") as f:
+        a = list(csv.reader(f))
+    with open(two / "steps_per_episode.csv") as f:
+        b = list(csv.reader(f))
+    assert a == b and len(a) == 5 and all(r[2] == "full" and r[3] == "8192" for r in a[1:])
+    for name in ("V_table.pkl", "H_table.pkl"):
+        with open(one / name, "rb") as f:
+            x = pickle.load(f)      # written by this test's runs
+        with open(two / name, "rb") as f:
+            y = pickle.load(f)
+        assert x.keys() == y.keys() and len(x) > 10000, name
+        for k in x:
+            assert np.array_equal(np.asarray(x[k], np.float64).view(np.uint64),
+                                  np.asarray(y[k], np.float64).view(np.uint64)), name
+    ta = sorted(p.name for p in (one / "trajectories").iterdir())
+    tb = sorted(p.name for p in (two / "trajectories").iterdir())
+    assert ta == tb and len(ta) == 2
+    for n in ta:
+        za, zb = np.load(one / "trajectories" / n, allow_pickle=True), np.load(two / "trajectories" / n,
+                                                                              allow_pickle=True)
+        assert int(za["steps"]) == int(zb["steps"]) and len(za["positions"]) == len(zb["positions"])
+        assert all(np.array_equal(p, q) for p, q in zip(za["positions"], zb["positions"]))
+    sa = (one / "summary.txt").read_text().splitlines()
+    sb = (two / "summary.txt").read_text().splitlines()
+    assert [l for l in sa if not l.startswith("seconds")] == [l for l in sb if not l.startswith("seconds")]
