@@ -83,6 +83,8 @@ struct ffm_learner {
     long long eplog_cap = 0;
     int F_all = 0;                           // free cells of the map (placement capacity)
     ffm::TrajCapture traj{};                 // trajectory capture (n_sel = 0: off)
+    bool v_chain = false;                    // LearnArgs::v_chain: a batched step ran since the last
+                                             // set_state / V import (agents' s are the last step's s')
     int sync_period = 1;                     // tables applied every sync_period-th step
     int since_apply = 0;                     // steps since the last apply
     bool external_sync = false;              // driven by a multi-rank TableSync: no local flush
@@ -229,6 +231,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.dff_in = l->d_dff[l->cur]; a.dff_out = l->d_dff[l->cur ^ 1];
     a.episodes = l->d_eps; a.ep_steps = l->d_ep_steps; a.done = l->d_done; a.nstart = l->d_nstart;
     a.ep_cap = l->d_epcap;
+    a.v_chain = l->v_chain ? 1 : 0;
     a.counters = l->d_ctr;
     a.V = l->V.t; a.Ht = l->H.t;
     a.hstat = l->d_hstat; a.hpart = l->d_hpart; a.recs = l->d_recs; a.overflow = l->d_overflow;
@@ -527,6 +530,7 @@ static int phase_local(ffm_learner* l, hipStream_t s) {
         l->hstat_valid = true;
     }
     HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
+    l->v_chain = true;
     l->phase = 1;
     return FFM_OK;
 }
@@ -617,6 +621,7 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             const bool tt = !l->single_tm && !tstart_t_off();
             if (tt) a.tstart_out = l->d_tstartT;
             HIP_TRY(ffm::launch_learn_batch(a, s));
+            l->v_chain = true;
             a.tstart_out = nullptr;
             if (l->single_tm) {      // records reordered tile-major, then the passes
                 a.ow = 1;
@@ -765,8 +770,10 @@ int ffm_learner_set_state(ffm_learner* l, int64_t env0, int64_t n, const uint16_
             for (int j = 0; j < counts[i]; j++) seen[positions[i * A + j]] = 0;
         }
     }
-    if (positions)
+    if (positions) {
+        l->v_chain = false;      // the next step's s are not the last step's s'
         HIP_TRY(hipMemcpyAsync(l->d_pos + env0 * A, positions, (size_t)n * A * 2, hipMemcpyHostToDevice, s));
+    }
     if (counts) HIP_TRY(hipMemcpyAsync(l->d_cnt + env0, counts, (size_t)n * 4, hipMemcpyHostToDevice, s));
     if (dff)
         HIP_TRY(hipMemcpyAsync(l->d_dff[l->cur] + env0 * l->HW, dff, (size_t)n * l->HW * 4, hipMemcpyHostToDevice, s));
@@ -931,6 +938,7 @@ int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys
         return fail(FFM_E_INVALID, "import between two applies of a shared learner: TableSync.flush() first");
     if (int rc = flush_pending(l, s)) return rc;
     if (which == FFM_TABLE_H) l->hstat_valid = l->tstats_valid = false;
+    if (which == FFM_TABLE_V) l->v_chain = false;   // V(s) no longer known present
     HIP_TRY(clear_table(l, *T, which == FFM_TABLE_V ? l->L.v_default : 0.0, s));
     if (n > 0) {
         unsigned long long* dk = nullptr;
@@ -1011,6 +1019,7 @@ int ffm_learner_step_tiled_local(ffm_learner* l, void* stream) {
     ffm::LearnArgs a = make_args(l);
     a.trecs = l->d_trecs;
     HIP_TRY(ffm::launch_learn_batch(a, s));
+    l->v_chain = true;
     l->phase = 5;
     return FFM_OK;
 }
@@ -1124,6 +1133,7 @@ int ffm_learner_step_owner_local(ffm_learner* l, void* stream) {
     ffm::LearnArgs a = owner_args(l);
     a.trecs = l->d_trecs;
     HIP_TRY(ffm::launch_learn_batch(a, s));
+    l->v_chain = true;
     HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt, l->d_pack, s));
     HIP_TRY(ffm::launch_learn_new_slots(l->V.t, l->d_newv, l->d_xcnt + l->ow, s));
     if (l->actor) HIP_TRY(ffm::launch_learn_new_slots(l->H.t, l->d_newh, l->d_xcnt + l->ow + 1, s));

@@ -94,6 +94,9 @@ struct LearnArgs {
     int* done;                  // [E] re-place at the end of this step
     const int* ep_cap;          // [E] episodes env e runs before it stays empty (nullptr: no quota)
     int* nstart;                // [E] live agents at step start
+    int v_chain;                // every live agent's V(s) is present: its s was the previous step's s',
+                                // inserted then (cleared after set_state / import; an env's first step
+                                // after a placement has ep_steps 0)
     unsigned long long* counters;  // [E][4] agent_steps, exits, resets, steps
     LearnTable V, Ht;
     double* hstat;              // [4] has, nonfinite, min, max of H (step start)

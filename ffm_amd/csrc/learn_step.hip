@@ -35,6 +35,14 @@ __device__ __forceinline__ double* tval(const LearnTable& T, size_t h) {
     return reinterpret_cast<double*>(T.rec + h * T.stride + 1);
 }
 
+// A dense record's key and first value in one 16-B load (V: the whole record; H: the key
+// and action 0).  The key is stored after the presence bit is set, so a non-empty key
+// means the slot is present and its presence word need not be read; an empty key sends
+// the caller to dense_ensure (which then finds the bit of a concurrent insert).
+__device__ __forceinline__ ulonglong2 trec16(const LearnTable& T, size_t h, int i = 0) {
+    return *reinterpret_cast<const ulonglong2*>(T.rec + h * T.stride + 2 * i);
+}
+
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
     z ^= z >> 33; z *= 0xff51afd7ed558ccdULL;
     z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ULL;
@@ -1340,6 +1348,7 @@ void learn_batch_kernel(LearnArgs a) {
     const bool live = e < a.E;
     const uint32_t genv = (uint32_t)(a.env_base + e);
     const int n = live ? a.cnt[e] : 0;
+    const bool vchain = a.v_chain && live && a.ep_steps[e] > 0;   // every V(s) was inserted as a V(s')
     constexpr bool UNI = VK == 1;
     const int variant = UNI ? (int)kVarUnified : a.variant;
     const bool actor = UNI || variant == kVarActorOnly || (variant == kVarUnified && a.mode != kModeCritic);
@@ -1529,8 +1538,13 @@ void learn_batch_kernel(LearnArgs a) {
                 } else if (hdense) {
                     const int h = (int)dense_slot(sk, a.Ht);
                     if (KEYS) hsl[j] = h;
-                    actor_policy(a, tval(a.Ht, h), coord, valid, dff, hs, false, P);
-                    dense_ensure(a.Ht, (uint32_t)h, sk);
+                    // the record's key with the row (one line): present rows skip the bitmap
+                    const ulonglong2 r0 = trec16(a.Ht, h, 0), r1 = trec16(a.Ht, h, 1), r2 = trec16(a.Ht, h, 2);
+                    const double hr[5] = {__longlong_as_double((long long)r0.y), __longlong_as_double((long long)r1.x),
+                                          __longlong_as_double((long long)r1.y), __longlong_as_double((long long)r2.x),
+                                          __longlong_as_double((long long)r2.y)};
+                    actor_policy(a, hr, coord, valid, dff, hs, false, P);
+                    if (r0.x == kEmptyKey) dense_ensure(a.Ht, (uint32_t)h, sk);
                 } else {
                     double hr[5];
                     const int h = tab_get_row<5>(a.Ht, sk, a.overflow, hr);
@@ -1678,11 +1692,14 @@ void learn_batch_kernel(LearnArgs a) {
             if (vdense) {
                 if (!BK_WEXIT(j)) {
                     sn = (int)dense_slot(nk, a.V);
-                    vn = tval(a.V, sn)[0];
-                    dense_ensure(a.V, (uint32_t)sn, nk);
+                    const ulonglong2 rn = trec16(a.V, sn);      // key and value: one 16-B record
+                    vn = __longlong_as_double((long long)rn.y);
+                    if (rn.x == kEmptyKey) dense_ensure(a.V, (uint32_t)sn, nk);
                 }
                 sv = (int)dense_slot(skj, a.V);
-                dense_ensure(a.V, (uint32_t)sv, skj);
+                // s is the previous step's s' (inserted then) unless the episode starts here
+                // or the tables / positions were replaced since (LearnArgs::v_chain)
+                if (!vchain) dense_ensure(a.V, (uint32_t)sv, skj);
                 if (!(TILED && rec_target(a))) vs = tval(a.V, sv)[0];
             } else {
                 // both home slots in one round trip; the probing / inserting path only for
