@@ -373,6 +373,8 @@ def bench_learner(args, world, rank, torch, dist):
     ev1.record(stream)
     torch.cuda.synchronize()
     step_ms = ev0.elapsed_time(ev1) / nk
+    if world > 1:
+        sync.flush()       # the ranks' key sets merged (the owner exchange keeps V's lazily)
     v_size, h_size = L.table_size("V"), L.table_size("H")
     if rank == 0:
         D = 4 if cfg["variant"] == "actor_only" else 1

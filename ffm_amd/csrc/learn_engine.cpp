@@ -111,15 +111,15 @@ struct ffm_learner {
     uint32_t* d_toff = nullptr;              // [NT] + chunk sums and offsets
     uint32_t* d_hdr = nullptr;               // [ow][ths] per destination: its tiles' record offsets
     ffm::TileRec* d_pack = nullptr;          // [E][A] records, grouped by destination, tile-major
-    long long* d_xcnt = nullptr;             // [kMaxOwners + 2] records per destination, new V / H slots
-    uint32_t* d_newv = nullptr;              // [2 E A] new V slots of the step
-    uint32_t* d_newh = nullptr;              // [2 E A] new H slots (the V list's capacity: one stride)
-    uint32_t* d_vslot = nullptr;             // owner outputs, grown on demand
+    long long* d_xcnt = nullptr;             // [kMaxOwners + 2] records per destination
+    ffm::TileRec* d_opack = nullptr;         // [ow][rcap] the owner exchange's fixed-capacity send blocks
+    long long rcap = 0;                      // records per destination block (set_owner_capacity)
+    uint32_t* d_vslot = nullptr;             // owner outputs: vcap V values, hcap H increments
     double* d_vval = nullptr;
     uint32_t* d_hkey = nullptr;
     long long* d_hq = nullptr;
     unsigned long long* d_on = nullptr;      // [2] V / H output counts
-    size_t ocap = 0;
+    size_t vcap = 0, hcap = 0;
     double* d_tsum = nullptr;                // [ths][5] this rank's tile summaries
     unsigned char* d_bph = nullptr;          // the phase-split batch step's per-env state (learn_batch_phases)
     uint16_t* d_tstartT = nullptr;           // [NT + 1][E] transposed tile offsets (one-device env-major passes)
@@ -155,7 +155,7 @@ static void release(ffm_learner* l) {
                     l->d_eps, l->d_ep_steps, l->d_done, l->d_nstart, l->d_epcap, l->d_ctr, l->d_hstat, l->d_hpart,
                     l->d_recs, l->d_overflow, l->d_mt_np, l->d_mt_py, l->d_scratch, l->d_count,
                     l->d_eplog, l->d_eplog_n, l->d_trecs, l->d_tstart, l->d_tstats, l->d_tdirty, l->d_tcand,
-                    l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_pack, l->d_xcnt, l->d_newv, l->d_newh,
+                    l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_pack, l->d_xcnt, l->d_opack,
                     l->d_vslot, l->d_vval, l->d_hkey, l->d_hq, l->d_on, l->d_tsum, l->d_bph, l->d_tstartT};
     for (void* p : bufs) (void)hipFree(p);
     if (l->h_overflow) (void)hipHostFree(l->h_overflow);
@@ -267,6 +267,7 @@ static int async_overflow(ffm_learner* l) {
     const int32_t ov = l->h_overflow ? __atomic_load_n(l->h_overflow, __ATOMIC_ACQUIRE) : 0;
     if (ov & 1) return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
     if (ov & 4) return fail(FFM_E_INVALID, "asynchronous delta export: record buffer too small (raise its capacity)");
+    if (ov & 8) return fail(FFM_E_INVALID, "owner exchange: a count exceeded its buffer capacity (set_owner_capacity)");
     return FFM_OK;
 }
 
@@ -277,6 +278,7 @@ static int check_overflow(ffm_learner* l, hipStream_t s) {
     if (ov & 1) return fail(FFM_E_NOMEM, "V/H hash table is full (raise log2_v_capacity / log2_h_capacity)");
     if (ov & 2) return fail(FFM_E_HIP, "placement candidate list out of range (reset)");
     if (ov & 4) return fail(FFM_E_INVALID, "asynchronous delta export: record buffer too small (raise its capacity)");
+    if (ov & 8) return fail(FFM_E_INVALID, "owner exchange: a count exceeded its buffer capacity (set_owner_capacity)");
     return FFM_OK;
 }
 
@@ -1053,22 +1055,19 @@ int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank) {
     HIP_TRY(hipDeviceSynchronize());
     int mx = 0;
     for (int q = 0; q < world; q++) mx = std::max(mx, ffm::owner_tiles(l->NT, world, ffm::kOwnChunk, q));
-    const size_t E = (size_t)l->d.n_envs, A = (size_t)l->d.agent_capacity;
     const int ths = mx + 1;
     // the new buffers first: a failed allocation leaves the learner as it was
-    uint32_t* hdr = nullptr; double* tsum = nullptr; uint32_t* newv = nullptr; uint32_t* newh = nullptr;
+    uint32_t* hdr = nullptr; double* tsum = nullptr;
     if (hipMalloc((void**)&hdr, (size_t)world * ths * 4) != hipSuccess ||
-        hipMalloc((void**)&tsum, (size_t)ths * 5 * 8) != hipSuccess ||
-        hipMalloc((void**)&newv, 2 * E * A * 4) != hipSuccess ||
-        hipMalloc((void**)&newh, 2 * E * A * 4) != hipSuccess) {
-        (void)hipFree(hdr); (void)hipFree(tsum); (void)hipFree(newv); (void)hipFree(newh);
+        hipMalloc((void**)&tsum, (size_t)ths * 5 * 8) != hipSuccess) {
+        (void)hipFree(hdr); (void)hipFree(tsum);
         return fail(FFM_E_NOMEM, "hipMalloc (owner exchange)");
     }
     (void)hipFree(l->d_hdr);
     (void)hipFree(l->d_tsum);
-    (void)hipFree(l->d_newv);
-    (void)hipFree(l->d_newh);
-    l->d_hdr = hdr; l->d_tsum = tsum; l->d_newv = newv; l->d_newh = newh;
+    (void)hipFree(l->d_opack);
+    l->d_hdr = hdr; l->d_tsum = tsum; l->d_opack = nullptr;
+    l->rcap = 0;            // the send blocks depend on world: set_owner_capacity again
     l->ow = world;
     l->orank = rank;
     l->ths = ths;
@@ -1076,27 +1075,54 @@ int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank) {
     return FFM_OK;
 }
 
+int ffm_learner_set_owner_capacity(ffm_learner* l, int64_t rec_capacity, int64_t v_capacity, int64_t h_capacity) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    if (rec_capacity < 1 || v_capacity < 1 || h_capacity < 1) return fail(FFM_E_INVALID, "capacities must be >= 1");
+    if ((unsigned long long)rec_capacity * (unsigned long long)l->ow >= (1ull << 32) || v_capacity >= (1ll << 31) ||
+        h_capacity >= (1ll << 31))
+        return fail(FFM_E_INVALID, "owner capacities: world * rec_capacity < 2^32, outputs < 2^31");
+    HIP_TRY(hipDeviceSynchronize());        // queued steps may still use the old buffers
+    const size_t nrec = (size_t)l->ow * (size_t)rec_capacity;
+    ffm::TileRec* pack = nullptr;
+    uint32_t* vs = nullptr; double* vv = nullptr; uint32_t* hk = nullptr; long long* hq = nullptr;
+    if (hipMalloc((void**)&pack, nrec * sizeof(ffm::TileRec)) != hipSuccess ||
+        hipMalloc((void**)&vs, (size_t)v_capacity * 4) != hipSuccess ||
+        hipMalloc((void**)&vv, (size_t)v_capacity * 8) != hipSuccess ||
+        hipMalloc((void**)&hk, (size_t)h_capacity * 4) != hipSuccess ||
+        hipMalloc((void**)&hq, (size_t)h_capacity * 8) != hipSuccess) {
+        (void)hipFree(pack); (void)hipFree(vs); (void)hipFree(vv); (void)hipFree(hk); (void)hipFree(hq);
+        return fail(FFM_E_NOMEM, "hipMalloc (owner exchange capacity)");
+    }
+    (void)hipFree(l->d_opack); (void)hipFree(l->d_vslot); (void)hipFree(l->d_vval);
+    (void)hipFree(l->d_hkey); (void)hipFree(l->d_hq);
+    l->d_opack = pack; l->d_vslot = vs; l->d_vval = vv; l->d_hkey = hk; l->d_hq = hq;
+    l->rcap = rec_capacity;
+    l->vcap = (size_t)v_capacity;
+    l->hcap = (size_t)h_capacity;
+    HIP_TRY(hipMemset(l->d_on, 0, 16));
+    HIP_TRY(hipMemset(l->d_xcnt, 0, (ffm::kMaxOwners + 2) * 8));
+    return FFM_OK;
+}
+
 int ffm_learner_owner_buffers(ffm_learner* l, ffm_owner_buffers* b) {
     if (!l || !b) return fail(FFM_E_INVALID, "null argument");
     if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
-    const size_t E = (size_t)l->d.n_envs, A = (size_t)l->d.agent_capacity;
     b->world = l->ow;
     b->rank = l->orank;
-    b->send_recs = l->d_pack;
-    b->send_rec_capacity = (int64_t)(E * A);
+    b->send_recs = l->d_opack;
+    b->send_rec_capacity = (int64_t)l->rcap;
     b->send_hdr = l->d_hdr;
     b->hdr_stride = l->ths;
     b->counts = reinterpret_cast<int64_t*>(l->d_xcnt);
-    b->new_v = l->d_newv;
-    b->new_h = l->d_newh;
-    b->new_v_capacity = (int64_t)(2 * E * A);
-    b->new_h_capacity = (int64_t)(2 * E * A);
     b->v_slot = l->d_vslot;
     b->v_val = l->d_vval;
     b->h_key = l->d_hkey;
     b->h_q = reinterpret_cast<int64_t*>(l->d_hq);
     b->out_counts = reinterpret_cast<int64_t*>(l->d_on);
-    b->out_capacity = (int64_t)l->ocap;
+    b->v_capacity = (int64_t)l->vcap;
+    b->h_capacity = (int64_t)l->hcap;
     b->tsum = l->d_tsum;
     b->tsum_count = (int64_t)ffm::owner_tiles(l->NT, l->ow, ffm::kOwnChunk, l->orank);
     return FFM_OK;
@@ -1109,20 +1135,15 @@ static ffm::LearnArgs owner_args(ffm_learner* l) {
     a.ochunk = ffm::kOwnChunk;
     a.ths = l->ths;
     a.NTk = ffm::owner_tiles(l->NT, l->ow, ffm::kOwnChunk, l->orank);
+    a.tblk = l->rcap;
     return a;
-}
-
-static ffm::OwnerCounts owner_counts(const int64_t* c, int ranks, int64_t step = 1) {
-    ffm::OwnerCounts oc{};
-    for (int r = 0; r < ranks; r++) oc.n[r] = c ? (long long)c[(size_t)r * step] : 0;
-    return oc;
 }
 
 int ffm_learner_step_owner_local(ffm_learner* l, void* stream) {
     if (!l) return fail(FFM_E_INVALID, "null learner");
     if (!l->tiled_ok || l->sync_period != 1 || !l->tile_major)
         return fail(FFM_E_UNSUPPORTED, "owner step: tiled learner, tile-major records, sync period 1");
-    if (!l->d_newv) return fail(FFM_E_INVALID, "owner step: ffm_learner_set_tile_owners first");
+    if (!l->d_opack) return fail(FFM_E_INVALID, "owner step: ffm_learner_set_tile_owners and set_owner_capacity first");
     if (l->phase != 0) return fail(FFM_E_INVALID, "step_owner_local: previous step not ended");
     if (int rc = async_overflow(l)) return rc;
     hipStream_t s = (hipStream_t)stream;
@@ -1134,46 +1155,15 @@ int ffm_learner_step_owner_local(ffm_learner* l, void* stream) {
     a.trecs = l->d_trecs;
     HIP_TRY(ffm::launch_learn_batch(a, s));
     l->v_chain = true;
-    HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt, l->d_pack, s));
-    HIP_TRY(ffm::launch_learn_new_slots(l->V.t, l->d_newv, l->d_xcnt + l->ow, s));
-    if (l->actor) HIP_TRY(ffm::launch_learn_new_slots(l->H.t, l->d_newh, l->d_xcnt + l->ow + 1, s));
-    else HIP_TRY(hipMemsetAsync(l->d_xcnt + l->ow + 1, 0, 8, s));
+    HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt, l->d_opack, s));
     l->phase = 7;
     return FFM_OK;
 }
 
-int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, const int64_t* recv_counts,
-                             const uint32_t* d_new_v, const uint32_t* d_new_h, const int64_t* new_counts,
-                             int64_t new_stride, void* stream) {
-    if (!l || !d_hdrs || !recv_counts || !new_counts) return fail(FFM_E_INVALID, "null argument");
+int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, void* stream) {
+    if (!l || !d_recs || !d_hdrs) return fail(FFM_E_INVALID, "null argument");
     if (l->phase != 7) return fail(FFM_E_INVALID, "step_owner_v must follow step_owner_local");
     hipStream_t s = (hipStream_t)stream;
-    long long total = 0;
-    for (int r = 0; r < l->ow; r++) {
-        if (recv_counts[r] < 0) return fail(FFM_E_INVALID, "negative record count");
-        total += recv_counts[r];
-    }
-    if (total >= (1ll << 32)) return fail(FFM_E_INVALID, "owner step: 2^32 records or more");
-    if (total > 0 && !d_recs) return fail(FFM_E_INVALID, "null records");
-    // the outputs: at most one V value and one H increment per (slot, action) per record
-    if ((size_t)total > l->ocap) {
-        HIP_TRY(hipStreamSynchronize(s));
-        (void)hipFree(l->d_vslot); (void)hipFree(l->d_vval); (void)hipFree(l->d_hkey); (void)hipFree(l->d_hq);
-        l->d_vslot = nullptr; l->d_vval = nullptr; l->d_hkey = nullptr; l->d_hq = nullptr;
-        const size_t cap = std::max<size_t>((size_t)total + (size_t)total / 4, 1 << 16);
-        if (hipMalloc((void**)&l->d_vslot, cap * 4) != hipSuccess || hipMalloc((void**)&l->d_vval, cap * 8) != hipSuccess ||
-            hipMalloc((void**)&l->d_hkey, cap * 4) != hipSuccess || hipMalloc((void**)&l->d_hq, cap * 8) != hipSuccess) {
-            l->ocap = 0;
-            return fail(FFM_E_NOMEM, "hipMalloc (owner outputs)");
-        }
-        l->ocap = cap;
-    }
-    // the other ranks' new slots join this rank's tables (presence, key, order)
-    HIP_TRY(ffm::launch_learn_adopt_slots(l->V.t, d_new_v, new_stride, owner_counts(new_counts, l->ow, 2), l->ow,
-                                          l->orank, s));
-    if (l->actor)
-        HIP_TRY(ffm::launch_learn_adopt_slots(l->H.t, d_new_h, new_stride, owner_counts(new_counts + 1, l->ow, 2),
-                                              l->ow, l->orank, s));
     l->own_recs = reinterpret_cast<const ffm::TileRec*>(d_recs);
     l->own_hdr = d_hdrs;
     ffm::LearnArgs a = owner_args(l);
@@ -1183,18 +1173,20 @@ int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t*
     a.vout_slot = l->d_vslot;
     a.vout_val = l->d_vval;
     a.vout_n = l->d_on;
+    a.vout_cap = (long long)l->vcap;
     HIP_TRY(ffm::launch_learn_tiles_owner_v(a, s));
     l->phase = 8;
     return FFM_OK;
 }
 
 int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const double* d_v_val,
-                             const int64_t* v_counts, int64_t v_stride, void* stream) {
-    if (!l || !v_counts) return fail(FFM_E_INVALID, "null argument");
+                             const int64_t* d_v_counts, int64_t v_stride, void* stream) {
+    if (!l || !d_v_counts || (l->ow > 1 && (!d_v_slot || !d_v_val))) return fail(FFM_E_INVALID, "null argument");
+    if (v_stride < 0) return fail(FFM_E_INVALID, "v_stride");
     if (l->phase != 8) return fail(FFM_E_INVALID, "step_owner_h must follow step_owner_v");
     hipStream_t s = (hipStream_t)stream;
-    HIP_TRY(ffm::launch_learn_v_scatter(l->V.t, d_v_slot, d_v_val, v_stride, owner_counts(v_counts, l->ow), l->ow,
-                                        l->orank, s));
+    HIP_TRY(ffm::launch_learn_v_scatter(l->V.t, d_v_slot, d_v_val, v_stride, reinterpret_cast<const long long*>(d_v_counts),
+                                        l->ow, l->orank, l->d_overflow, s));
     if (l->actor) {     // the actor's td reads the V every owner updated
         ffm::LearnArgs a = owner_args(l);
         a.trecs = const_cast<ffm::TileRec*>(l->own_recs);
@@ -1203,22 +1195,26 @@ int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const dou
         a.hout_key = l->d_hkey;
         a.hout_q = l->d_hq;
         a.hout_n = l->d_on + 1;
+        a.hout_cap = (long long)l->hcap;
         HIP_TRY(ffm::launch_learn_tiles_owner_h(a, l->d_tsum, s));
     }
     l->phase = 9;
     return FFM_OK;
 }
 
-int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q, const int64_t* h_counts,
-                               int64_t h_stride, const double* d_tsum_all, int64_t tsum_stride, void* stream) {
+int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q,
+                               const int64_t* d_h_counts, int64_t h_stride, const double* d_tsum_all,
+                               int64_t tsum_stride, void* stream) {
     if (!l) return fail(FFM_E_INVALID, "null learner");
     if (l->phase != 9) return fail(FFM_E_INVALID, "step_owner_end must follow step_owner_h");
     hipStream_t s = (hipStream_t)stream;
     ffm::LearnArgs a = owner_args(l);
     if (l->actor) {
-        if (!h_counts || !d_tsum_all) return fail(FFM_E_INVALID, "null argument");
+        if (!d_h_counts || !d_tsum_all || h_stride < 0 || (l->ow > 1 && (!d_h_key || !d_h_q)))
+            return fail(FFM_E_INVALID, "null argument");
         HIP_TRY(ffm::launch_learn_h_deltas(l->H.t, d_h_key, reinterpret_cast<const long long*>(d_h_q), h_stride,
-                                           owner_counts(h_counts, l->ow), l->ow, l->orank, s));
+                                           reinterpret_cast<const long long*>(d_h_counts), l->ow, l->orank,
+                                           l->d_overflow, s));
         HIP_TRY(ffm::launch_learn_tsum_unpack(a, d_tsum_all, tsum_stride, s));
         HIP_TRY(ffm::launch_learn_tile_stats(a, s));     // every rank: the same summaries, the same statistics
     } else {
@@ -1379,7 +1375,7 @@ int ffm_learner_dense_adopt(ffm_learner* l, int32_t which, const uint32_t* d_uni
     DevTable* T = which == FFM_TABLE_V ? &l->V : (which == FFM_TABLE_H && l->actor ? &l->H : nullptr);
     if (!T) return fail(FFM_E_INVALID, "no such table for this variant");
     if (!T->t.dense_by) return fail(FFM_E_UNSUPPORTED, "not a dense (rank-key) table");
-    if (l->phase == 0) return fail(FFM_E_INVALID, "dense_adopt outside a phased step");
+    if (l->phase == 0 && !l->tiled_ok) return fail(FFM_E_INVALID, "dense_adopt outside a phased step");
     HIP_TRY(ffm::launch_learn_dense_adopt(T->t, d_union, (hipStream_t)stream));
     return FFM_OK;
 }

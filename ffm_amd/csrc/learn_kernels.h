@@ -25,13 +25,18 @@ struct LearnRec {
 // and two tile kernels sum a tile of cells' records in LDS and apply them.  A tile owns
 // every slot of its cells (rank-major dense slots: p * (cap / 256) + cell at block 1).
 struct TileRec {
-    uint32_t svk;               // V / H slot of s (bits 0-27), action k (28-31; 15 = no H increment)
+    uint32_t svk;               // V / H slot of s (bits 0-26), H(s) inserted by this rank's step (27; owner
+                                // exchange: the row is new to every other rank), action k (28-31; 15 = none)
     uint32_t snf;               // V slot of s' (bits 0-27; 0x0FFFFFFF = terminal), wexit (28), coll + 1 (29-31)
     double td;                  // ffm_unified both: the TD error with the step-start V (the actor's td);
                                 // otherwise the TD target r + gamma V(s') (the V pass subtracts V(s))
 };
 constexpr int kTileCells = 4;   // cells per tile: a tile's slots are 256 rank patterns x 4 cells
 constexpr uint32_t kTileNoAct = 15u, kTileTerminal = 0x0FFFFFFFu;
+constexpr uint32_t kTileSlot = 0x07FFFFFFu, kTileNewH = 1u << 27;   // svk: slot bits, new-row flag
+// Owner outputs: an H increment's key is slot | action << 28; bit 31 marks the row's first
+// entry when the row is new this step (receivers insert it; q may then be 0).
+constexpr uint32_t kHoutNew = 1u << 31;
 
 struct LearnTable {
     // [cap][stride] 64-bit words, one record per slot: the key (~0 = empty), then
@@ -122,6 +127,8 @@ struct LearnArgs {
     // dealt round-robin over ow ranks; ow <= 1: k itself).
     const uint32_t* thdr;       // nullptr: env-major (tstart)
     int tR, ths, NTk;
+    long long tblk;             // > 0: range r's block starts at record r * tblk (fixed-capacity blocks of the
+                                // sync-free owner exchange; a header offset past tblk is clamped), 0: back to back
     int ow, orank, ochunk;
     // owner mode outputs: the V values the launch's tiles updated (slot, new value) and the
     // H increments (slot | action << 28, fixed-point sum), appended for the other ranks
@@ -131,6 +138,7 @@ struct LearnArgs {
     uint32_t* hout_key;
     long long* hout_q;
     unsigned long long* hout_n;
+    long long vout_cap, hout_cap;   // output capacities: entries past them are dropped and flagged (overflow 8)
     // Phase-split batch step (learn_batch_phases): per env the 2-bit state
     // maps of the current and next positions, the agents in raster order (cell, agent index)
     // and the decide / resolve outputs per raster rank.  nullptr: the fused batch kernel.
@@ -168,11 +176,6 @@ inline __host__ __device__ int owner_tiles(int NT, int ow, int C, int q) {
     if (rem && nch % ow == q) n += rem;
     return n;
 }
-
-// Host-known per-rank element counts of an exchange (kernel argument).
-struct OwnerCounts {
-    long long n[kMaxOwners];
-};
 
 // Trajectory capture of the batched step (ffm_learner_set_trajectory_capture): the
 // selected envs' positions after every step of a captured episode, appended as rows.
@@ -216,14 +219,13 @@ hipError_t launch_learn_tile_pack(const LearnArgs& a, uint32_t* pe, uint32_t* tp
 hipError_t launch_learn_tiles_owner_v(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStream_t s);
 hipError_t launch_learn_tile_stats(const LearnArgs& a, hipStream_t s);
-hipError_t launch_learn_new_slots(const LearnTable& T, uint32_t* out, long long* count, hipStream_t s);
 hipError_t launch_learn_mark(const LearnArgs& a, hipStream_t s);
-hipError_t launch_learn_adopt_slots(const LearnTable& T, const uint32_t* slots, long long stride,
-                                    const OwnerCounts& c, int ranks, int self, hipStream_t s);
+// The other owners' outputs, [ranks][stride] with the counts on the device (counts[r], capped
+// at stride): V values (stored), H increments (applied; a kHoutNew entry inserts its row).
 hipError_t launch_learn_v_scatter(const LearnTable& T, const uint32_t* slots, const double* vals, long long stride,
-                                  const OwnerCounts& c, int ranks, int self, hipStream_t s);
+                                  const long long* counts, int ranks, int self, int* overflow, hipStream_t s);
 hipError_t launch_learn_h_deltas(const LearnTable& T, const uint32_t* keys, const long long* q, long long stride,
-                                 const OwnerCounts& c, int ranks, int self, hipStream_t s);
+                                 const long long* counts, int ranks, int self, int* overflow, hipStream_t s);
 hipError_t launch_learn_tsum_unpack(const LearnArgs& a, const double* tsum, long long stride, hipStream_t s);
 hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);

@@ -167,13 +167,17 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t* ctr) {
 // so a caller may load the values together with the presence word (not after it)
 // and insert afterwards.  Presence is one bit of a 2 MB-scale bitmap that stays in
 // L2; the key is stored for export only.
-__device__ __forceinline__ void dense_ensure(const LearnTable& T, uint32_t h, unsigned long long key) {
+__device__ __forceinline__ bool dense_ensure_new(const LearnTable& T, uint32_t h, unsigned long long key) {
     const uint32_t bit = 1u << (h & 31);
     uint32_t* w = T.present + (h >> 5);
-    if (*w & bit) return;                                 // stale 0 only costs the atomic
-    if (atomicOr(w, bit) & bit) return;
+    if (*w & bit) return false;                           // stale 0 only costs the atomic
+    if (atomicOr(w, bit) & bit) return false;
     tkey(T, h) = key;
     T.order[wave_claim(T.n)] = h;
+    return true;                                          // this lane inserted the slot
+}
+__device__ __forceinline__ void dense_ensure(const LearnTable& T, uint32_t h, unsigned long long key) {
+    (void)dense_ensure_new(T, h, key);
 }
 
 
@@ -1328,6 +1332,9 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB,
 // mode, dense V and H, tiled records (learn_batch_uni) -- so the unrolled agent slots carry
 // none of the other variants' paths (a fraction of the generic kernel's code: fewer
 // instruction-cache misses across 16 waves walking it)
+// per-slot state word (sa) of learn_batch_kernel: bit 15 = the decide phase inserted H(s)
+constexpr uint32_t kSaNewH = 1u << 15;
+
 template <int BS, int EPB, int APT, int D, bool DL, int VK = 0>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(FFM_LBATCH_WAVES, 8)))
 void learn_batch_kernel(LearnArgs a) {
@@ -1401,6 +1408,7 @@ void learn_batch_kernel(LearnArgs a) {
 #define BK_COLL(j) ((int)((sa[j] >> 5) & 31u) - 1)
 #define BK_WINS(j) ((int)((sa[j] >> 10) & 15u))
 #define BK_NXT(j) ((int)(sa[j] >> 16))
+#define BK_NEWH(j) ((sa[j] & kSaNewH) != 0u)
 #pragma unroll
     for (int j = 0; j < APT; j++) {
         const int i = tid + j * LPE;
@@ -1544,7 +1552,7 @@ void learn_batch_kernel(LearnArgs a) {
                                           __longlong_as_double((long long)r1.y), __longlong_as_double((long long)r2.x),
                                           __longlong_as_double((long long)r2.y)};
                     actor_policy(a, hr, coord, valid, dff, hs, false, P);
-                    if (r0.x == kEmptyKey) dense_ensure(a.Ht, (uint32_t)h, sk);
+                    if (r0.x == kEmptyKey && dense_ensure_new(a.Ht, (uint32_t)h, sk)) sa[j] |= kSaNewH;
                 } else {
                     double hr[5];
                     const int h = tab_get_row<5>(a.Ht, sk, a.overflow, hr);
@@ -1643,7 +1651,7 @@ void learn_batch_kernel(LearnArgs a) {
             }
         }
         }
-        sa[j] = (sa[j] & 0x1Fu) | ((uint32_t)(clj + 1) << 5) | ((uint32_t)wnj << 10) | ((uint32_t)nxj << 16);
+        sa[j] = (sa[j] & (0x1Fu | kSaNewH)) | ((uint32_t)(clj + 1) << 5) | ((uint32_t)wnj << 10) | ((uint32_t)nxj << 16);
     }
     // deposits at the winners' own cells (distinct per agent: no races); every
     // agent's next cell joins the next state map unless it is an exit
@@ -1670,6 +1678,7 @@ void learn_batch_kernel(LearnArgs a) {
         long long vq = 0;
         double tdv = 0.0;  // tiled step: the record's td, s' slot and action
         int snv = -1, kk = (int)kTileNoAct;
+        bool newh = BK_NEWH(j);   // this step inserted H(s) here (decide, or an exit-forced agent below)
         do {
             if (i >= n || trained || (FFM_LABLATE & 2)) break;
             unsigned long long skj;
@@ -1741,10 +1750,10 @@ void learn_batch_kernel(LearnArgs a) {
             // the decide phase's H slot; without KEYS, dense tables recompute it (the decide
             // phase inserted it unless the agent was exit-forced) and hashed ones probe again
             int hslj = KEYS ? hsl[j] : (hdense && !BK_WEXIT(j) ? (int)dense_slot(skj, a.Ht) : -1);
-            if (hslj < 0) {     // dense: slot + insert, no probe
-                if (UNI) {
+            if (hslj < 0) {     // dense: slot + insert, no probe (flagged for the owner exchange)
+                if (hdense) {
                     hslj = (int)dense_slot(skj, a.Ht);
-                    dense_ensure(a.Ht, (uint32_t)hslj, skj);
+                    if (dense_ensure_new(a.Ht, (uint32_t)hslj, skj)) newh = true;
                 } else {
                     hslj = tab_get(a.Ht, skj, a.overflow);
                 }
@@ -1765,7 +1774,7 @@ void learn_batch_kernel(LearnArgs a) {
         if (TILED) {
             if (vsl >= 0) {
                 TileRec rc;
-                rc.svk = (uint32_t)vsl | ((uint32_t)kk << 28);
+                rc.svk = (uint32_t)vsl | (newh ? kTileNewH : 0u) | ((uint32_t)kk << 28);
                 rc.snf = (snv >= 0 ? (uint32_t)snv : kTileTerminal) | ((uint32_t)BK_WEXIT(j) << 28) |
                          ((uint32_t)(BK_COLL(j) + 1) << 29);
                 rc.td = tdv;
@@ -2492,6 +2501,12 @@ __device__ __forceinline__ int tm_spans(const LearnArgs& a, int k, uint32_t* rs,
             lo = h[k];
             n = h[k + 1] - lo;
             blk = h[a.NTk];
+            if (a.tblk > 0) {     // fixed-capacity blocks: range r at r * tblk, offsets past tblk clamped
+                const uint32_t cap = (uint32_t)a.tblk, l0 = lo < cap ? lo : cap, l1 = h[k + 1] < cap ? h[k + 1] : cap;
+                lo = l0;
+                n = l1 - l0;
+                blk = 0;
+            }
         }
         uint32_t incl = n, bincl = blk;
 #pragma unroll
@@ -2502,7 +2517,7 @@ __device__ __forceinline__ int tm_spans(const LearnArgs& a, int k, uint32_t* rs,
                 bincl += w;
             }
         }
-        lo += bincl - blk;
+        lo += a.tblk > 0 ? (uint32_t)((long long)r * a.tblk) : bincl - blk;
         if (r < a.tR) {
             rs[r + 1] = incl;
             rb[r] = lo;
@@ -2570,6 +2585,10 @@ __device__ __forceinline__ void vout_push(const LearnArgs& a, const bool (&p)[J]
 #pragma unroll
     for (int j = 0; j < J; j++)
         if (idx[j] >= 0) {
+            if (idx[j] >= a.vout_cap) {       // capacity exceeded: reported at the next sync point
+                atomicOr(a.overflow, 8);
+                continue;
+            }
             a.vout_slot[idx[j]] = slot[j];
             a.vout_val[idx[j]] = v[j];
         }
@@ -2622,15 +2641,39 @@ __device__ __forceinline__ void hout_reserve(const LearnArgs& a, const int (&n)[
     block_append_runs<J>(a.hout_n, n, base, lw);
 }
 
-__device__ __forceinline__ void hout_row(const LearnArgs& a, int base, uint32_t slot, const long long (&q)[5]) {
+// nw: the row is new this step: its first entry carries kHoutNew (receivers insert the row),
+// and a new row without increments still sends one (q = 0; hout_count counts it).
+__device__ __forceinline__ int hout_count(const long long (&q)[5], bool nw) {
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) n += q[k] != 0 ? 1 : 0;
+    return n == 0 && nw ? 1 : n;
+}
+
+__device__ __forceinline__ void hout_row(const LearnArgs& a, int base, uint32_t slot, const long long (&q)[5],
+                                         bool nw) {
     if (!a.hout_n) return;
+    const int n = hout_count(q, nw);
+    if (n == 0) return;
+    if ((long long)base + n > a.hout_cap) {    // capacity exceeded: reported at the next sync point
+        atomicOr(a.overflow, 8);
+        return;
+    }
+    uint32_t flag = nw ? kHoutNew : 0u;
+    bool any = false;
 #pragma unroll
     for (int k = 0; k < 5; k++)
         if (q[k] != 0) {
-            a.hout_key[base] = slot | ((uint32_t)k << 28);
+            a.hout_key[base] = slot | ((uint32_t)k << 28) | flag;
             a.hout_q[base] = q[k];
             base++;
+            flag = 0u;
+            any = true;
         }
+    if (!any) {
+        a.hout_key[base] = slot | kHoutNew;
+        a.hout_q[base] = 0;
+    }
 }
 
 constexpr int kTileEnvChunk = 2 * kTileThreads;   // envs whose ranges one pass gathers
@@ -2816,7 +2859,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
         for (int j = 0; j < kTileJ; j++) {
             own[j] = false;
             if (tid + j * kTileThreads >= m) continue;
-            const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+            const uint32_t sv = rc[j].svk & kTileSlot;
             ix[j] = tile_idx(sv, qsh, Q, c0);
             own[j] = atomicAdd(&ks[ix[j]], 1u) == 0u;
             const double vs = tgt || own[j] ? tval(a.V, sv)[0] : 0.0;
@@ -2829,7 +2872,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
 #pragma unroll
         for (int j = 0; j < kTileJ; j++) {
             nv[j] = 0.0;
-            sl[j] = rc[j].svk & 0x0FFFFFFFu;
+            sl[j] = rc[j].svk & kTileSlot;
             if (own[j]) {
                 nv[j] = v_visits(vv[j], qs[ix[j]], (long long)ks[ix[j]], a.V.alpha);
                 tval(a.V, sl[j])[0] = nv[j];
@@ -2846,7 +2889,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
 #pragma unroll
             for (int j = 0; j < kTileJ; j++) {
                 if (tid + j * kTileThreads >= mw) continue;
-                const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+                const uint32_t sv = rc[j].svk & kTileSlot;
                 const int idx = tile_idx(sv, qsh, Q, c0);
                 atomicAdd(&ks[idx], 1u);
                 add(rc[j], sv, idx, tgt ? tval(a.V, sv)[0] : 0.0);
@@ -2856,7 +2899,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a)
     } else {
         tile_records<TM>(a, t, k, list, wsum, rs, rb, [&](uint32_t g) {
             const TileRec rc = a.trecs[g];
-            const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+            const uint32_t sv = rc.svk & kTileSlot;
             const int idx = tile_idx(sv, qsh, Q, c0);
             atomicAdd(&ks[idx], 1u);
             add(rc, sv, idx, tgt ? tval(a.V, sv)[0] : 0.0);
@@ -3056,6 +3099,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     __shared__ uint16_t pid[kTilePairs];            // pair -> index into hq (valid where pbit is set)
     __shared__ uint32_t pbit[kTilePairs / 32];
     __shared__ uint32_t touched[NS / 32];
+    __shared__ uint32_t newb[NS / 32];               // rows another rank's step inserted (kTileNewH)
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
     __shared__ uint32_t list[kTileList];
@@ -3070,7 +3114,10 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
     for (int i = tid; i < kTileList; i += kTileThreads) hq[i] = 0;
     for (int i = tid; i < kTilePairs / 32; i += kTileThreads) pbit[i] = 0u;
-    if (tid < NS / 32) touched[tid] = 0u;
+    if (tid < NS / 32) {
+        touched[tid] = 0u;
+        newb[tid] = 0u;
+    }
     if (tid == 0) npair = 0;
     // (tile_window's barriers order these stores before any use)
     const int m = tile_window<TM>(a, t, k, list, wsum, rs, rb);
@@ -3092,10 +3139,11 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
         pown[j] = false;
         pr[j] = -1;
         if (tid + j * kTileThreads >= m) continue;
-        const uint32_t sv = rc[j].svk & 0x0FFFFFFFu;
+        const uint32_t sv = rc[j].svk & kTileSlot;
         ix[j] = tile_idx(sv, qsh, Q, c0);
         const uint32_t bit = 1u << (ix[j] & 31);
         own[j] = !(atomicOr(&touched[ix[j] >> 5], bit) & bit);
+        if (rc[j].svk & kTileNewH) atomicOr(&newb[ix[j] >> 5], bit);
         tile_h_vpair(a, rc[j], sv, vn[j], vs[j]);
         if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
         const int act = (int)(rc[j].svk >> 28);
@@ -3126,7 +3174,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
 #pragma unroll
     for (int j = 0; j < kTileJ; j++) {
         if (!own[j]) continue;
-        const double* vp = tval(a.Ht, rc[j].svk & 0x0FFFFFFFu);
+        const double* vp = tval(a.Ht, rc[j].svk & kTileSlot);
 #pragma unroll
         for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
     }
@@ -3138,14 +3186,18 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
         }
     };
     int hn[kTileJ], hb[kTileJ];
+    bool nw[kTileJ];
 #pragma unroll
     for (int j = 0; j < kTileJ; j++) {     // owner mode: each row's nonzero increments, reserved
         hn[j] = 0;
-        if (TM && a.hout_n && own[j]) {
+        nw[j] = false;
+        if (!own[j]) continue;
+        // a row another rank's step inserted joins this rank's table here, and goes out flagged
+        nw[j] = TM && ((newb[ix[j] >> 5] >> (ix[j] & 31)) & 1u);
+        if (TM && a.hout_n) {
             long long q[5];
             row_q(j, q);
-#pragma unroll
-            for (int kk = 0; kk < 5; kk++) hn[j] += q[kk] != 0 ? 1 : 0;
+            hn[j] = hout_count(q, nw[j]);
         }
     }
     if (TM) hout_reserve<kTileJ>(a, hn, hb, wsum);
@@ -3154,9 +3206,10 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
         if (!own[j]) continue;
         long long q[5];
         row_q(j, q);
-        const uint32_t sl = rc[j].svk & 0x0FFFFFFFu;
+        const uint32_t sl = rc[j].svk & kTileSlot;
+        if (nw[j]) dense_ensure(a.Ht, sl, dense_key(sl, qsh, Q, a.Ht.dense_by));
         tile_h_apply(tval(a.Ht, sl), q, hv[j], c);
-        if (TM) hout_row(a, hb[j], sl, q);
+        if (TM) hout_row(a, hb[j], sl, q, nw[j]);
     }
     tile_h_end(a, t, c, smn, smx, sfl);
 }
@@ -3169,6 +3222,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
     constexpr int NS = 256 * kTileCells;
     __shared__ long long hq[NS * 5];
     __shared__ uint32_t touched[NS / 32];
+    __shared__ uint32_t newb[NS / 32];
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
     __shared__ uint32_t list[kTileList];
@@ -3181,7 +3235,10 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
     for (int ci = (int)blockIdx.x; ci < n; ci += (int)gridDim.x) {
         const int t = a.tcand[1 + ci], c0 = t * kTileCells, kt = TM ? own_local(a, t) : t;
         for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
-        for (int i = tid; i < NS / 32; i += kTileThreads) touched[i] = 0u;
+        for (int i = tid; i < NS / 32; i += kTileThreads) {
+            touched[i] = 0u;
+            newb[i] = 0u;
+        }
         __syncthreads();
         TileHCtx c = tile_h_begin(a, t);
         if (TM) {           // tile-major: windows of kTileJ records per thread, the loads first
@@ -3192,12 +3249,13 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
                 double vn[kTileJ], vs[kTileJ];
 #pragma unroll
                 for (int j = 0; j < kTileJ; j++)
-                    if (tid + j * kTileThreads < mw) tile_h_vpair(a, rc[j], rc[j].svk & 0x0FFFFFFFu, vn[j], vs[j]);
+                    if (tid + j * kTileThreads < mw) tile_h_vpair(a, rc[j], rc[j].svk & kTileSlot, vn[j], vs[j]);
 #pragma unroll
                 for (int j = 0; j < kTileJ; j++) {
                     if (tid + j * kTileThreads >= mw) continue;
-                    const int idx = tile_idx(rc[j].svk & 0x0FFFFFFFu, qsh, Q, c0);
+                    const int idx = tile_idx(rc[j].svk & kTileSlot, qsh, Q, c0);
                     atomicOr(&touched[idx >> 5], 1u << (idx & 31));
+                    if (rc[j].svk & kTileNewH) atomicOr(&newb[idx >> 5], 1u << (idx & 31));
                     const int act = (int)(rc[j].svk >> 28);
                     if (act == (int)kTileNoAct) continue;
                     atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + act]),
@@ -3208,7 +3266,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
         } else {
             tile_records<TM>(a, t, kt, list, wsum, rs, rb, [&](uint32_t g) {
                 const TileRec rc = a.trecs[g];
-                const uint32_t sv = rc.svk & 0x0FFFFFFFu;
+                const uint32_t sv = rc.svk & kTileSlot;
                 const int idx = tile_idx(sv, qsh, Q, c0);
                 atomicOr(&touched[idx >> 5], 1u << (idx & 31));
                 if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
@@ -3235,13 +3293,18 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
             }
         }
         int hn[kPer], hb[kPer];
+        bool nw[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
             const int i = tid + j * kTileThreads;
             hn[j] = 0;
-            if (TM && a.hout_n && tch[j])
+            nw[j] = TM && tch[j] && ((newb[i >> 5] >> (i & 31)) & 1u);
+            if (TM && a.hout_n && tch[j]) {
+                long long q[5];
 #pragma unroll
-                for (int kk = 0; kk < 5; kk++) hn[j] += hq[i * 5 + kk] != 0 ? 1 : 0;
+                for (int kk = 0; kk < 5; kk++) q[kk] = hq[i * 5 + kk];
+                hn[j] = hout_count(q, nw[j]);
+            }
         }
         if (TM) hout_reserve<kPer>(a, hn, hb, wsum);
 #pragma unroll
@@ -3252,8 +3315,9 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
             long long q[5];
 #pragma unroll
             for (int kk = 0; kk < 5; kk++) q[kk] = hq[i * 5 + kk];
+            if (nw[j]) dense_ensure(a.Ht, sl, dense_key(sl, qsh, Q, a.Ht.dense_by));
             tile_h_apply(tval(a.Ht, sl), q, hv[j], c);
-            if (TM) hout_row(a, hb[j], sl, q);
+            if (TM) hout_row(a, hb[j], sl, q, nw[j]);
         }
         tile_h_end(a, t, c, smn, smx, sfl);
     }
@@ -3631,13 +3695,16 @@ __global__ __launch_bounds__(kOffThreads) void learn_tile_offsets_kernel(LearnAr
     for (int t = tid; t < a.NT; t += kOffThreads) {
         const int c = t / C, q = c % ow, k = (c / ow) * C + t % C;
         const uint32_t o = coff[c] + tpre[t];
-        toff[t] = o;
+        // fixed-capacity blocks (tblk > 0): destination q's block starts at q * tblk
+        toff[t] = a.tblk > 0 ? (uint32_t)((long long)q * a.tblk) + (o - seg[q]) : o;
         hdr[(size_t)q * a.ths + k] = o - seg[q];
     }
     if (tid < ow) {
         const int n = owner_tiles(a.NT, ow, C, tid);
-        hdr[(size_t)tid * a.ths + n] = seg[tid + 1] - seg[tid];
-        xcnt[tid] = (long long)(seg[tid + 1] - seg[tid]);
+        const uint32_t cnt = seg[tid + 1] - seg[tid];
+        hdr[(size_t)tid * a.ths + n] = cnt;
+        xcnt[tid] = (long long)cnt;
+        if (a.tblk > 0 && (long long)cnt > a.tblk) atomicOr(a.overflow, 8);   // reported at the next sync point
     }
 }
 
@@ -3660,21 +3727,23 @@ __global__ __launch_bounds__(256) void learn_tile_scatter_kernel(LearnArgs a, co
     for (int j = 0; j < kScatterJ; j++)
         if (i0 + j * 256 < n) rc[j] = a.trecs[e * a.A + i0 + j * 256];
 #pragma unroll
-    for (int j = 0; j < kScatterJ; j++) t[j] = (int)(((rc[j].svk & 0x0FFFFFFFu) & (Q - 1u)) / kTileCells);
+    for (int j = 0; j < kScatterJ; j++) t[j] = (int)(((rc[j].svk & kTileSlot) & (Q - 1u)) / kTileCells);
     uint32_t d[kScatterJ];
 #pragma unroll
     for (int j = 0; j < kScatterJ; j++)
         if (i0 + j * 256 < n) d[j] = toff[t[j]] + pe[e * a.NT + t[j]] + (uint32_t)(i0 + j * 256);
+    bool in[kScatterJ];
+#pragma unroll
+    for (int j = 0; j < kScatterJ; j++) {
+        in[j] = i0 + j * 256 < n;
+        // fixed-capacity blocks: a record past its destination's block is dropped (the
+        // offsets kernel flagged the overflow)
+        if (a.tblk > 0 && in[j])
+            in[j] = d[j] < (uint32_t)((long long)((t[j] / kOwnChunk) % (a.ow <= 1 ? 1 : a.ow) + 1) * a.tblk);
+    }
 #pragma unroll
     for (int j = 0; j < kScatterJ; j++)
-        if (i0 + j * 256 < n) out[d[j]] = rc[j];
-}
-
-// Slots this rank's step inserted (order[mark .. n)): the other ranks adopt them.
-__global__ __launch_bounds__(256) void learn_new_slots_kernel(LearnTable T, uint32_t* out, long long* count) {
-    const uint32_t m0 = *T.mark, m1 = *T.n;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *count = (long long)(m1 - m0);
-    for (uint32_t i = m0 + blockIdx.x * 256 + threadIdx.x; i < m1; i += gridDim.x * 256) out[i - m0] = T.order[i];
+        if (in[j]) out[d[j]] = rc[j];
 }
 
 __global__ void learn_mark_kernel(LearnArgs a) {
@@ -3682,41 +3751,44 @@ __global__ void learn_mark_kernel(LearnArgs a) {
     if (a.Ht.n) *a.Ht.mark = *a.Ht.n;
 }
 
-// The other ranks' new slots, inserted here (dense_ensure: presence bit, key, order).
-__global__ __launch_bounds__(256) void learn_adopt_slots_kernel(LearnTable T, const uint32_t* slots,
-                                                                long long stride, OwnerCounts c, int ranks,
-                                                                int self) {
-    const uint32_t Q = (T.mask + 1u) >> 8;
-    const int qsh = __builtin_ctz(Q);
-    for (int r = 0; r < ranks; r++) {
-        if (r == self) continue;
-        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < c.n[r]; i += (long long)gridDim.x * 256) {
-            const uint32_t h = slots[r * stride + i];
-            dense_ensure(T, h, dense_key(h, qsh, Q, T.dense_by));
-        }
-    }
-}
-
-// The other owners' updated V values.
+// The other owners' updated V values ([ranks][stride], counts on the device).
 __global__ __launch_bounds__(256) void learn_v_scatter_kernel(LearnTable T, const uint32_t* slots,
-                                                              const double* vals, long long stride, OwnerCounts c,
-                                                              int ranks, int self) {
+                                                              const double* vals, long long stride,
+                                                              const long long* counts, int ranks, int self,
+                                                              int* overflow) {
     for (int r = 0; r < ranks; r++) {
         if (r == self) continue;
-        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < c.n[r]; i += (long long)gridDim.x * 256)
+        long long n = counts[r];
+        if (n > stride) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(overflow, 8);
+            n = stride;
+        }
+        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
             tval(T, slots[r * stride + i])[0] = vals[r * stride + i];
     }
 }
 
-// The other owners' H increments: v + q * 2^-32, the owner's tile_h_apply arithmetic.
+// The other owners' H increments: v + q * 2^-32, the owner's tile_h_apply arithmetic; a
+// kHoutNew entry first inserts its row (another rank's step created it).
 __global__ __launch_bounds__(256) void learn_h_deltas_kernel(LearnTable T, const uint32_t* keys, const long long* q,
-                                                             long long stride, OwnerCounts c, int ranks, int self) {
+                                                             long long stride, const long long* counts, int ranks,
+                                                             int self, int* overflow) {
+    const uint32_t Q = (T.mask + 1u) >> 8;
+    const int qsh = __builtin_ctz(Q);
     for (int r = 0; r < ranks; r++) {
         if (r == self) continue;
-        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < c.n[r]; i += (long long)gridDim.x * 256) {
-            const uint32_t key = keys[r * stride + i];
-            double* vp = tval(T, key & 0x0FFFFFFFu) + (key >> 28);
-            *vp = *vp + (double)q[r * stride + i] * (1.0 / kFxOne);
+        long long n = counts[r];
+        if (n > stride) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(overflow, 8);
+            n = stride;
+        }
+        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+            const uint32_t key = keys[r * stride + i], slot = key & 0x0FFFFFFFu;
+            if (key & kHoutNew) dense_ensure(T, slot, dense_key(slot, qsh, Q, T.dense_by));
+            const long long d = q[r * stride + i];
+            if (d == 0) continue;
+            double* vp = tval(T, slot) + ((key >> 28) & 7u);
+            *vp = *vp + (double)d * (1.0 / kFxOne);
         }
     }
 }
@@ -4333,7 +4405,8 @@ hipError_t launch_batch_d(const LearnArgs& a, hipStream_t s) {
         return launch_batch_t<256, 1, 1, D, false>(a, s);
     }
     if (A <= 1024) return launch_batch_t<1024, 1, 1, D, false>(a, s);
-    if (D == 1 && a.bph && learn_batch_uni(a) && learn_batch_phases_on()) return launch_batch_phases(a, s);
+    // (owner mode keeps the fused kernel: its records carry the new-row flags)
+    if (D == 1 && a.bph && a.ow <= 1 && learn_batch_uni(a) && learn_batch_phases_on()) return launch_batch_phases(a, s);
     if (A <= 2048) return launch_batch_t<1024, 1, 2, D, false>(a, s);
     if (A <= 4096) return launch_batch_t<1024, 1, 4, D, false>(a, s);
     if (A <= 8192) {
@@ -4517,41 +4590,28 @@ hipError_t launch_learn_tile_stats(const LearnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_learn_new_slots(const LearnTable& T, uint32_t* out, long long* count, hipStream_t s) {
-    learn_new_slots_kernel<<<dim3(1024), dim3(256), 0, s>>>(T, out, count);
-    return hipGetLastError();
-}
-
 hipError_t launch_learn_mark(const LearnArgs& a, hipStream_t s) {
     learn_mark_kernel<<<dim3(1), dim3(1), 0, s>>>(a);
     return hipGetLastError();
 }
 
-static unsigned owner_grid(const OwnerCounts& c, int ranks, int self) {
-    long long mx = 0;
-    for (int r = 0; r < ranks; r++)
-        if (r != self && c.n[r] > mx) mx = c.n[r];
-    return (unsigned)std::min<long long>(32768, (mx + 255) / 256);
-}
-
-hipError_t launch_learn_adopt_slots(const LearnTable& T, const uint32_t* slots, long long stride,
-                                    const OwnerCounts& c, int ranks, int self, hipStream_t s) {
-    const unsigned g = owner_grid(c, ranks, self);
-    if (g) learn_adopt_slots_kernel<<<dim3(g), dim3(256), 0, s>>>(T, slots, stride, c, ranks, self);
-    return hipGetLastError();
-}
+// Grid of the apply kernels: their counts live on the device, so the grid covers the
+// capacity (grid-stride loops; stride entries per rank at most).
+static unsigned owner_grid(long long stride) { return (unsigned)std::min<long long>(4096, std::max<long long>(1, (stride + 255) / 256)); }
 
 hipError_t launch_learn_v_scatter(const LearnTable& T, const uint32_t* slots, const double* vals, long long stride,
-                                  const OwnerCounts& c, int ranks, int self, hipStream_t s) {
-    const unsigned g = owner_grid(c, ranks, self);
-    if (g) learn_v_scatter_kernel<<<dim3(g), dim3(256), 0, s>>>(T, slots, vals, stride, c, ranks, self);
+                                  const long long* counts, int ranks, int self, int* overflow, hipStream_t s) {
+    if (ranks > 1 && stride > 0)
+        learn_v_scatter_kernel<<<dim3(owner_grid(stride)), dim3(256), 0, s>>>(T, slots, vals, stride, counts, ranks, self,
+                                                                               overflow);
     return hipGetLastError();
 }
 
 hipError_t launch_learn_h_deltas(const LearnTable& T, const uint32_t* keys, const long long* q, long long stride,
-                                 const OwnerCounts& c, int ranks, int self, hipStream_t s) {
-    const unsigned g = owner_grid(c, ranks, self);
-    if (g) learn_h_deltas_kernel<<<dim3(g), dim3(256), 0, s>>>(T, keys, q, stride, c, ranks, self);
+                                 const long long* counts, int ranks, int self, int* overflow, hipStream_t s) {
+    if (ranks > 1 && stride > 0)
+        learn_h_deltas_kernel<<<dim3(owner_grid(stride)), dim3(256), 0, s>>>(T, keys, q, stride, counts, ranks, self,
+                                                                              overflow);
     return hipGetLastError();
 }
 

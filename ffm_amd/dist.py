@@ -62,6 +62,111 @@ def reduce_max(x: float, device=None, group=None) -> float:
 # ---------------------------------------------------------------------------
 # Learning variants: the tables are shared by every env of every rank
 # ---------------------------------------------------------------------------
+_OWN_CHUNK = 64     # tiles per ownership chunk (learn_kernels.h kOwnChunk)
+
+
+def owner_tiles(nt: int, world: int, q: int, chunk: int = _OWN_CHUNK) -> int:
+    """Tiles rank q owns (learn_kernels.h owner_tiles: chunks of 64 dealt round-robin)."""
+    if world <= 1:
+        return nt
+    nch, rem = divmod(nt, chunk)
+    n = ((nch - 1 - q) // world + 1) * chunk if nch > q else 0
+    return n + (rem if rem and nch % world == q else 0)
+
+
+def _tiles_of(shard) -> int:
+    h, w = np.asarray(shard.map).shape
+    return (h * w + 3) // 4
+
+
+class OwnerCaps:
+    """Fixed sizes of the owner-sharded exchange (records per destination block, V values and H
+    increments per rank and step), so a step's collectives are queued without waiting for the
+    GPU.  They start from bounds of the shapes (generous, and exact for V and H: a rank's tiles
+    hold tiles * 1,024 slots), then follow the counts observed: every rank copies the gathered
+    counts (identical everywhere) to pinned memory behind the exchange, and every `adapt_every`
+    exchanges the capacities become `headroom` x the largest count observed so far, from the
+    window `lag` exchanges back (the host waits only for copies that old).  They never fall
+    below what any observed step needed; a count past its capacity is an error reported at the
+    next sync point (never a silent drop).  `fixed` = (records, v, h) disables the adaptation."""
+
+    def __init__(self, world: int, e_max: int, agents: int, n_tiles: int, fixed=None, headroom=(1.25, 1.5, 1.5),
+                 adapt_every: int = 8, lag: int = 4, granule: int = 4096):
+        # records per destination move slowly (agents are conserved, the rows dealt round-robin);
+        # the V / H output counts follow the crowding of the rooms: more headroom
+        self.world, self.granule = int(world), int(granule)
+        self.headroom = tuple(float(h) for h in headroom) if isinstance(headroom, (tuple, list)) else (float(headroom),) * 3
+        self.adapt_every, self.lag = int(adapt_every), int(lag)
+        self.rmax = max(1, int(e_max) * int(agents))        # one rank's records, all to one destination
+        ntk = max(owner_tiles(int(n_tiles), self.world, q) for q in range(self.world))
+        self.vmax = max(1, ntk * 1024)                       # slots one rank owns
+        self.hmax = 5 * self.vmax
+        self.adaptive = fixed is None
+        if fixed is not None:
+            self.caps = tuple(int(x) for x in fixed)
+        else:
+            r0 = min(self.rmax, self._round(2.0 * self.rmax / self.world))
+            v0 = min(self.vmax, self.world * r0)
+            self.caps = (r0, v0, min(self.hmax, 5 * v0))
+        self.max_seen = [0, 0, 0]
+        self.seen = []
+        self.n = 0
+
+    def _round(self, x: float) -> int:
+        g = self.granule
+        return max(g, -(-int(x) // g) * g)
+
+    def apply(self, shards):
+        for s in shards:
+            s.set_owner_capacity(*self.caps)
+
+    def observe(self, rc, vc, hc) -> bool:
+        """Queue pinned copies of one exchange's gathered counts; True when the capacities
+        changed (the caller applies them before its next step)."""
+        if not self.adaptive:
+            return False
+        cp = []
+        for t in (rc, vc, hc):
+            if t is None:
+                cp.append(None)
+                continue
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda)
+            h.copy_(t, non_blocking=True)
+            cp.append(h)
+        ev = None
+        if rc.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        self.seen.append((ev, cp))
+        self.n += 1
+        if self.n % self.adapt_every or len(self.seen) <= self.lag:
+            return False
+        window = self.seen[: len(self.seen) - self.lag]
+        del self.seen[: len(self.seen) - self.lag]
+        for e, cs in window:
+            if e is not None:
+                e.synchronize()              # an exchange `lag` steps back: long done
+            for i, h in enumerate(cs):
+                if h is not None:
+                    self.max_seen[i] = max(self.max_seen[i], int(h.max()))
+        hr, hv, hh = self.headroom
+        new = (min(self.rmax, self._round(hr * self.max_seen[0])),
+               min(self.vmax, self._round(hv * self.max_seen[1])),
+               min(self.hmax, self._round(hh * max(self.max_seen[2], 1))))
+        changed = new != self.caps
+        self.caps = new
+        return changed
+
+    def rescale(self, factor: float):
+        """The workload grows by `factor` (more agents per env): scale the capacities and the
+        observed maxima up front (the observations lag the change)."""
+        if not self.adaptive or factor <= 1.0:
+            return
+        self.max_seen = [int(m * factor) for m in self.max_seen]
+        r, v, h = self.caps
+        self.caps = (min(self.rmax, self._round(r * factor)), min(self.vmax, self._round(v * factor)),
+                     min(self.hmax, self._round(h * factor)))
+
 class TableSync:
     """The batched learning step of one rank's shard, with the V / H table deltas
     exchanged so every rank ends each sync step with the tables a single device
@@ -106,7 +211,7 @@ class TableSync:
 
     def __init__(self, shard, group=None, device=None, capacity: int | None = 1 << 16, sync_period: int = 1,
                  dense: bool | None = None, max_capacity: int = 1 << 20, headroom: float = 1.5,
-                 adapt_every: int = 16, lag: int = 8, tiled_exchange: str = "owner"):
+                 adapt_every: int = 16, lag: int = 8, tiled_exchange: str = "owner", owner_caps=None):
         self.shard = shard
         self.group = group
         self.device = device
@@ -142,6 +247,11 @@ class TableSync:
         self.tiled = self.owner or (bool(v[0].item()) and int(v[2].item()) == -int(v[3].item()))
         if self.owner:
             shard.set_tile_owners(self.world, self.rank)
+            # the exchange sizes are fixed per step (no host sync inside a step): initial
+            # capacities from the shapes, then the counts observed (identical on every rank)
+            self.ocaps = OwnerCaps(self.world, -int(v[3].item()), int(getattr(shard, "A", 0)),
+                                   int(getattr(shard, "NT", 0)) or _tiles_of(shard), fixed=owner_caps)
+            self.ocaps.apply([shard])
         self.backend = dist.get_backend(group)
         self.received_bytes = 0        # per rank, summed over exchanges (owner mode)
         self.bufs = {}
@@ -211,6 +321,10 @@ class TableSync:
         adaptive record capacities up front, since the observed counts lag the change by the
         adaptation window (a touched count jumping past the capacity is an error).  Every rank
         calls it with the same factor at the same step; it never shrinks a capacity."""
+        if self.owner and factor > 1.0 and self.ocaps.adaptive:
+            self.ocaps.rescale(factor)
+            self.ocaps.apply([self.shard])
+            return
         if not self.adaptive or self.dense or self.tiled or factor <= 1.0:
             return
         for w in self.caps:
@@ -238,81 +352,82 @@ class TableSync:
         (self._exchange_dense if self.dense else self._exchange_records)(which)
 
     # -- the owner-sharded tiled step ----------------------------------
-    def _host(self, t):
-        """A small device tensor on the host (the step's size decisions: a host sync)."""
-        return t.cpu().numpy()
+    def _buf(self, key, shape, device, dtype=None):
+        shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
+        dtype = dtype or torch.uint8
+        n = int(np.prod(shape))
+        b = self.bufs.get(key)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = torch.empty(n, dtype=dtype, device=device)
+            self.bufs[key] = b
+        return b[:n].view(shape)
 
-    def _gather_rows(self, x, n_bytes: int, key):
-        """all-gather the first n_bytes of every rank's byte buffer x: [world, n_bytes]
-        (a rank whose buffer is shorter sends a zero-padded copy)."""
-        n = max(int(n_bytes), 1)
-        src = x[:n] if x.numel() >= n else torch.nn.functional.pad(x, (0, n - x.numel()))
-        out = self._buf(key, (self.world, n), x.device)
-        dist.all_gather([out[r] for r in range(self.world)], src.contiguous(), group=self.group)
-        self.received_bytes += (self.world - 1) * n
-        self.bytes_sent += n
+    def _gather(self, x, key):
+        """all-gather of a fixed-size device buffer: [world, *x.shape]."""
+        out = self._buf(key, (self.world,) + tuple(x.shape), x.device, x.dtype)
+        dist.all_gather([out[r] for r in range(self.world)], x.contiguous(), group=self.group)
+        nb = x.numel() * x.element_size()
+        self.received_bytes += (self.world - 1) * nb
+        self.bytes_sent += nb
         return out
 
-    def _buf(self, key, shape, device):
-        shape = tuple(shape) if isinstance(shape, (tuple, list)) else (int(shape),)
-        b = self.bufs.get(key)
-        if b is None or b.numel() < int(np.prod(shape)):
-            b = torch.empty(int(np.prod(shape)), dtype=torch.uint8, device=device)
-            self.bufs[key] = b
-        return b[: int(np.prod(shape))].view(shape)
-
-    def _a2av(self, out, inp, out_splits, in_splits):
-        """all-to-all with uneven byte splits (gloo: staged through host memory)."""
+    def _a2a(self, out, inp):
+        """all-to-all with equal splits (gloo: staged through host memory)."""
         if self.backend == "gloo" and inp.is_cuda:
-            ho = torch.empty(out.numel(), dtype=torch.uint8)
-            dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=self.group)
+            ho = torch.empty(out.numel(), dtype=out.dtype)
+            dist.all_to_all_single(ho, inp.cpu(), group=self.group)
             out.copy_(ho)
         else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            dist.all_to_all_single(out, inp, group=self.group)
+        nb = inp.numel() * inp.element_size() * (self.world - 1) // self.world
+        self.received_bytes += nb
+        self.bytes_sent += nb
 
     def _step_owner(self):
-        s, W, r = self.shard, self.world, self.rank
+        """One owner-sharded step, queued without a host synchronisation: every collective has a
+        fixed size (OwnerCaps), the counts travel on the device beside the data."""
+        s, W = self.shard, self.world
         s.step_owner_local()
         b = s.owner_buffers()
         dev = b["counts"].device
-        hs = b["hdr_stride"]
-        # 1. the record counts (per destination) and new-slot counts of every rank
-        g = self._buf("counts", (W, 8 * (W + 2)), dev)
-        dist.all_gather([g[q] for q in range(W)], b["counts"].view(torch.uint8), group=self.group)
-        allc = self._host(g).view(np.int64).reshape(W, W + 2)
-        send, recv = allc[r, :W], allc[:, r]
-        rrecs = self._buf("rrecs", 16 * max(1, int(recv.sum())), dev)
-        self._a2av(rrecs[: 16 * int(recv.sum())], b["send_recs"][: 16 * int(send.sum())],
-                   [16 * int(x) for x in recv], [16 * int(x) for x in send])
-        rhdr = self._buf("rhdr", (W, 4 * hs), dev)
-        self._a2av(rhdr.view(-1), b["send_hdr"].reshape(-1), [4 * hs] * W, [4 * hs] * W)
-        nmax = max(1, int(allc[:, W:].max()))
-        gv = self._gather_rows(b["new_v"], 4 * nmax, "gnewv")
-        gh = self._gather_rows(b["new_h"], 4 * nmax, "gnewh")
-        s.step_owner_v(rrecs.data_ptr(), rhdr.data_ptr(), recv, gv.data_ptr(), gh.data_ptr(), allc[:, W:], nmax)
-        self.received_bytes += 16 * int(recv.sum() - recv[r]) + 4 * hs * (W - 1)
-        self.bytes_sent += 16 * int(send.sum() - send[r]) + 4 * hs * (W - 1)
+        # 1. the record blocks (equal splits) and header rows, the per-destination counts
+        rrecs = self._buf("rrecs", b["send_recs"].numel(), dev)
+        self._a2a(rrecs, b["send_recs"])
+        rhdr = self._buf("rhdr", b["send_hdr"].numel(), dev)
+        self._a2a(rhdr, b["send_hdr"].reshape(-1))
+        rc = self._gather(b["counts"], "rcnt")            # [W][W]: observed, never read here
+        s.step_owner_v(rrecs.data_ptr(), rhdr.data_ptr())
         # 2. the V values every owner updated
-        b = s.owner_buffers()
-        vc = self._gather_rows(b["out_counts"].view(torch.uint8)[:8], 8, "vcnt")
-        vcount = self._host(vc).view(np.int64).reshape(W)
-        vmax = max(1, int(vcount.max()))
-        gs = self._gather_rows(b["v_slot"], 4 * vmax, "gvs")
-        gval = self._gather_rows(b["v_val"], 8 * vmax, "gvv")
-        s.step_owner_h(gs.data_ptr(), gval.data_ptr(), vcount, vmax)
-        if not s.actor:
-            s.step_owner_end(0, 0, None, 0, 0, 0)
-            self.exchanges += 1
-            return
-        # 3. the H increments and tile summaries every owner produced
-        hc = self._gather_rows(b["out_counts"].view(torch.uint8)[8:16], 8, "hcnt")
-        hcount = self._host(hc).view(np.int64).reshape(W)
-        hmax = max(1, int(hcount.max()))
-        gk = self._gather_rows(b["h_key"], 4 * hmax, "ghk")
-        gq = self._gather_rows(b["h_q"], 8 * hmax, "ghq")
-        gt = self._gather_rows(b["tsum"], 40 * hs, "gts")
-        s.step_owner_end(gk.data_ptr(), gq.data_ptr(), hcount, hmax, gt.data_ptr(), hs)
+        gvs, gvv = self._gather(b["v_slot"], "gvs"), self._gather(b["v_val"], "gvv")
+        gvc = self._gather(b["out_counts"][:1], "gvc")
+        s.step_owner_h(gvs.data_ptr(), gvv.data_ptr(), gvc.data_ptr(), b["v_capacity"])
+        ghc = None
+        if s.actor:
+            # 3. the H increments and tile summaries every owner produced
+            gk, gq = self._gather(b["h_key"], "ghk"), self._gather(b["h_q"], "ghq")
+            ghc = self._gather(b["out_counts"][1:], "ghc")
+            gt = self._gather(b["tsum"], "gts")
+            s.step_owner_end(gk.data_ptr(), gq.data_ptr(), ghc.data_ptr(), b["h_capacity"], gt.data_ptr(),
+                             b["hdr_stride"])
+        else:
+            s.step_owner_end(0, 0, 0, 0, 0, 0)
         self.exchanges += 1
+        if self.ocaps.observe(rc, gvc, ghc):             # a decision window ended: every rank alike
+            self.ocaps.apply([s])
+
+    def sync_presence(self):
+        """The owner exchange keeps H's key set exact every step, V's lazily: merge the V
+        presence bitmaps of all ranks (the slots other ranks inserted join this rank's keys).
+        Collective; TableSync.flush() calls it, so exports and table sizes agree everywhere."""
+        s = self.shard
+        _, present = s.dense_buffers("V")
+        g = self._buf("presV", (self.world, present.numel()), present.device, present.dtype)
+        dist.all_gather([g[r] for r in range(self.world)], present, group=self.group)
+        uni = g[0].clone()
+        for r in range(1, self.world):
+            uni.bitwise_or_(g[r])
+        s.dense_adopt("V", uni.data_ptr())
+        torch.cuda.synchronize(present.device) if present.is_cuda else None
 
     def _step_tiled(self):
         s = self.shard
@@ -335,6 +450,9 @@ class TableSync:
         step.  Call it before reading the tables mid-period (an export of a shared learner
         is read-only: it returns the tables as of the last apply)."""
         s = self.shard
+        if self.owner:
+            self.sync_presence()
+            return
         if self.tiled or not s.flush_begin():    # the periods advance in lockstep: all ranks agree
             return
         self._exchange("V")
@@ -363,55 +481,78 @@ class TableSync:
             s.step_end()
 
 
-def _owner_step_coupled(shards):
-    """One owner-sharded step of shards coupled in-process: TableSync._step_owner's
-    exchanges done by slicing the shards' buffers (one device)."""
+def _owner_step_coupled(shards, caps: OwnerCaps, bufs: dict):
+    """One owner-sharded step of shards coupled in-process: TableSync._step_owner's fixed-size
+    exchanges done as device copies between the shards' buffers (one device), queued with no
+    host synchronisation."""
     W = len(shards)
     for s in shards:
         s.step_owner_local()
     bs = [s.owner_buffers() for s in shards]
-    hs = bs[0]["hdr_stride"]
-    allc = torch.stack([b["counts"] for b in bs]).cpu().numpy()
-    offs = np.concatenate([np.zeros((W, 1), np.int64), np.cumsum(allc[:, :W], axis=1)], axis=1)
-    nmax = max(1, int(allc[:, W:].max()))
+    R, Vc, Hc, hs = bs[0]["rec_capacity"], bs[0]["v_capacity"], bs[0]["h_capacity"], bs[0]["hdr_stride"]
+    dev = bs[0]["counts"].device
 
-    def rows(key, nbytes):
-        out = []
-        for b in bs:
-            x = b[key]
-            out.append(x[:nbytes] if x.numel() >= nbytes else torch.nn.functional.pad(x, (0, nbytes - x.numel())))
-        return torch.stack(out).contiguous()
+    def buf(key, shape, dtype=torch.uint8):
+        n = int(np.prod(shape))
+        b = bufs.get(key)
+        if b is None or b.numel() < n or b.dtype != dtype:
+            b = torch.empty(n, dtype=dtype, device=dev)
+            bufs[key] = b
+        return b[:n].view(shape)
 
-    gv, gh = rows("new_v", 4 * nmax), rows("new_h", 4 * nmax)
-    keep = [gv, gh]
+    rec = 16 * R
+    recv = buf("recv", (W, W, rec))                          # [destination][source] blocks
+    hdr = buf("hdr", (W, W, 4 * hs))
+    for q in range(W):
+        for r in range(W):
+            recv[q, r].copy_(bs[r]["send_recs"][q * rec:(q + 1) * rec])
+            hdr[q, r].copy_(bs[r]["send_hdr"][q])
+    rc = torch.stack([b["counts"] for b in bs])
     for q, s in enumerate(shards):
-        recv = allc[:, q]
-        recs = torch.cat([bs[r]["send_recs"][16 * int(offs[r, q]): 16 * int(offs[r, q + 1])] for r in range(W)]
-                         + [torch.empty(16, dtype=torch.uint8, device=gv.device)])
-        hdr = torch.stack([bs[r]["send_hdr"][q] for r in range(W)]).contiguous()
-        keep += [recs, hdr]
-        s.step_owner_v(recs.data_ptr(), hdr.data_ptr(), recv, gv.data_ptr(), gh.data_ptr(), allc[:, W:], nmax)
-    bs = [s.owner_buffers() for s in shards]
-    vcount = torch.stack([b["out_counts"][0] for b in bs]).cpu().numpy()
-    vmax = max(1, int(vcount.max()))
-    gs, gval = rows("v_slot", 4 * vmax), rows("v_val", 8 * vmax)
+        s.step_owner_v(recv[q].data_ptr(), hdr[q].data_ptr())
+    gvs = buf("gvs", (W, 4 * Vc))
+    gvv = buf("gvv", (W, 8 * Vc))
+    gvc = buf("gvc", (W,), torch.int64)
+    for r, b in enumerate(bs):
+        gvs[r].copy_(b["v_slot"])
+        gvv[r].copy_(b["v_val"])
+        gvc[r:r + 1].copy_(b["out_counts"][:1])
     for s in shards:
-        s.step_owner_h(gs.data_ptr(), gval.data_ptr(), vcount, vmax)
+        s.step_owner_h(gvs.data_ptr(), gvv.data_ptr(), gvc.data_ptr(), Vc)
+    ghc = None
     if not shards[0].actor:
         for s in shards:
-            s.step_owner_end(0, 0, None, 0, 0, 0)
+            s.step_owner_end(0, 0, 0, 0, 0, 0)
     else:
-        hcount = torch.stack([b["out_counts"][1] for b in bs]).cpu().numpy()
-        hmax = max(1, int(hcount.max()))
-        gk, gq, gt = rows("h_key", 4 * hmax), rows("h_q", 8 * hmax), rows("tsum", 40 * hs)
+        gk = buf("ghk", (W, 4 * Hc))
+        gq = buf("ghq", (W, 8 * Hc))
+        ghc = buf("ghc", (W,), torch.int64)
+        gt = buf("gts", (W, 40 * hs))
+        for r, b in enumerate(bs):
+            gk[r].copy_(b["h_key"])
+            gq[r].copy_(b["h_q"])
+            ghc[r:r + 1].copy_(b["out_counts"][1:])
+            gt[r].copy_(b["tsum"])
         for s in shards:
-            s.step_owner_end(gk.data_ptr(), gq.data_ptr(), hcount, hmax, gt.data_ptr(), hs)
-    torch.cuda.synchronize()      # the gathered buffers outlive the kernels that read them
-    del keep
+            s.step_owner_end(gk.data_ptr(), gq.data_ptr(), ghc.data_ptr(), Hc, gt.data_ptr(), hs)
+    if caps.observe(rc, gvc, ghc):
+        caps.apply(shards)
+
+
+def sync_presence_coupled(shards):
+    """TableSync.sync_presence for coupled shards: the union of the V presence bitmaps."""
+    ps = [s.dense_buffers("V")[1] for s in shards]
+    uni = ps[0].clone()
+    for p in ps[1:]:
+        uni.bitwise_or_(p)
+    for s in shards:
+        s.dense_adopt("V", uni.data_ptr())
+    torch.cuda.synchronize()
 
 
 def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16, sync_period: int = 1,
-                 dense: bool = False, async_records: bool = False, tiled: bool = False, owner: bool = False):
+                 dense: bool = False, async_records: bool = False, tiled: bool = False, owner: bool = False,
+                 owner_caps=None):
     """TableSync's protocol for several shards driven by one process (e.g. one
     Learner per device, or shards of one device): the same phases, with the
     collectives replaced by handing every shard the others' records (or, dense,
@@ -425,12 +566,20 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
     for s in shards:
         s.set_sync_period(sync_period)
     if owner:      # TableSync's owner-sharded exchange: shard q sums the tiles it owns
-        for q, s in enumerate(shards):
-            if getattr(s, "_owners", None) != (len(shards), q):
-                s.set_tile_owners(len(shards), q)
-                s._owners = (len(shards), q)
+        W = len(shards)
+        st = getattr(shards[0], "_coupled", None)
+        if st is None or st[0] != W:
+            for q, s in enumerate(shards):
+                s.set_tile_owners(W, q)
+            caps = OwnerCaps(W, max(s.n_envs for s in shards), shards[0].A, _tiles_of(shards[0]), fixed=owner_caps)
+            caps.apply(shards)
+            st = (W, caps, {})
+            for s in shards:
+                s._coupled = st
         for _ in range(int(n_steps)):
-            _owner_step_coupled(shards)
+            _owner_step_coupled(shards, st[1], st[2])
+        if W > 1:
+            sync_presence_coupled(shards)  # V's key set, as TableSync.flush() merges it
         return
     if tiled:      # TableSync's tiled exchange: every shard sums all shards' records (equal E)
         for _ in range(int(n_steps)):

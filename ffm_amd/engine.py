@@ -44,7 +44,7 @@ EXPORTED = [
     "ffm_learner_set_external_sync", "ffm_learner_flush_begin", "ffm_learner_flush_end",
     "ffm_learner_set_tile_owners", "ffm_learner_owner_buffers", "ffm_learner_step_owner_local",
     "ffm_learner_step_owner_v", "ffm_learner_step_owner_h", "ffm_learner_step_owner_end",
-    "ffm_learner_set_epsilon_stride", "ffm_learner_set_episode_caps",
+    "ffm_learner_set_epsilon_stride", "ffm_learner_set_episode_caps", "ffm_learner_set_owner_capacity",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -84,9 +84,8 @@ class OwnerBuffers(C.Structure):
         ("send_recs", C.c_void_p), ("send_rec_capacity", C.c_int64),
         ("send_hdr", C.c_void_p), ("hdr_stride", C.c_int64),
         ("counts", C.c_void_p),
-        ("new_v", C.c_void_p), ("new_h", C.c_void_p), ("new_v_capacity", C.c_int64), ("new_h_capacity", C.c_int64),
         ("v_slot", C.c_void_p), ("v_val", C.c_void_p), ("h_key", C.c_void_p), ("h_q", C.c_void_p),
-        ("out_counts", C.c_void_p), ("out_capacity", C.c_int64),
+        ("out_counts", C.c_void_p), ("v_capacity", C.c_int64), ("h_capacity", C.c_int64),
         ("tsum", C.c_void_p), ("tsum_count", C.c_int64),
     ]
 
@@ -174,7 +173,8 @@ def load_library():
     L.ffm_learner_set_tile_owners.argtypes = [P, i32, i32]
     L.ffm_learner_owner_buffers.argtypes = [P, C.POINTER(OwnerBuffers)]
     L.ffm_learner_step_owner_local.argtypes = [P, P]
-    L.ffm_learner_step_owner_v.argtypes = [P, P, P, P, P, P, P, i64, P]
+    L.ffm_learner_set_owner_capacity.argtypes = [P, i64, i64, i64]
+    L.ffm_learner_step_owner_v.argtypes = [P, P, P, P]
     L.ffm_learner_step_owner_h.argtypes = [P, P, P, P, i64, P]
     L.ffm_learner_step_owner_end.argtypes = [P, P, P, P, i64, P, i64, P]
     L.ffm_learner_set_external_sync.argtypes = [P, i32]
@@ -898,9 +898,15 @@ class Learner:
         """Deal the tiles of cells over `world` ranks; this learner owns rank `rank`'s."""
         _check(self._L.ffm_learner_set_tile_owners(self._h, int(world), int(rank)))
 
+    def set_owner_capacity(self, records: int, v_out: int, h_out: int):
+        """Fixed exchange sizes of the owner-sharded step: records per destination block, V
+        values and H increments this rank's tiles may emit per step (a count past its capacity
+        is an error at the next sync point)."""
+        _check(self._L.ffm_learner_set_owner_capacity(self._h, int(records), int(v_out), int(h_out)))
+
     def owner_buffers(self) -> dict:
         """Torch views (zero copy) of the exchange buffers: byte views where a collective
-        carries them (records, headers, slot lists), typed views for the counts."""
+        carries them (records, headers, outputs), int64 views for the device counts."""
         import torch
         b = OwnerBuffers()
         _check(self._L.ffm_learner_owner_buffers(self._h, C.byref(b)))
@@ -911,17 +917,16 @@ class Learner:
                 return torch.empty(0, dtype=torch.uint8, device=dev)
             return torch.as_tensor(_DevArray(ptr, n, typestr), device=dev)
 
-        w, hs, oc = int(b.world), int(b.hdr_stride), int(b.out_capacity)
+        w, hs, rc = int(b.world), int(b.hdr_stride), int(b.send_rec_capacity)
+        vc, hc = int(b.v_capacity), int(b.h_capacity)
         return {
-            "world": w, "rank": int(b.rank), "hdr_stride": hs, "out_capacity": oc,
-            "tsum_count": int(b.tsum_count),
-            "send_recs": view(b.send_recs, 16 * int(b.send_rec_capacity), "|u1"),
+            "world": w, "rank": int(b.rank), "hdr_stride": hs, "rec_capacity": rc, "v_capacity": vc,
+            "h_capacity": hc, "tsum_count": int(b.tsum_count),
+            "send_recs": view(b.send_recs, 16 * w * rc, "|u1"),
             "send_hdr": view(b.send_hdr, 4 * w * hs, "|u1").view(w, 4 * hs),
-            "counts": view(b.counts, w + 2, "<i8"),
-            "new_v": view(b.new_v, 4 * int(b.new_v_capacity), "|u1"),
-            "new_h": view(b.new_h, 4 * int(b.new_h_capacity), "|u1"),
-            "v_slot": view(b.v_slot, 4 * oc, "|u1"), "v_val": view(b.v_val, 8 * oc, "|u1"),
-            "h_key": view(b.h_key, 4 * oc, "|u1"), "h_q": view(b.h_q, 8 * oc, "|u1"),
+            "counts": view(b.counts, w, "<i8"),
+            "v_slot": view(b.v_slot, 4 * vc, "|u1"), "v_val": view(b.v_val, 8 * vc, "|u1"),
+            "h_key": view(b.h_key, 4 * hc, "|u1"), "h_q": view(b.h_q, 8 * hc, "|u1"),
             "out_counts": view(b.out_counts, 2, "<i8"),
             "tsum": view(b.tsum, 40 * hs, "|u1"),
         }
@@ -929,22 +934,19 @@ class Learner:
     def step_owner_local(self, stream=None):
         _check(self._L.ffm_learner_step_owner_local(self._h, _stream_handle(stream)))
 
-    def step_owner_v(self, recs_ptr: int, hdrs_ptr: int, recv_counts, new_v_ptr: int, new_h_ptr: int, new_counts,
-                     new_stride: int, stream=None):
-        rc = np.ascontiguousarray(recv_counts, np.int64)
-        nc = np.ascontiguousarray(new_counts, np.int64)
-        _check(self._L.ffm_learner_step_owner_v(self._h, recs_ptr, hdrs_ptr, _ptr(rc), new_v_ptr, new_h_ptr, _ptr(nc),
-                                                int(new_stride), _stream_handle(stream)))
+    def step_owner_v(self, recs_ptr: int, hdrs_ptr: int, stream=None):
+        """recs: the received record blocks ([world][rec_capacity] records), hdrs: the received
+        header rows ([world][hdr_stride] u32), both device pointers."""
+        _check(self._L.ffm_learner_step_owner_v(self._h, recs_ptr, hdrs_ptr, _stream_handle(stream)))
 
-    def step_owner_h(self, v_slot_ptr: int, v_val_ptr: int, v_counts, v_stride: int, stream=None):
-        vc = np.ascontiguousarray(v_counts, np.int64)
-        _check(self._L.ffm_learner_step_owner_h(self._h, v_slot_ptr, v_val_ptr, _ptr(vc), int(v_stride),
+    def step_owner_h(self, v_slot_ptr: int, v_val_ptr: int, v_counts_ptr: int, v_stride: int, stream=None):
+        """The gathered V outputs ([world][v_stride]) and their counts (device int64 [world])."""
+        _check(self._L.ffm_learner_step_owner_h(self._h, v_slot_ptr, v_val_ptr, v_counts_ptr, int(v_stride),
                                                 _stream_handle(stream)))
 
-    def step_owner_end(self, h_key_ptr: int, h_q_ptr: int, h_counts, h_stride: int, tsum_ptr: int, tsum_stride: int,
-                       stream=None):
-        hc = np.ascontiguousarray(h_counts if h_counts is not None else np.zeros(1), np.int64)
-        _check(self._L.ffm_learner_step_owner_end(self._h, h_key_ptr, h_q_ptr, _ptr(hc), int(h_stride), tsum_ptr,
+    def step_owner_end(self, h_key_ptr: int, h_q_ptr: int, h_counts_ptr: int, h_stride: int, tsum_ptr: int,
+                       tsum_stride: int, stream=None):
+        _check(self._L.ffm_learner_step_owner_end(self._h, h_key_ptr, h_q_ptr, h_counts_ptr, int(h_stride), tsum_ptr,
                                                   int(tsum_stride), _stream_handle(stream)))
 
     # -- telemetry -----------------------------------------------------------------------

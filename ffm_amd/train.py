@@ -152,7 +152,7 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
                     L.set_epsilon_phase(episodes_per_config)
                 else:
                     L.set_epsilon_schedule(eps_start, eps_end, 1, per_env)
-            v0 = L.table_size("V")
+            v0 = g.table_size(L, "V")
             L.reset()
             done, trajs = [], {}
             while True:
@@ -169,8 +169,8 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
                     break
             ended = np.concatenate(done) if done else np.zeros((0, 4), np.int32)
             ended = ended[ended[:, 1] < per_env]
-            v1 = L.table_size("V")
-            h1 = L.table_size("H") if L.actor else 0
+            v1 = g.table_size(L, "V")
+            h1 = g.table_size(L, "H") if L.actor else 0
             base = episode_num
             for env, k, steps, emptied in ended.tolist():
                 idx = env * per_env + k                  # env-major position among all G * per_env episodes
@@ -310,6 +310,12 @@ class _Group:
         if self.sync is not None:
             self.sync.flush()
 
+    def table_size(self, L, which: str) -> int:
+        """The table's size on every rank: a sharded learner's key sets are merged first
+        (TableSync.flush: the owner exchange keeps V's key set lazily).  Collective."""
+        self.flush()
+        return L.table_size(which)
+
 
 def _pickle_table(L: Learner, which: str) -> dict:
     """get_v_table() / get_h_table() of the reference's model (key objects, insertion order)."""
@@ -390,8 +396,8 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
         while True:
             g.step(L, chunk)
             d = L.drain_episodes()
-            vs = L.table_size("V") + v_initial
-            hs = L.table_size("H") if actor else 0
+            vs = g.table_size(L, "V") + v_initial
+            hs = g.table_size(L, "H") if actor else 0
             if len(d):
                 done.append(np.concatenate([d, np.full((len(d), 1), len(sizes), np.int64)], axis=1))
             sizes.append((vs, hs))
@@ -439,9 +445,10 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
             if out_dir and g.rank == 0:                     # run_actor_only_training.py:293-300
                 with open(os.path.join(out_dir, f"H_actor_N{N}_total{P}ep.pkl"), "wb") as f:
                     pickle.dump(h_n, f)
+        vsz, hsz = g.table_size(L, "V"), (g.table_size(L, "H") if actor else 0)    # collective: every rank
         if verbose and g.rank == 0:
             print(f"N={N:3d}: mean steps={np.mean(pattern['avg_steps']):7.2f} over {len(rows)} episodes, "
-                  f"V {L.table_size('V')}, H {L.table_size('H') if actor else 0}", flush=True)
+                  f"V {vsz}, H {hsz}", flush=True)
     g.flush()
     L.set_episode_caps(None)
     result = {"n_list": list(n_list), "episodes_per_n": P, "model_params": dict(params or {}),

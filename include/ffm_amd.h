@@ -298,55 +298,59 @@ int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const u
                                  int64_t n_envs_all, void* stream);
 /* The owner-sharded tiled step: the tiles of cells are dealt to the ranks
  * (chunks of 64 tiles round-robin) and each rank sums only its own tiles' records, from all
- * ranks, so the per-rank table work does not grow with the rank count.  Per step:
- *   step_owner_local: the step; the records packed tile-major by destination rank
- *     (send_recs, counts[q] records for rank q from offset sum(counts[<q]); send_hdr row q:
- *     q's tiles' record offsets within its block, hdr_stride u32 per row) and this rank's new
- *     V / H slots (new_v / new_h, counts[world] / counts[world + 1]);
- *   the ranks all-to-all the records and header rows and all-gather the new slots;
- *   step_owner_v: adopts the other ranks' new slots, sums this rank's tiles' V (the received
- *     blocks back to back, source rank order; hdrs = the received header rows), writes the
- *     updated V values to v_slot / v_val (out_counts[0]);
- *   the ranks all-gather those;
+ * ranks, so the per-rank table work does not grow with the rank count.  Every exchange has a
+ * fixed size and the counts travel on the device, so the host queues a whole step without
+ * waiting for the GPU (ffm_amd/dist.py TableSync).  Per step:
+ *   step_owner_local: the step; the records packed tile-major by destination rank into
+ *     fixed-capacity blocks (send_recs: rank q's records at [q * send_rec_capacity, + counts[q]);
+ *     send_hdr row q: q's tiles' record offsets within its block, hdr_stride u32 per row);
+ *   the ranks all-to-all the record blocks (equal splits) and header rows;
+ *   step_owner_v: sums this rank's tiles' V (d_recs: the received blocks, rank-major, each
+ *     send_rec_capacity records; d_hdrs: the received header rows) and writes the updated V
+ *     values to v_slot / v_val (out_counts[0] of them, at most v_capacity);
+ *   the ranks all-gather v_capacity entries and the count;
  *   step_owner_h: stores the other ranks' V values; actor modes sum this rank's tiles' H
- *     (h_key = slot | action << 28, h_q = the fixed-point increment; out_counts[1]) and write
- *     the tiles' H summaries (tsum, tsum_count rows of 5 doubles);
- *   the ranks all-gather those;
- *   step_owner_end: applies the other ranks' H increments and summaries, the H statistics,
- *     ends the step.
- * Counts passed as int64_t* are HOST arrays ([world]; new_counts [world][2]); record and
- * table buffers are DEVICE pointers, "_all" buffers rank-major with the given row stride in
- * elements.  Every rank ends each step with the tables one device stepping all envs would
- * hold, bit for bit.  Buffer pointers can change at step_owner_v (out_capacity grows). */
+ *     (h_key = slot | action << 28, bit 31 on the first entry of a row another rank's step
+ *     created; h_q = the fixed-point increment; out_counts[1] entries, at most h_capacity)
+ *     and write the tiles' H summaries (tsum, tsum_count rows of 5 doubles);
+ *   the ranks all-gather h_capacity entries, the count and the summaries;
+ *   step_owner_end: inserts the flagged rows, applies the other ranks' H increments and
+ *     summaries, the H statistics, ends the step.
+ * Counts are DEVICE int64 arrays ([world], rank-major), as are every buffer; "_all"
+ * buffers are rank-major with the given row stride in elements.  A count past its capacity
+ * is reported at the next sync point (FFM_E_INVALID), never silently dropped.  Every rank
+ * ends each step with the H table (keys and values) and the V values one device stepping
+ * all envs would hold, bit for bit; the V slots other ranks inserted join a rank's key set
+ * when the presence bitmaps are merged (ffm_learner_dense_buffers + dense_adopt, which a
+ * shared learner accepts between steps as well): TableSync does so before every export or
+ * size query.  set_owner_capacity sizes the buffers (records per destination, V and H output
+ * entries); pointers change only there. */
 typedef struct ffm_owner_buffers {
     int32_t world, rank;
-    void* send_recs;                 /* 16-B records */
+    void* send_recs;                 /* 16-B records, world blocks of send_rec_capacity */
     int64_t send_rec_capacity;
     uint32_t* send_hdr;
     int64_t hdr_stride;
-    int64_t* counts;                 /* [world + 2] */
-    uint32_t* new_v;
-    uint32_t* new_h;
-    int64_t new_v_capacity, new_h_capacity;
+    int64_t* counts;                 /* [world] records per destination (device) */
     uint32_t* v_slot;
     double* v_val;
     uint32_t* h_key;
     int64_t* h_q;
-    int64_t* out_counts;             /* [2] */
-    int64_t out_capacity;
+    int64_t* out_counts;             /* [2] V values, H increments (device) */
+    int64_t v_capacity, h_capacity;
     double* tsum;
     int64_t tsum_count;
 } ffm_owner_buffers;
 int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank);
+int ffm_learner_set_owner_capacity(ffm_learner* l, int64_t rec_capacity, int64_t v_capacity, int64_t h_capacity);
 int ffm_learner_owner_buffers(ffm_learner* l, ffm_owner_buffers* b);
 int ffm_learner_step_owner_local(ffm_learner* l, void* stream);
-int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, const int64_t* recv_counts,
-                             const uint32_t* d_new_v, const uint32_t* d_new_h, const int64_t* new_counts,
-                             int64_t new_stride, void* stream);
+int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, void* stream);
 int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const double* d_v_val,
-                             const int64_t* v_counts, int64_t v_stride, void* stream);
-int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q, const int64_t* h_counts,
-                               int64_t h_stride, const double* d_tsum_all, int64_t tsum_stride, void* stream);
+                             const int64_t* d_v_counts, int64_t v_stride, void* stream);
+int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q,
+                               const int64_t* d_h_counts, int64_t h_stride, const double* d_tsum_all,
+                               int64_t tsum_stride, void* stream);
 /* Table sync period K >= 1 (default 1 = the reference's per-step updates): the fixed-point
  * increments of K steps accumulate and V / H (and the actor's H statistics) are applied
  * at every K-th step only; a multi-rank run exchanges deltas at those steps only, so
@@ -368,7 +372,8 @@ int ffm_learner_flush_end(ffm_learner* l, void* stream);
 /* Dense (ffm_unified rank-key) tables: the device fixed-point accumulators (acc_count
  * int64) and presence bitmap (present_words u32), for an all-reduce of the increments;
  * dense_adopt then takes the presence union of all ranks (a DEVICE bitmap): slots other
- * ranks inserted get their keys.  Between step_local and step_apply. */
+ * ranks inserted get their keys.  Between step_local and step_apply (or, for a tiled learner,
+ * between steps). */
 int ffm_learner_dense_buffers(ffm_learner* l, int32_t which, int64_t** d_acc, int64_t* acc_count,
                               uint32_t** d_present, int64_t* present_words);
 int ffm_learner_dense_adopt(ffm_learner* l, int32_t which, const uint32_t* d_union, void* stream);

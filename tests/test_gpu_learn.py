@@ -1061,6 +1061,7 @@ def _owner_sync_worker(rank, world, port, sizes, mode, T, out_path):
         sync = TableSync(L, device="cuda")
         assert sync.tiled and sync.owner
         sync.step(T)
+        sync.flush()                 # V's key set: the presence union (collective)
         torch.cuda.synchronize()
         st = L.get_state()
         tabs = {w: L.export_table(w) for w in (("V", "H") if L.actor else ("V",))}
@@ -1231,3 +1232,53 @@ def test_c5_curriculum_sharded_gloo_world2_equals_single(tmp_path):
     sa = (one / "summary.txt").read_text().splitlines()
     sb = (two / "summary.txt").read_text().splitlines()
     assert [l for l in sa if not l.startswith("seconds")] == [l for l in sb if not l.startswith("seconds")]
+
+
+@pytest.mark.timeout(900)
+def test_learner_owner_8_shards_c5_full_size_equal_one_learner():
+    """The owner-sharded exchange at the C5 N = 8 shape itself: 8 coupled shards of 512 envs
+    (256x256 room, 8,192 agents, bench.LEARN_CONFIGS[5], global env ids r * 512 + e) against
+    one learner stepping all 4,096 envs, for 305 steps: through the lockstep truncation and
+    reset at step 300, with tiles holding thousands of records from eight sources (the
+    multi-window general forms).  Positions, counts, DFF bits and the V / H tables (keys and
+    value bits) of every shard equal the single learner's."""
+    import bench
+    from ffm_amd.data import make_room, l1_sff
+    from ffm_amd.dist import step_coupled
+    cfg = bench.LEARN_CONFIGS[5]
+    m = make_room(256, 256)
+    s = l1_sff(m)
+    W, E, T = 8, 512, 305
+    kw = dict(mode=cfg["mode"], params=cfg["params"], rng="philox", seed=42, auto_reset=True,
+              max_steps=cfg["max_steps"], log2_v_capacity=24, log2_h_capacity=24)
+    one = _learner(m, s, cfg["variant"], n_envs=W * E, n_agents=8192, **kw)
+    one.reset()
+    one.step(T)
+    op, oc, od = one.get_state()
+    eps1, _ = one.episodes()
+    assert (eps1 == 1).all()                     # every env truncated at 300 and re-placed
+    tabs1 = {w: one.export_table(w) for w in ("V", "H")}
+    one.close()
+    shards = [_learner(m, s, cfg["variant"], n_envs=E, n_agents=8192, env_base=r * E, **kw) for r in range(W)]
+    for L in shards:
+        L.reset()
+    step_coupled(shards, T, device="cuda", owner=True)
+    for r, L in enumerate(shards):
+        p, c, d = L.get_state()
+        sl = slice(r * E, (r + 1) * E)
+        assert np.array_equal(c, oc[sl]), r
+        assert np.array_equal(d.view(np.uint32), od[sl].view(np.uint32)), r
+        for e in range(E):
+            assert np.array_equal(p[e, :c[e]], op[r * E + e, :c[e]]), (r, e)
+        del p, d
+    for w in ("V", "H"):
+        k0, v0 = tabs1[w]
+        o0 = np.argsort(k0)
+        assert len(k0) > 100000, w
+        for L in shards:
+            k, v = L.export_table(w)
+            o = np.argsort(k)
+            assert np.array_equal(k[o], k0[o0]), w
+            assert np.array_equal(np.asarray(v)[o].view(np.uint64), np.asarray(v0)[o0].view(np.uint64)), w
+    for L in shards:
+        L.close()

@@ -53,7 +53,8 @@ def main():
         out["records_out"] = [int(x["counts"][: a.shards].sum()) for x in b]
         out["v_values_out"] = [int(x["out_counts"][0]) for x in b]
         out["h_increments_out"] = [int(x["out_counts"][1]) for x in b]
-        out["new_v_slots"] = [int(x["counts"][a.shards]) for x in b]
+        out["capacities"] = {"records_per_destination": b[0]["rec_capacity"], "v": b[0]["v_capacity"],
+                             "h": b[0]["h_capacity"]}
     print(json.dumps(out), flush=True)
 
 
