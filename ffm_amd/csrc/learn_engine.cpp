@@ -113,6 +113,13 @@ struct ffm_learner {
     ffm::TileRec* d_pack = nullptr;          // [E][A] records, grouped by destination, tile-major
     long long* d_xcnt = nullptr;             // [kMaxOwners + 2] records per destination
     ffm::TileRec* d_opack = nullptr;         // [ow][rcap] the owner exchange's fixed-capacity send blocks
+    ffm::TileRec* x_opack = nullptr;         // an external send buffer (ffm_learner_set_owner_send_buffer)
+    uint32_t* x_vslot = nullptr;             // external output buffers (ffm_learner_set_owner_output_buffers)
+    double* x_vval = nullptr;
+    unsigned long long* x_vn = nullptr;
+    uint32_t* x_hkey = nullptr;
+    long long* x_hq = nullptr;
+    unsigned long long* x_hn = nullptr;
     long long rcap = 0;                      // records per destination block (set_owner_capacity)
     uint32_t* d_vslot = nullptr;             // owner outputs: vcap V values, hcap H increments
     double* d_vval = nullptr;
@@ -125,6 +132,7 @@ struct ffm_learner {
     uint16_t* d_tstartT = nullptr;           // [NT + 1][E] transposed tile offsets (one-device env-major passes)
     const ffm::TileRec* own_recs = nullptr;  // the received records of the current owner step
     const uint32_t* own_hdr = nullptr;
+    long long own_src = 0;                   // records between the received blocks (0: rcap)
     DevTable V, H;
 };
 
@@ -1106,12 +1114,33 @@ int ffm_learner_set_owner_capacity(ffm_learner* l, int64_t rec_capacity, int64_t
     return FFM_OK;
 }
 
+int ffm_learner_set_owner_send_buffer(ffm_learner* l, void* d_buf) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    HIP_TRY(hipDeviceSynchronize());
+    l->x_opack = reinterpret_cast<ffm::TileRec*>(d_buf);
+    return FFM_OK;
+}
+
+int ffm_learner_set_owner_output_buffers(ffm_learner* l, uint32_t* v_slot, double* v_val, int64_t* v_count,
+                                         uint32_t* h_key, int64_t* h_q, int64_t* h_count) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    const bool vset = v_slot && v_val && v_count, hset = h_key && h_q && h_count;
+    if ((v_slot || v_val || v_count) && !vset) return fail(FFM_E_INVALID, "V outputs: all three buffers or none");
+    if ((h_key || h_q || h_count) && !hset) return fail(FFM_E_INVALID, "H outputs: all three buffers or none");
+    HIP_TRY(hipDeviceSynchronize());
+    l->x_vslot = v_slot; l->x_vval = v_val; l->x_vn = reinterpret_cast<unsigned long long*>(v_count);
+    l->x_hkey = h_key; l->x_hq = reinterpret_cast<long long*>(h_q); l->x_hn = reinterpret_cast<unsigned long long*>(h_count);
+    return FFM_OK;
+}
+
 int ffm_learner_owner_buffers(ffm_learner* l, ffm_owner_buffers* b) {
     if (!l || !b) return fail(FFM_E_INVALID, "null argument");
     if (!l->tiled_ok) return fail(FFM_E_UNSUPPORTED, "not a tiled learner (ffm_unified, block size 1, large map)");
     b->world = l->ow;
     b->rank = l->orank;
-    b->send_recs = l->d_opack;
+    b->send_recs = l->x_opack ? l->x_opack : l->d_opack;
     b->send_rec_capacity = (int64_t)l->rcap;
     b->send_hdr = l->d_hdr;
     b->hdr_stride = l->ths;
@@ -1155,13 +1184,16 @@ int ffm_learner_step_owner_local(ffm_learner* l, void* stream) {
     a.trecs = l->d_trecs;
     HIP_TRY(ffm::launch_learn_batch(a, s));
     l->v_chain = true;
-    HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt, l->d_opack, s));
+    HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt,
+                                        l->x_opack ? l->x_opack : l->d_opack, s));
     l->phase = 7;
     return FFM_OK;
 }
 
-int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, void* stream) {
+int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, int64_t src_stride,
+                             void* stream) {
     if (!l || !d_recs || !d_hdrs) return fail(FFM_E_INVALID, "null argument");
+    if (src_stride != 0 && src_stride < l->rcap) return fail(FFM_E_INVALID, "src_stride below the block capacity");
     if (l->phase != 7) return fail(FFM_E_INVALID, "step_owner_v must follow step_owner_local");
     hipStream_t s = (hipStream_t)stream;
     l->own_recs = reinterpret_cast<const ffm::TileRec*>(d_recs);
@@ -1170,9 +1202,11 @@ int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t*
     a.trecs = const_cast<ffm::TileRec*>(l->own_recs);
     a.thdr = d_hdrs;
     a.tR = l->ow;
-    a.vout_slot = l->d_vslot;
-    a.vout_val = l->d_vval;
-    a.vout_n = l->d_on;
+    a.tsrc = src_stride;
+    l->own_src = src_stride;
+    a.vout_slot = l->x_vslot ? l->x_vslot : l->d_vslot;
+    a.vout_val = l->x_vslot ? l->x_vval : l->d_vval;
+    a.vout_n = l->x_vslot ? l->x_vn : l->d_on;
     a.vout_cap = (long long)l->vcap;
     HIP_TRY(ffm::launch_learn_tiles_owner_v(a, s));
     l->phase = 8;
@@ -1192,9 +1226,10 @@ int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const dou
         a.trecs = const_cast<ffm::TileRec*>(l->own_recs);
         a.thdr = l->own_hdr;
         a.tR = l->ow;
-        a.hout_key = l->d_hkey;
-        a.hout_q = l->d_hq;
-        a.hout_n = l->d_on + 1;
+        a.tsrc = l->own_src;
+        a.hout_key = l->x_hkey ? l->x_hkey : l->d_hkey;
+        a.hout_q = l->x_hkey ? l->x_hq : l->d_hq;
+        a.hout_n = l->x_hkey ? l->x_hn : l->d_on + 1;
         a.hout_cap = (long long)l->hcap;
         HIP_TRY(ffm::launch_learn_tiles_owner_h(a, l->d_tsum, s));
     }

@@ -127,8 +127,9 @@ struct LearnArgs {
     // dealt round-robin over ow ranks; ow <= 1: k itself).
     const uint32_t* thdr;       // nullptr: env-major (tstart)
     int tR, ths, NTk;
-    long long tblk;             // > 0: range r's block starts at record r * tblk (fixed-capacity blocks of the
-                                // sync-free owner exchange; a header offset past tblk is clamped), 0: back to back
+    long long tblk;             // > 0: range r's block starts at record r * tsrc (fixed-capacity blocks of tblk
+                                // records, the sync-free owner exchange; a header offset past tblk is clamped),
+    long long tsrc;             // 0: back to back.  tsrc: records between two ranges' blocks (tblk when 0)
     int ow, orank, ochunk;
     // owner mode outputs: the V values the launch's tiles updated (slot, new value) and the
     // H increments (slot | action << 28, fixed-point sum), appended for the other ranks

@@ -2517,7 +2517,7 @@ __device__ __forceinline__ int tm_spans(const LearnArgs& a, int k, uint32_t* rs,
                 bincl += w;
             }
         }
-        lo += a.tblk > 0 ? (uint32_t)((long long)r * a.tblk) : bincl - blk;
+        lo += a.tblk > 0 ? (uint32_t)((long long)r * (a.tsrc > 0 ? a.tsrc : a.tblk)) : bincl - blk;
         if (r < a.tR) {
             rs[r + 1] = incl;
             rb[r] = lo;
@@ -3751,44 +3751,88 @@ __global__ void learn_mark_kernel(LearnArgs a) {
     if (a.Ht.n) *a.Ht.mark = *a.Ht.n;
 }
 
-// The other owners' updated V values ([ranks][stride], counts on the device).
+// The other owners' updated V values ([ranks][stride], counts on the device).  Each thread
+// takes kApplyJ entries at a time, every load issued before the first store (the entries of
+// all owners address distinct slots, so none of a batch's stores feeds another's load).
+constexpr int kApplyJ = 4;
+
+__device__ __forceinline__ long long owner_count(const long long* counts, int r, long long stride, int* overflow) {
+    long long n = counts[r];
+    if (n > stride) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(overflow, 8);
+        n = stride;
+    }
+    return n;
+}
+
 __global__ __launch_bounds__(256) void learn_v_scatter_kernel(LearnTable T, const uint32_t* slots,
                                                               const double* vals, long long stride,
                                                               const long long* counts, int ranks, int self,
                                                               int* overflow) {
+    const long long nthr = (long long)gridDim.x * 256, t0 = (long long)blockIdx.x * 256 + threadIdx.x;
     for (int r = 0; r < ranks; r++) {
         if (r == self) continue;
-        long long n = counts[r];
-        if (n > stride) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(overflow, 8);
-            n = stride;
+        const long long n = owner_count(counts, r, stride, overflow);
+        const uint32_t* sl = slots + r * stride;
+        const double* vl = vals + r * stride;
+        for (long long i0 = t0; i0 < n; i0 += nthr * kApplyJ) {
+            uint32_t k[kApplyJ];
+            double v[kApplyJ];
+#pragma unroll
+            for (int j = 0; j < kApplyJ; j++) {
+                const long long i = i0 + j * nthr;
+                if (i < n) {
+                    k[j] = sl[i];
+                    v[j] = vl[i];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kApplyJ; j++)
+                if (i0 + j * nthr < n) tval(T, k[j])[0] = v[j];
         }
-        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-            tval(T, slots[r * stride + i])[0] = vals[r * stride + i];
     }
 }
 
 // The other owners' H increments: v + q * 2^-32, the owner's tile_h_apply arithmetic; a
-// kHoutNew entry first inserts its row (another rank's step created it).
+// kHoutNew entry first inserts its row (another rank's step created it).  Batches of
+// kApplyJ entries: keys and increments, then the rows' values, then the stores.
 __global__ __launch_bounds__(256) void learn_h_deltas_kernel(LearnTable T, const uint32_t* keys, const long long* q,
                                                              long long stride, const long long* counts, int ranks,
                                                              int self, int* overflow) {
     const uint32_t Q = (T.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q);
+    const long long nthr = (long long)gridDim.x * 256, t0 = (long long)blockIdx.x * 256 + threadIdx.x;
     for (int r = 0; r < ranks; r++) {
         if (r == self) continue;
-        long long n = counts[r];
-        if (n > stride) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(overflow, 8);
-            n = stride;
-        }
-        for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-            const uint32_t key = keys[r * stride + i], slot = key & 0x0FFFFFFFu;
-            if (key & kHoutNew) dense_ensure(T, slot, dense_key(slot, qsh, Q, T.dense_by));
-            const long long d = q[r * stride + i];
-            if (d == 0) continue;
-            double* vp = tval(T, slot) + ((key >> 28) & 7u);
-            *vp = *vp + (double)d * (1.0 / kFxOne);
+        const long long n = owner_count(counts, r, stride, overflow);
+        const uint32_t* kl = keys + r * stride;
+        const long long* ql = q + r * stride;
+        for (long long i0 = t0; i0 < n; i0 += nthr * kApplyJ) {
+            uint32_t k[kApplyJ];
+            long long d[kApplyJ];
+            double v[kApplyJ];
+            bool live[kApplyJ];
+#pragma unroll
+            for (int j = 0; j < kApplyJ; j++) {
+                const long long i = i0 + j * nthr;
+                live[j] = i < n;
+                k[j] = 0u;
+                d[j] = 0;
+                if (live[j]) {
+                    k[j] = kl[i];
+                    d[j] = ql[i];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kApplyJ; j++) {
+                const uint32_t slot = k[j] & 0x0FFFFFFFu;
+                if (live[j] && (k[j] & kHoutNew)) dense_ensure(T, slot, dense_key(slot, qsh, Q, T.dense_by));
+                live[j] = live[j] && d[j] != 0;
+                if (live[j]) v[j] = tval(T, slot)[(k[j] >> 28) & 7u];
+            }
+#pragma unroll
+            for (int j = 0; j < kApplyJ; j++)
+                if (live[j]) tval(T, k[j] & 0x0FFFFFFFu)[(k[j] >> 28) & 7u] = v[j] + (double)d[j] * (1.0 / kFxOne);
         }
     }
 }
@@ -4597,7 +4641,9 @@ hipError_t launch_learn_mark(const LearnArgs& a, hipStream_t s) {
 
 // Grid of the apply kernels: their counts live on the device, so the grid covers the
 // capacity (grid-stride loops; stride entries per rank at most).
-static unsigned owner_grid(long long stride) { return (unsigned)std::min<long long>(4096, std::max<long long>(1, (stride + 255) / 256)); }
+static unsigned owner_grid(long long stride) {
+    return (unsigned)std::min<long long>(2048, std::max<long long>(1, (stride + 256 * kApplyJ - 1) / (256 * kApplyJ)));
+}
 
 hipError_t launch_learn_v_scatter(const LearnTable& T, const uint32_t* slots, const double* vals, long long stride,
                                   const long long* counts, int ranks, int self, int* overflow, hipStream_t s) {

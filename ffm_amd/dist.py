@@ -492,31 +492,17 @@ def _owner_step_coupled(shards, caps: OwnerCaps, bufs: dict):
     R, Vc, Hc, hs = bs[0]["rec_capacity"], bs[0]["v_capacity"], bs[0]["h_capacity"], bs[0]["hdr_stride"]
     dev = bs[0]["counts"].device
 
-    def buf(key, shape, dtype=torch.uint8):
-        n = int(np.prod(shape))
-        b = bufs.get(key)
-        if b is None or b.numel() < n or b.dtype != dtype:
-            b = torch.empty(n, dtype=dtype, device=dev)
-            bufs[key] = b
-        return b[:n].view(shape)
-
-    rec = 16 * R
-    recv = buf("recv", (W, W, rec))                          # [destination][source] blocks
-    hdr = buf("hdr", (W, W, 4 * hs))
-    for q in range(W):
-        for r in range(W):
-            recv[q, r].copy_(bs[r]["send_recs"][q * rec:(q + 1) * rec])
-            hdr[q, r].copy_(bs[r]["send_hdr"][q])
+    # the shards pack into one shared buffer ([source][destination] blocks, set up by
+    # _owner_send_buffers), so destination q reads source r's block in place at stride W * R
+    big = bufs["send"]
+    # header rows [source][destination] -> [destination][source]: two launches, not W * W copies
+    hdr = torch.stack([b["send_hdr"] for b in bs]).transpose(0, 1).contiguous()
+    bufs["hdr"] = hdr                    # alive until the V / H passes that read it have run
     rc = torch.stack([b["counts"] for b in bs])
     for q, s in enumerate(shards):
-        s.step_owner_v(recv[q].data_ptr(), hdr[q].data_ptr())
-    gvs = buf("gvs", (W, 4 * Vc))
-    gvv = buf("gvv", (W, 8 * Vc))
-    gvc = buf("gvc", (W,), torch.int64)
-    for r, b in enumerate(bs):
-        gvs[r].copy_(b["v_slot"])
-        gvv[r].copy_(b["v_val"])
-        gvc[r:r + 1].copy_(b["out_counts"][:1])
+        s.step_owner_v(big.data_ptr() + q * 16 * R, hdr[q].data_ptr(), W * R)
+    # the V / H outputs were written in place into the gathered buffers (_owner_send_buffers)
+    gvs, gvv, gvc = bufs["gvs"], bufs["gvv"], bufs["gvc"]
     for s in shards:
         s.step_owner_h(gvs.data_ptr(), gvv.data_ptr(), gvc.data_ptr(), Vc)
     ghc = None
@@ -524,19 +510,39 @@ def _owner_step_coupled(shards, caps: OwnerCaps, bufs: dict):
         for s in shards:
             s.step_owner_end(0, 0, 0, 0, 0, 0)
     else:
-        gk = buf("ghk", (W, 4 * Hc))
-        gq = buf("ghq", (W, 8 * Hc))
-        ghc = buf("ghc", (W,), torch.int64)
-        gt = buf("gts", (W, 40 * hs))
-        for r, b in enumerate(bs):
-            gk[r].copy_(b["h_key"])
-            gq[r].copy_(b["h_q"])
-            ghc[r:r + 1].copy_(b["out_counts"][1:])
-            gt[r].copy_(b["tsum"])
+        gk, gq, ghc = bufs["ghk"], bufs["ghq"], bufs["ghc"]
+        gt = torch.stack([b["tsum"] for b in bs])
+        bufs["gts"] = gt
         for s in shards:
             s.step_owner_end(gk.data_ptr(), gq.data_ptr(), ghc.data_ptr(), Hc, gt.data_ptr(), hs)
     if caps.observe(rc, gvc, ghc):
         caps.apply(shards)
+        _owner_send_buffers(shards, caps, bufs)
+
+
+def _owner_send_buffers(shards, caps: OwnerCaps, bufs: dict):
+    """One send buffer for all coupled shards: shard r packs its W blocks at [r][0..W)."""
+    W, (R, Vc, Hc) = len(shards), caps.caps
+    for s in shards:
+        s.set_owner_send_buffer(None)
+        s.set_owner_output_buffers(None, None)
+    for k in ("send", "gvs", "gvv", "gvc", "ghk", "ghq", "ghc"):
+        bufs.pop(k, None)
+    torch.cuda.synchronize()
+    dev = shards[0].owner_buffers()["counts"].device
+    big = torch.empty(W * W * R * 16, dtype=torch.uint8, device=dev)
+    bufs["send"] = big
+    g = {"gvs": torch.empty((W, 4 * Vc), dtype=torch.uint8, device=dev),
+         "gvv": torch.empty((W, 8 * Vc), dtype=torch.uint8, device=dev),
+         "gvc": torch.zeros(W, dtype=torch.int64, device=dev),
+         "ghk": torch.empty((W, 4 * Hc), dtype=torch.uint8, device=dev),
+         "ghq": torch.empty((W, 8 * Hc), dtype=torch.uint8, device=dev),
+         "ghc": torch.zeros(W, dtype=torch.int64, device=dev)}
+    bufs.update(g)
+    for r, s in enumerate(shards):
+        s.set_owner_send_buffer(big.data_ptr() + r * W * R * 16)
+        s.set_owner_output_buffers((g["gvs"][r].data_ptr(), g["gvv"][r].data_ptr(), g["gvc"][r:].data_ptr()),
+                                   (g["ghk"][r].data_ptr(), g["ghq"][r].data_ptr(), g["ghc"][r:].data_ptr()))
 
 
 def sync_presence_coupled(shards):
@@ -574,6 +580,7 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
             caps = OwnerCaps(W, max(s.n_envs for s in shards), shards[0].A, _tiles_of(shards[0]), fixed=owner_caps)
             caps.apply(shards)
             st = (W, caps, {})
+            _owner_send_buffers(shards, caps, st[2])
             for s in shards:
                 s._coupled = st
         for _ in range(int(n_steps)):

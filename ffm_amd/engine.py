@@ -45,6 +45,7 @@ EXPORTED = [
     "ffm_learner_set_tile_owners", "ffm_learner_owner_buffers", "ffm_learner_step_owner_local",
     "ffm_learner_step_owner_v", "ffm_learner_step_owner_h", "ffm_learner_step_owner_end",
     "ffm_learner_set_epsilon_stride", "ffm_learner_set_episode_caps", "ffm_learner_set_owner_capacity",
+    "ffm_learner_set_owner_send_buffer", "ffm_learner_set_owner_output_buffers",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -174,7 +175,9 @@ def load_library():
     L.ffm_learner_owner_buffers.argtypes = [P, C.POINTER(OwnerBuffers)]
     L.ffm_learner_step_owner_local.argtypes = [P, P]
     L.ffm_learner_set_owner_capacity.argtypes = [P, i64, i64, i64]
-    L.ffm_learner_step_owner_v.argtypes = [P, P, P, P]
+    L.ffm_learner_step_owner_v.argtypes = [P, P, P, i64, P]
+    L.ffm_learner_set_owner_send_buffer.argtypes = [P, P]
+    L.ffm_learner_set_owner_output_buffers.argtypes = [P, P, P, P, P, P, P]
     L.ffm_learner_step_owner_h.argtypes = [P, P, P, P, i64, P]
     L.ffm_learner_step_owner_end.argtypes = [P, P, P, P, i64, P, i64, P]
     L.ffm_learner_set_external_sync.argtypes = [P, i32]
@@ -934,10 +937,22 @@ class Learner:
     def step_owner_local(self, stream=None):
         _check(self._L.ffm_learner_step_owner_local(self._h, _stream_handle(stream)))
 
-    def step_owner_v(self, recs_ptr: int, hdrs_ptr: int, stream=None):
-        """recs: the received record blocks ([world][rec_capacity] records), hdrs: the received
-        header rows ([world][hdr_stride] u32), both device pointers."""
-        _check(self._L.ffm_learner_step_owner_v(self._h, recs_ptr, hdrs_ptr, _stream_handle(stream)))
+    def set_owner_send_buffer(self, ptr: int | None):
+        """Pack the owner exchange's send blocks into this device buffer (world * rec_capacity
+        records) instead of the learner's own; None restores it."""
+        _check(self._L.ffm_learner_set_owner_send_buffer(self._h, ptr))
+
+    def set_owner_output_buffers(self, v=None, h=None):
+        """v / h: (slot or key, value or increment, count) device pointers the owner passes
+        write instead of the learner's own buffers; None restores them."""
+        v = v or (None, None, None)
+        h = h or (None, None, None)
+        _check(self._L.ffm_learner_set_owner_output_buffers(self._h, *v, *h))
+
+    def step_owner_v(self, recs_ptr: int, hdrs_ptr: int, src_stride: int = 0, stream=None):
+        """recs: the received record blocks (source r's block at r * src_stride records; 0 =
+        rec_capacity), hdrs: the received header rows ([world][hdr_stride] u32), device pointers."""
+        _check(self._L.ffm_learner_step_owner_v(self._h, recs_ptr, hdrs_ptr, int(src_stride), _stream_handle(stream)))
 
     def step_owner_h(self, v_slot_ptr: int, v_val_ptr: int, v_counts_ptr: int, v_stride: int, stream=None):
         """The gathered V outputs ([world][v_stride]) and their counts (device int64 [world])."""

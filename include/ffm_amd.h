@@ -345,7 +345,18 @@ int ffm_learner_set_tile_owners(ffm_learner* l, int32_t world, int32_t rank);
 int ffm_learner_set_owner_capacity(ffm_learner* l, int64_t rec_capacity, int64_t v_capacity, int64_t h_capacity);
 int ffm_learner_owner_buffers(ffm_learner* l, ffm_owner_buffers* b);
 int ffm_learner_step_owner_local(ffm_learner* l, void* stream);
-int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, void* stream);
+/* src_stride: records between two sources' blocks in d_recs (0 = send_rec_capacity: the
+ * all-to-all's receive buffer).  set_owner_send_buffer: pack into a caller's device buffer of
+ * world * send_rec_capacity records instead (NULL: the learner's own), e.g. one allocation
+ * shared by coupled shards, which then read each other's blocks in place. */
+int ffm_learner_set_owner_send_buffer(ffm_learner* l, void* d_buf);
+/* The V / H outputs written into caller buffers (v_capacity / h_capacity entries, the counts
+ * as int64) instead of the learner's own, e.g. rows of the gathered buffers coupled shards
+ * read in place; NULLs restore the learner's own.  owner_buffers keeps describing its own. */
+int ffm_learner_set_owner_output_buffers(ffm_learner* l, uint32_t* v_slot, double* v_val, int64_t* v_count,
+                                         uint32_t* h_key, int64_t* h_q, int64_t* h_count);
+int ffm_learner_step_owner_v(ffm_learner* l, const void* d_recs, const uint32_t* d_hdrs, int64_t src_stride,
+                             void* stream);
 int ffm_learner_step_owner_h(ffm_learner* l, const uint32_t* d_v_slot, const double* d_v_val,
                              const int64_t* d_v_counts, int64_t v_stride, void* stream);
 int ffm_learner_step_owner_end(ffm_learner* l, const uint32_t* d_h_key, const int64_t* d_h_q,

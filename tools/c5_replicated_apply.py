@@ -51,8 +51,9 @@ def main():
     if a.owner:     # the last step's exchange volumes per shard (records in, V values out, H increments out)
         b = [L.owner_buffers() for L in shards]
         out["records_out"] = [int(x["counts"][: a.shards].sum()) for x in b]
-        out["v_values_out"] = [int(x["out_counts"][0]) for x in b]
-        out["h_increments_out"] = [int(x["out_counts"][1]) for x in b]
+        g = shards[0]._coupled[2]        # coupled shards write their outputs into the gathered buffers
+        out["v_values_out"] = g["gvc"].tolist()
+        out["h_increments_out"] = g["ghc"].tolist()
         out["capacities"] = {"records_per_destination": b[0]["rec_capacity"], "v": b[0]["v_capacity"],
                              "h": b[0]["h_capacity"]}
     print(json.dumps(out), flush=True)
