@@ -39,6 +39,7 @@
 
 #include "core_common.h"
 #include "kernels.h"
+#include "lane_common.h"
 #include "wave_reset.h"
 
 #ifndef FFM_STAMPS
@@ -739,11 +740,27 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             float* t = tile + iq.k * PHW + (iq.r + 1) * PW + 4 * iq.c + 1;
             t[0] = v.x; t[1] = v.y; t[2] = v.z; t[3] = v.w;
         }
-        Idx3 ix(tid, BS, H + 2, PW);
-        for (int i = tid; i < nP; i += BS, ix.advance()) {
-            const bool halo = ix.r == 0 || ix.r == H + 1 || ix.c == 0 || ix.c == W + 1;
-            if (halo) tile[i] = 0.0f;
-            grid[i] = a.pmap[ix.r * PW + ix.c];
+        // the halo ring of every env's tile: 2 PW + 2 H cells (rows 0 and H + 1, then the
+        // side columns), no per-cell row / column arithmetic over the whole grid
+        const int ring = 2 * PW + 2 * H;
+        for (int k = 0; k < K; k++)
+            for (int j = tid; j < ring; j += BS) {
+                const int jc = j - 2 * PW;
+                const int c = j < PW ? j : j < 2 * PW ? (H + 1) * PW + (j - PW) : (1 + (jc >> 1)) * PW + ((jc & 1) ? W + 1 : 0);
+                tile[k * PHW + c] = 0.0f;
+            }
+        // every env's grid starts as the map: four u8 cells per load, two u16 dwords per store
+        // (W % 4 == 0: PW and PHW are even, so each env's grid is dword aligned)
+        const uint32_t* m32 = reinterpret_cast<const uint32_t*>(a.pmap);
+        const int P4 = PHW >> 2;
+        for (int k = 0; k < K; k++) {
+            uint32_t* g32 = reinterpret_cast<uint32_t*>(grid + k * PHW);
+            for (int i = tid; i < P4; i += BS) {
+                const uint32_t m = m32[i];
+                g32[2 * i] = (m & 0xFFu) | ((m << 8) & 0xFF0000u);
+                g32[2 * i + 1] = ((m >> 16) & 0xFFu) | ((m >> 8) & 0xFF0000u);
+            }
+            for (int i = 4 * P4 + tid; i < PHW; i += BS) grid[k * PHW + i] = a.pmap[i];
         }
     } else {
         Idx3 ix(tid, BS, H + 2, PW);
@@ -798,8 +815,23 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             const uint4 pb = philox(make_uint4(a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i, kPurDecide << 28),
                                     a.key0, a.key1);
             reinterpret_cast<uint2*>(gbase + cv.u)[it] = make_uint2(pb.z, pb.w);
-            r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0, a.kS32, a.kD32,
-                                                     a.kS64, DrawFixed{u53(pb.x, pb.y)}), pp, PW);
+            if (F64) {
+                r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
+                                                         a.kS32, a.kD32, a.kS64, DrawFixed{u53(pb.x, pb.y)}), pp, PW);
+            } else {
+                // the trimmed fast pass of the small-env kernels (float32 u, masked scores, no
+                // double conversion; the tile has the grid's layout: DWS = 0), the exact NumPy
+                // pass only when u lies within the margin of a cdf boundary (identical results)
+                bool to_exit = false;
+                uint32_t slot = lane_decide<NB, false, false, 0>(pp, PW, grid + k * PHW, psff32, tile + k * PHW, 0,
+                                                                 a.kS32, a.kD32, pb.x, to_exit);
+                if (slot == kPending)
+                    slot = NB == 4 ? lane_decide_exact<NB, false, 0>(pp, PW, grid + k * PHW, psff32, tile + k * PHW, 0,
+                                                                     a.kS32, a.kD32, u53(pb.x, pb.y))
+                                   : lane_decide_exact_arr<NB, false, 0>(pp, PW, grid + k * PHW, psff32, tile + k * PHW,
+                                                                         0, a.kS32, a.kD32, u53(pb.x, pb.y));
+                r = req_cell<NB, CT>(slot, pp, PW);
+            }
         }
         sreq[it] = r;
     }

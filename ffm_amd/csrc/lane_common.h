@@ -39,7 +39,9 @@ __device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, int off, float
 // for the agent at padded cell pp; shared by the fast and the exact pass.
 // PRE: psff holds f32(-k_S) * SFF already (the product the score takes, staged once per
 // workgroup), so kS is not applied again; results are identical.
-template <int NB, bool PRE = false>
+// DWS: the DFF tile's row stride minus the grid's (the small-env tiles have no halo columns:
+// -2; a tile laid out like the grid: 0).
+template <int NB, bool PRE = false, int DWS = -2>
 __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, const float* psff, const float* dk,
                                            int dd0, float kS, float kD, bool (&v)[NB + 1], float (&xs)[NB + 1],
                                            int& exit_slot) {
@@ -49,7 +51,7 @@ __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, c
 #pragma unroll
     for (int s = 0; s < NB; s++) {
         cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
-        dcell[s] = cell[s] + dd0 - nb_dx<NB>(s) * 2;   // the tile row is 2 shorter than the grid row
+        dcell[s] = cell[s] + dd0 + nb_dx<NB>(s) * DWS;   // the tile row is -DWS shorter than the grid row
         g[s] = gk[cell[s]];
     }
     cell[NB] = pp;
@@ -93,7 +95,7 @@ __device__ __forceinline__ int lane_scores(int pp, int PW, const uint16_t* gk, c
 //     acceptance test (cum > t + d) sends to the exact pass -- the same decisions as
 //     masking every step separately, in 7 instead of 11 VALU per candidate.
 //   * KD1 (k_D == 1, the drivers' setting): k_D * DFF is DFF itself (an exact product).
-template <int NB, bool PRE = false, bool KD1 = false>
+template <int NB, bool PRE = false, bool KD1 = false, int DWS = -2>
 __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* gk, const float* psff,
                                                 const float* dk, int dd0, float kS, float kD, uint32_t wx,
                                                 bool& to_exit) {
@@ -103,7 +105,7 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
 #pragma unroll
     for (int s = 0; s < NB; s++) {
         cell[s] = pp + nb_dx<NB>(s) * PW + nb_dy<NB>(s);
-        dcell[s] = cell[s] + dd0 - nb_dx<NB>(s) * 2;   // the tile row is 2 shorter than the grid row
+        dcell[s] = cell[s] + dd0 + nb_dx<NB>(s) * DWS;   // the tile row is -DWS shorter than the grid row
         g[s] = gk[cell[s]];
     }
     cell[NB] = pp;
@@ -163,7 +165,7 @@ __device__ __forceinline__ uint32_t lane_decide(int pp, int PW, const uint16_t* 
 // (max, sum, cdf total, search) with one candidate live at a time: this path sets
 // the kernel's register peak otherwise.  Neumann only (the 8-lane pairwise sum of
 // add.reduce needs every term at once: lane_decide_exact_arr).
-template <int NB, bool PRE = false>
+template <int NB, bool PRE = false, int DWS = -2>
 __device__ __forceinline__ float lane_score1(int k, int pp, int PW, const uint16_t* gk, const float* psff,
                                              const float* dk, int dd0, float kS, float kD, bool& valid) {
     int dx = 0, dy = 0;
@@ -176,32 +178,32 @@ __device__ __forceinline__ float lane_score1(int k, int pp, int PW, const uint16
     const uint32_t g = gk[cell];
     valid = k == NB || g == 0u || g == 3u;
     const float sa = PRE ? psff[cell] : kS * psff[cell];
-    const float sb = kD * dk[cell + dd0 - dx * 2];
+    const float sb = kD * dk[cell + dd0 + dx * DWS];
     return sa + sb;                                                      // :77
 }
 
-template <int NB, bool PRE = false>
+template <int NB, bool PRE = false, int DWS = -2>
 __device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint16_t* gk, const float* psff,
                                                       const float* dk, int dd0, float kS, float kD, double u) {
     float mx = -__builtin_inff();
 #pragma unroll 1
     for (int k = 0; k <= NB; k++) {
         bool v;
-        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE, DWS>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         mx = (v && sc > mx) ? sc : mx;                                   // :78
     }
     float sum = -0.0f;                                                   // add.reduce, < 8 terms: left fold
 #pragma unroll 1
     for (int k = 0; k <= NB; k++) {
         bool v;
-        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE, DWS>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         if (v) sum += np_expf(sc - mx);                                  // :80-81
     }
     double last = 0.0;
 #pragma unroll 1
     for (int k = 0; k <= NB; k++) {
         bool v;
-        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE, DWS>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         if (v) last += (double)(np_expf(sc - mx) / sum);                 // :83, cumsum in choice
     }
     const double inv = 1.0 / last;
@@ -210,7 +212,7 @@ __device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint
 #pragma unroll 1
     for (int k = 0; k < NB; k++) {
         bool v;
-        const float sc = lane_score1<NB, PRE>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
+        const float sc = lane_score1<NB, PRE, DWS>(k, pp, PW, gk, psff, dk, dd0, kS, kD, v);
         if (v) {
             run += (double)(np_expf(sc - mx) / sum);
             if (cdf_gt(run, last, inv, u)) {
@@ -223,13 +225,13 @@ __device__ __forceinline__ uint32_t lane_decide_exact(int pp, int PW, const uint
 }
 
 // The same with every term held (Moore: add.reduce pairs 8 terms).
-template <int NB, bool PRE = false>
+template <int NB, bool PRE = false, int DWS = -2>
 __device__ __forceinline__ uint32_t lane_decide_exact_arr(int pp, int PW, const uint16_t* gk, const float* psff,
                                                           const float* dk, int dd0, float kS, float kD, double u) {
     bool v[NB + 1];
     float xs[NB + 1];
     int exit_slot;
-    const int nvalid = lane_scores<NB, PRE>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
+    const int nvalid = lane_scores<NB, PRE, DWS>(pp, PW, gk, psff, dk, dd0, kS, kD, v, xs, exit_slot);
     float e[NB + 1];
 #pragma unroll
     for (int k = 0; k <= NB; k++) e[k] = v[k] ? np_expf(xs[k]) : 0.0f;   // :80
