@@ -344,6 +344,16 @@ __device__ __forceinline__ uint32_t reset_threshold(int N, int F) {
     return t >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
+// n / d for n < 2^17 and d < 2^16 by one multiply-high: m = ceil(2^32 / d) (magic_div); the
+// rounding error n * (m - 2^32 / d) / 2^32 < 2^-15 stays below the 1 / d gap to the next integer.
+__device__ __forceinline__ int mdiv(int n, uint32_t m) { return (int)__umulhi((uint32_t)n, m); }
+
+// unpad with a runtime row width: the quotient by magic_div(PW)
+__device__ __forceinline__ int unpad_m(int pp, int PW, uint32_t mPW) {
+    const int q = mdiv(pp, mPW);
+    return (q - 1) * (PW - 2) + (pp - q * PW - 1);
+}
+
 __device__ __forceinline__ int unpad(int pp, int PW) {
     const int x = pp / PW - 1, y = pp - (pp / PW) * PW - 1;
     return x * (PW - 2) + y;

@@ -728,6 +728,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
     const int nA = K * A;
     const int nP = K * PHW;
     const AgentIdx ag0(tid, BS, A);   // this thread's first (env, agent) slot
+    const uint32_t mW = a.mW, mPW = a.mPW;   // cell -> row without a divide (host-computed magic numbers)
 
     // ---- load -------------------------------------------------------------------
     if ((W & 3) == 0) {
@@ -782,7 +783,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         int pp = 0;
         if (i < scnt[k]) {
             const int c = a.pos[(e0 + k) * A + i];
-            const int x = c / W, y = c - (c / W) * W;
+            const int x = mdiv(c, mW), y = c - x * W;
             pp = (x + 1) * PW + y + 1;
         }
         spos[it] = (CT)pp;
@@ -947,7 +948,7 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
             __syncthreads();
             if (it < nA) {
                 const int seg = sseg[k];
-                if (keep) a.pos[(e0 + k) * A + (excl - seg)] = (uint16_t)unpad(snxt[it], PW);
+                if (keep) a.pos[(e0 + k) * A + (excl - seg)] = (uint16_t)unpad_m(snxt[it], PW, mPW);
                 if (i == A - 1) snew[k] = excl + (keep ? 1 : 0) - seg;
             }
             carry += tot;

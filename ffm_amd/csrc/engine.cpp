@@ -187,6 +187,8 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     e->wave = !e->lane && !e->group && (d.envs_per_block == 0 || d.envs_per_block == -1) && A <= 64 && !e->f64 && W % 4 == 0 && EW * HW <= 512 &&
               ffm::core_wave_smem_bytes(H, W, A, e->F, e->mt, reset_lds, 4) <= 64 * 1024;
     e->block = A > 256 ? 512 : 256;
+    if (const char* bs = getenv("FFM_BLOCK_BS"))     // A/B switch: the block kernel's workgroup size
+        if (atoi(bs) == 256 || atoi(bs) == 512) e->block = atoi(bs);
     int K = d.envs_per_block > 0 ? d.envs_per_block : std::max(1, 256 / A);
     if (e->mt) K = 1;
     while (K > 1 && ffm::core_block_smem_bytes(H, W, A, K, e->F, e->f64, e->mt, reset_lds) > 64 * 1024) K--;
@@ -333,6 +335,8 @@ int ffm_engine_destroy(ffm_engine* e) {
 
 static ffm::CoreStepArgs make_args(ffm_engine* e) {
     ffm::CoreStepArgs a{};
+    a.mW = ffm::magic_div((uint32_t)e->d.W);
+    a.mPW = ffm::magic_div((uint32_t)e->d.W + 2u);
     a.H = e->d.H;
     a.W = e->d.W;
     a.HW = e->HW;

@@ -6,8 +6,12 @@
 
 namespace ffm {
 
+// ceil(2^32 / d): n / d == mulhi(n, magic_div(d)) for n < 2^17, d < 2^16 (core_common.h mdiv)
+__host__ __device__ inline uint32_t magic_div(uint32_t d) { return (uint32_t)((0x100000000ull + d - 1) / d); }
+
 struct CoreStepArgs {
     int H, W, HW;          // map shape
+    uint32_t mW, mPW;      // magic_div(W), magic_div(W + 2): row of a cell index by one multiply-high
     int A;                 // agent slots per env (stride of pos)
     int K;                 // envs per workgroup
     long long E;           // envs on this device
