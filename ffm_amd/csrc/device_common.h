@@ -50,6 +50,10 @@ __device__ __forceinline__ int bit_length(uint32_t n) { return n ? 32 - __builti
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
     // Opaque key: keeps the compiler from hoisting the 20-word key schedule out of
     // the step loop into SGPRs (it spills them); 2 s_add per round are cheaper.
+    // (the keys are wave-uniform everywhere; readfirstlane pins them to SGPRs where a
+    // kernel's register allocation moved them into VGPRs -- a no-op otherwise)
+    k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+    k1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
     asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int r = 0; r < 10; r++) {

@@ -176,7 +176,7 @@ static void release(ffm_learner* l) {
 // dense_by > 0: ffm_unified's rank keys map injectively onto
 // ranks * (cap / 256) + bx * dense_by + by (learn_step.hip dense_slot); the capacity is
 // the next power of two >= 256 * Bx * By and the table can never fill.
-// width: values per record (V 1, H 5; H 9 with the Moore neighbourhood, MT step only).
+// width: values per record (V 1, H 5; H 9 with the Moore neighbourhood).
 static hipError_t alloc_table(DevTable& T, int log2cap, int width, uint32_t dense_by = 0, size_t dense_n = 0) {
     T.width = width;
     T.accw = width == 1 ? 2 : width;
@@ -319,9 +319,8 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
     if ((long long)d.H * d.W == 65536 && (d.map[65535] == 0 || d.map[65535] == 3))
         return fail(FFM_E_UNSUPPORTED, "the last cell of a 65536-cell map must be blocked");
-    if (d.neighborhood != 4 && !(d.neighborhood == 8 && d.rng_mode == FFM_RNG_MT))
-        return fail(FFM_E_UNSUPPORTED, "neighborhood 'moore' is built for the reference-exact (MT) step of every "
-                                       "learning variant; the batched step uses 'neumann'");
+    if (d.neighborhood != 4 && d.neighborhood != 8)
+        return fail(FFM_E_INVALID, "neighborhood must be 4 ('neumann') or 8 ('moore')");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
     if (d.n_envs < 1) return fail(FFM_E_INVALID, "n_envs must be >= 1");
     // batched: LDS grid codes hold 14-bit agent indices (<= 16383 agents); the exact (MT) step
@@ -362,7 +361,8 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     l->HW = HW;
     l->F = (int)fl.size();
     l->F_all = l->F;
-    l->D = d.variant == FFM_VARIANT_ACTOR_ONLY ? 4 : 1;
+    // ffm_actor_only: one decision per neighbour (4, Moore 8; model/ffm_actor_only.py:214-355)
+    l->D = d.variant == FFM_VARIANT_ACTOR_ONLY ? d.neighborhood : 1;
     l->actor = d.variant == FFM_VARIANT_ACTOR_ONLY || (d.variant == FFM_VARIANT_UNIFIED && learn->mode != FFM_LEARN_CRITIC_ONLY);
     l->post_update = d.variant == FFM_VARIANT_UNIFIED && learn->mode == FFM_LEARN_ACTOR_ONLY;
     l->trained = d.variant == FFM_VARIANT_TRAINED;
@@ -446,6 +446,7 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     {
         const char* ev = getenv("FFM_TILED");
         l->tiled_ok = !l->mt && d.variant == FFM_VARIANT_UNIFIED && dense_by && learn->block_size == 1 &&
+                      d.neighborhood == 4 &&
                       ffm::learn_batch_raster(HW, d.agent_capacity, l->D) && !(ev && ev[0] == '0') &&
                       (unsigned long long)E * (unsigned long long)A < (1ull << 31);
     }

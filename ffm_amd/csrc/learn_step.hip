@@ -627,23 +627,26 @@ __device__ __forceinline__ void moves5(const LearnArgs& a, int x, int y, const O
     valid[4] = 1;
 }
 
-// The exact kernel's moves: the a.nb neighbours in get_neighbors order (Neumann U, D,
-// L, R; Moore row-major, model/ffm_unified.py:173-185), then stay, with the validity mask.
-// moves5 on the class-carrying grid; cls[k] = the candidate's map class (2 off the map).
-__device__ __forceinline__ void moves5_grid(const LearnArgs& a, int x, int y, const uint16_t* grid, int* coord,
-                                            int* valid, int* inb, int* cls) {
+// The moves on the class-carrying grid: the NB neighbours in get_neighbors order
+// (Neumann U, D, L, R; Moore row-major, model/ffm_unified.py:173-185), then stay, with
+// the validity mask; cls[k] = the candidate's map class (2 off the map).
+template <int NB>
+__device__ __forceinline__ void moves_grid(const LearnArgs& a, int x, int y, const uint16_t* grid, int* coord,
+                                           int* valid, int* inb, int* cls) {
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const int nx = k < 4 ? x + kNBx[k] : x, ny = k < 4 ? y + kNBy[k] : y;
+    for (int k = 0; k <= NB; k++) {
+        const int dx = k == NB ? 0 : NB == 8 ? kMBx[k] : kNBx[k], dy = k == NB ? 0 : NB == 8 ? kMBy[k] : kNBy[k];
+        const int nx = x + dx, ny = y + dy;
         inb[k] = nx >= 0 && nx < a.H && ny >= 0 && ny < a.W;
         coord[k] = inb[k] ? nx * a.W + ny : x * a.W + y;
         const uint32_t g = grid[coord[k]];
         cls[k] = inb[k] ? (int)(g >> 14) : 2;
-        valid[k] = inb[k] && (cls[k] == 0 || cls[k] == 3) && (k == 4 || (g & kGIdx) == kGIdx);
+        valid[k] = inb[k] && (cls[k] == 0 || cls[k] == 3) && (k == NB || (g & kGIdx) == kGIdx);
     }
-    valid[4] = 1;
+    valid[NB] = 1;
 }
 
+// The exact kernel's moves: the a.nb neighbours in get_neighbors order, then stay.
 template <class OCC>
 __device__ void moves_n(const LearnArgs& a, int x, int y, const OCC& occ, int* coord, int* valid, int* inb) {
     const int nb = a.nb;
@@ -692,64 +695,82 @@ __device__ void h_stats_seq(const LearnArgs& a, HStat& hs) {
 }
 
 // A decision's policy, computed once per agent: the normalised cdf of
-// np.random.choice (cdf / cdf[-1], model/ffm_unified.py:497) over the five
-// moves (U, D, L, R, stay; invalid moves carry zero mass) and the valid-move
-// mask for the epsilon branch (:478-495).  ffm_actor_only repeats the same
-// decision up to four times per agent (the inner-loop quirk,
+// np.random.choice (cdf / cdf[-1], model/ffm_unified.py:497) over the NA moves (the
+// neighbours in get_neighbors order, then stay: 5 Neumann, 9 Moore; invalid moves
+// carry zero mass) and the valid-move mask for the epsilon branch (:478-495).
+// ffm_actor_only repeats the same decision once per neighbour (the inner-loop quirk,
 // model/ffm_actor_only.py:214-355): within a batched step the table, DFF and
 // statistics it reads are fixed, so only the draws differ.
-struct Policy {
-    double cn[5];
+template <int NA>
+struct PolicyN {
+    double cn[NA];
     int vmask;            // bit k: move k valid
     int none;             // ffm_ac_core: no request (softmax sum not finite / zero, :187)
 };
+using Policy = PolicyN<5>;
 
-__device__ __forceinline__ int kth_set_bit(int mask, int r) {
-    int k = 4;
+// NumPy's add.reduce of a fixed-length row (np_sum_n with a constant n: a left fold
+// from -0 below eight terms, pairwise from eight on -- Moore's nine moves)
+template <int N, class T>
+__device__ __forceinline__ T np_sum_fix(const T (&e)[N]) {
+    if (N < 8) {
+        T res = T(-0.0);
 #pragma unroll
-    for (int j = 4; j >= 0; j--) {
+        for (int k = 0; k < N; k++) res += e[k];
+        return res;
+    }
+    return np_sum_n(e, N);
+}
+
+template <int NA>
+__device__ __forceinline__ int kth_set_bit(int mask, int r) {
+    int k = NA - 1;
+#pragma unroll
+    for (int j = NA - 1; j >= 0; j--) {
         const int below = __builtin_popcount(mask & ((1 << j) - 1));
         if (((mask >> j) & 1) && below == r) k = j;
     }
     return k;
 }
 
-__device__ __forceinline__ void finish_cdf(Policy& P, const double* p) {
-    double acc = 0.0, cdf[5];
+template <int NA>
+__device__ __forceinline__ void finish_cdf(PolicyN<NA>& P, const double* p) {
+    double acc = 0.0, cdf[NA];
 #pragma unroll
-    for (int k = 0; k < 5; k++) { acc += p[k]; cdf[k] = acc; }
+    for (int k = 0; k < NA; k++) { acc += p[k]; cdf[k] = acc; }
 #pragma unroll
-    for (int k = 0; k < 5; k++) P.cn[k] = cdf[k] / acc;
+    for (int k = 0; k < NA; k++) P.cn[k] = cdf[k] / acc;
 }
 
-template <class R>
-__device__ __forceinline__ int policy_draw(const Policy& P, double eps, R& rng) {
+template <int NA, class R>
+__device__ __forceinline__ int policy_draw(const PolicyN<NA>& P, double eps, R& rng) {
     if (eps > 0 && rng.coin() < eps)
-        return kth_set_bit(P.vmask, (int)rng.randint((uint32_t)__builtin_popcount(P.vmask)));
+        return kth_set_bit<NA>(P.vmask, (int)rng.randint((uint32_t)__builtin_popcount(P.vmask)));
     const double u = rng.u();
-    int k = 4;
+    int k = NA - 1;
 #pragma unroll
-    for (int j = 3; j >= 0; j--) k = P.cn[j] > u ? j : k;
+    for (int j = NA - 2; j >= 0; j--) k = P.cn[j] > u ? j : k;
     return k;
 }
 
 // Actor policy (model/ffm_unified.py:394-476; compat: model/ffm_actor_only.py:257-326,
 // invalid moves -inf then uniform), the same arithmetic as actor_choose.
+template <int NA>
 __device__ __forceinline__ void actor_policy(const LearnArgs& a, const double* hrow, const int* coord,
                                              const int* valid, const float* dff, const HStat& hs, bool compat,
-                                             Policy& P) {
-    double h[5], score[5], e[5], p[5];
+                                             PolicyN<NA>& P) {
+    double h[NA], score[NA], e[NA], p[NA];
 #pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = hrow[k];
+    for (int k = 0; k < NA; k++) h[k] = hrow[k];
     if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
         const double smin = (double)a.smin, smax = (double)a.smax;
 #pragma unroll
-        for (int k = 0; k < 5; k++) h[k] = ((hs.mx - h[k]) / (hs.mx - hs.mn)) * (smax - smin) + smin;
+        for (int k = 0; k < NA; k++) h[k] = ((hs.mx - h[k]) / (hs.mx - hs.mn)) * (smax - smin) + smin;
     }
     bool bad = false;
     int vm = 0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const float d = a.kD32 * dff[coord[k]];
         score[k] = a.nkA * h[k] + (double)d;
         if (compat && !valid[k]) score[k] = -__builtin_inf();
@@ -759,40 +780,40 @@ __device__ __forceinline__ void actor_policy(const LearnArgs& a, const double* h
     // after the bad-score fallback every score is finite: np.max is a plain max
     double mx = -__builtin_inf();
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         if (bad) score[k] = valid[k] ? 1.0 : 0.0;
         const bool in = compat ? valid[k] != 0 : true;
         mx = in && score[k] > mx ? score[k] : mx;
     }
-    double sum = -0.0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const double x = det_exp(score[k] - mx);
         e[k] = valid[k] ? x : 0.0;
-        sum += e[k];
     }
+    const double sum = np_sum_fix(e);
     const int nvalid = __builtin_popcount(vm);
     const bool ok = __builtin_isfinite(sum) && sum > 0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) p[k] = ok ? e[k] / sum : (valid[k] ? 1.0 / (double)nvalid : 0.0);
+    for (int k = 0; k < NA; k++) p[k] = ok ? e[k] / sum : (valid[k] ? 1.0 / (double)nvalid : 0.0);
     P.vmask = vm;
     P.none = 0;
     finish_cdf(P, p);
 }
 
-// ffm_unified critic_only policy (:353-392): SFF/DFF softmax over all five moves,
+// ffm_unified critic_only policy (:353-392): SFF/DFF softmax over all NA moves,
 // invalid ones masked after the exp.
+template <int NA>
 __device__ __forceinline__ void critic_policy(const LearnArgs& a, const int* coord, const int* valid,
-                                              const float* dff, Policy& P) {
-    double p[5];
+                                              const float* dff, PolicyN<NA>& P) {
+    double p[NA];
     int vm = 0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) vm |= valid[k] << k;
+    for (int k = 0; k < NA; k++) vm |= valid[k] << k;
     const int nvalid = __builtin_popcount(vm);
     if (a.sff32) {
-        float s[5], e[5];
+        float s[NA], e[NA];
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float x = a.kS32 * a.sff32[coord[k]];
             const float y = a.kD32 * dff[coord[k]];
             s[k] = x + y;
@@ -800,94 +821,116 @@ __device__ __forceinline__ void critic_policy(const LearnArgs& a, const int* coo
         float mx = s[0];
         bool nan = s[0] != s[0];
 #pragma unroll
-        for (int k = 1; k < 5; k++) {
+        for (int k = 1; k < NA; k++) {
             if (!nan && s[k] != s[k]) { mx = s[k]; nan = true; }
             if (!nan) mx = s[k] > mx ? s[k] : mx;
         }
-        float sum = -0.0f;
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float x = np_expf(s[k] - mx);
             e[k] = valid[k] ? x : 0.0f;
-            sum += e[k];
         }
+        const float sum = np_sum_fix(e);
         const bool ok = __builtin_isfinite(sum) && sum > 0;
         const float u = (float)(1.0 / (double)nvalid);
 #pragma unroll
-        for (int k = 0; k < 5; k++) p[k] = ok ? (double)(e[k] / sum) : (valid[k] ? (double)u : 0.0);
+        for (int k = 0; k < NA; k++) p[k] = ok ? (double)(e[k] / sum) : (valid[k] ? (double)u : 0.0);
     } else {
-        double s[5], e[5];
+        double s[NA], e[NA];
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float y = a.kD32 * dff[coord[k]];
             s[k] = a.kS64 * a.sff64[coord[k]] + (double)y;
         }
-        const double mx = np_max5(s, 5);
-        double sum = -0.0;
+        const double mx = np_max5(s, NA);
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const double x = det_exp(s[k] - mx);
             e[k] = valid[k] ? x : 0.0;
-            sum += e[k];
         }
+        const double sum = np_sum_fix(e);
         const bool ok = __builtin_isfinite(sum) && sum > 0;
 #pragma unroll
-        for (int k = 0; k < 5; k++) p[k] = ok ? e[k] / sum : (valid[k] ? 1.0 / (double)nvalid : 0.0);
+        for (int k = 0; k < NA; k++) p[k] = ok ? e[k] / sum : (valid[k] ? 1.0 / (double)nvalid : 0.0);
     }
     P.vmask = vm;
     P.none = 0;
     finish_cdf(P, p);
 }
 
+// The free moves' terms in order (the compacted candidate list of ffm_ac_core), summed
+// as add.reduce sums that list: a fold below eight terms, pairwise from eight on (Moore:
+// eight or nine free moves; the list is formed by selects, not an indexed array).
+template <int NA, class T>
+__device__ __forceinline__ T np_sum_valid(const T (&e)[NA], const int* valid) {
+    int nc = 0;
+#pragma unroll
+    for (int k = 0; k < NA; k++) nc += valid[k] ? 1 : 0;
+    if (NA < 8 || nc < 8) {
+        T sum = T(-0.0);
+#pragma unroll
+        for (int k = 0; k < NA; k++) sum = valid[k] ? sum + e[k] : sum;
+        return sum;
+    }
+    if (nc == NA) return np_sum_n(e, NA);
+    // NA = 9, one move blocked at z: the list skips it
+    int z = 0;
+#pragma unroll
+    for (int k = NA - 1; k >= 0; k--) z = valid[k] ? z : k;
+    T c[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = j < z ? e[j] : e[j + 1 < NA ? j + 1 : j];
+    return ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
+}
+
 // ffm_ac_core (= ffm_core) policy (model/ffm_ac_core.py:126-199): softmax over the
 // free neighbours + stay.  Slots of blocked / occupied neighbours carry zero mass,
 // which leaves every sum, running cdf and draw exactly as over the compacted list.
+template <int NA>
 __device__ __forceinline__ void ac_policy(const LearnArgs& a, const int* coord, const int* valid,
-                                          const float* dff, Policy& P) {
-    double p[5];
+                                          const float* dff, PolicyN<NA>& P) {
+    double p[NA];
     int vm = 0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) vm |= valid[k] << k;
+    for (int k = 0; k < NA; k++) vm |= valid[k] << k;
     bool fin;
     if (a.sff32) {
-        float s[5], e[5];
+        float s[NA], e[NA];
         float mx = -__builtin_inff();
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float x = a.kS32 * a.sff32[coord[k]];
             const float y = a.kD32 * dff[coord[k]];
             s[k] = x + y;
             mx = valid[k] && s[k] > mx ? s[k] : mx;
         }
-        float sum = -0.0f;
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float x = np_expf(s[k] - mx);
             e[k] = valid[k] ? x : 0.0f;
-            sum = valid[k] ? sum + e[k] : sum;
         }
+        const float sum = np_sum_valid(e, valid);
         fin = __builtin_isfinite(sum) && sum != 0.0f;
 #pragma unroll
-        for (int k = 0; k < 5; k++) p[k] = valid[k] ? (double)(e[k] / sum) : 0.0;
+        for (int k = 0; k < NA; k++) p[k] = valid[k] ? (double)(e[k] / sum) : 0.0;
     } else {
-        double s[5], e[5];
+        double s[NA], e[NA];
         double mx = -__builtin_inf();
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float y = a.kD32 * dff[coord[k]];
             s[k] = a.kS64 * a.sff64[coord[k]] + (double)y;
             mx = valid[k] && s[k] > mx ? s[k] : mx;
         }
-        double sum = -0.0;
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const double x = det_exp(s[k] - mx);
             e[k] = valid[k] ? x : 0.0;
-            sum = valid[k] ? sum + e[k] : sum;
         }
+        const double sum = np_sum_valid(e, valid);
         fin = __builtin_isfinite(sum) && sum != 0.0;
 #pragma unroll
-        for (int k = 0; k < 5; k++) p[k] = valid[k] ? e[k] / sum : 0.0;
+        for (int k = 0; k < NA; k++) p[k] = valid[k] ? e[k] / sum : 0.0;
     }
     P.vmask = vm;
     P.none = !fin;
@@ -899,17 +942,18 @@ __device__ __forceinline__ void ac_policy(const LearnArgs& a, const int* coord, 
 // normalisation in float32 (Python floats are weak scalars next to the f32
 // array), score -k_A*h + k_D*dff in float32, NumPy's float32 exp, masked sum and
 // divide, uniform fallbacks.  Same arithmetic as the oracle's trained_choose.
+template <int NA>
 __device__ __forceinline__ void trained_policy(const LearnArgs& a, int hslot, const int* coord, const int* valid,
-                                               const float* dff, const HStat& hs, Policy& P) {
-    float h[5], score[5], e[5];
-    double p[5];
+                                               const float* dff, const HStat& hs, PolicyN<NA>& P) {
+    float h[NA], score[NA], e[NA];
+    double p[NA];
 #pragma unroll
-    for (int k = 0; k < 5; k++) h[k] = hslot >= 0 ? (float)tval(a.Ht, hslot)[k] : 0.0f;
+    for (int k = 0; k < NA; k++) h[k] = hslot >= 0 ? (float)tval(a.Ht, hslot)[k] : 0.0f;
     if (hs.has && !hs.nonfinite && hs.mx - hs.mn > 1e-6) {
         const float hmax = (float)hs.mx, den = (float)(hs.mx - hs.mn);
         const float srange = (float)((double)a.smax - (double)a.smin), smin = a.smin;
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const float q = (hmax - h[k]) / den;
             const float d = q * srange;
             h[k] = d + smin;
@@ -919,7 +963,7 @@ __device__ __forceinline__ void trained_policy(const LearnArgs& a, int hslot, co
     bool bad = false;
     int vm = 0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const float x = nkA * h[k];
         const float y = a.kD32 * dff[coord[k]];
         score[k] = x + y;
@@ -928,21 +972,20 @@ __device__ __forceinline__ void trained_policy(const LearnArgs& a, int hslot, co
     }
     float mx = -__builtin_inff();
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         if (bad) score[k] = valid[k] ? 1.0f : 0.0f;
         mx = score[k] > mx ? score[k] : mx;
     }
-    float sum = -0.0f;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < NA; k++) {
         const float x = np_expf(score[k] - mx);
         e[k] = valid[k] ? x : 0.0f;
-        sum += e[k];
     }
+    const float sum = np_sum_fix(e);
     const bool ok = __builtin_isfinite(sum) && sum > 0;
     const float u = (float)(1.0 / (double)__builtin_popcount(vm));
 #pragma unroll
-    for (int k = 0; k < 5; k++) p[k] = ok ? (double)(e[k] / sum) : (valid[k] ? (double)u : 0.0);
+    for (int k = 0; k < NA; k++) p[k] = ok ? (double)(e[k] / sum) : (valid[k] ? (double)u : 0.0);
     P.vmask = vm;
     P.none = 0;
     finish_cdf(P, p);
@@ -1335,7 +1378,10 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB,
 // per-slot state word (sa) of learn_batch_kernel: bit 15 = the decide phase inserted H(s)
 constexpr uint32_t kSaNewH = 1u << 15;
 
-template <int BS, int EPB, int APT, int D, bool DL, int VK = 0>
+// NB = 8: the Moore neighbourhood (model/ffm_unified.py:173-185, model/ffm_actor_only.py:
+// 87-93): nine moves, nine-value H rows, requesters of a target on its eight neighbours,
+// ffm_actor_only's eight decisions per agent (D = 8), the eight-neighbour stencil.
+template <int BS, int EPB, int APT, int D, bool DL, int VK = 0, int NB = 4>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(FFM_LBATCH_WAVES, 8)))
 void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1398,15 +1444,22 @@ void learn_batch_kernel(LearnArgs a) {
     // Per-agent state, packed so the APT slots of a lane stay in registers (APT = 8 at
     // C5: unpacked, the kernel spilled to scratch).  pa: cell (bits 0-15) | agent index
     // (16-29).  sa, from decide on: act + 1 (0-2), avalid (3), wexit (4), and from
-    // resolve: coll + 1 (5-9), wins (10-13), next cell (16-31).
+    // resolve: coll + 1 (5-9), wins (10-13), next cell (16-31).  Moore: act + 1 (0-3),
+    // avalid (4), wexit (5), coll + 1 (6-12: up to 72 requests of one target), no wins
+    // (the resolve deposits them itself).
+    constexpr int NA = NB + 1;
+    constexpr int kAB = NB == 8 ? 4 : 3;                      // act + 1 bits
+    constexpr uint32_t kSaValid = 1u << kAB, kSaWexit = 2u << kAB;
+    constexpr int kCS = kAB + 2, kCB = NB == 8 ? 7 : 5;       // coll + 1 shift, bits
+    constexpr uint32_t kSaDecide = (1u << kCS) - 1u;          // act, avalid, wexit
     uint32_t pa[APT], sa[APT];
 #define BK_P(j) ((int)(pa[j] & 0xFFFFu))
 #define BK_IA(j) ((int)(pa[j] >> 16))
-#define BK_ACT(j) ((int)(sa[j] & 7u) - 1)
-#define BK_AVALID(j) ((int)((sa[j] >> 3) & 1u))
-#define BK_WEXIT(j) ((int)((sa[j] >> 4) & 1u))
-#define BK_COLL(j) ((int)((sa[j] >> 5) & 31u) - 1)
-#define BK_WINS(j) ((int)((sa[j] >> 10) & 15u))
+#define BK_ACT(j) ((int)(sa[j] & ((1u << kAB) - 1u)) - 1)
+#define BK_AVALID(j) ((int)((sa[j] >> kAB) & 1u))
+#define BK_WEXIT(j) ((int)((sa[j] >> (kAB + 1)) & 1u))
+#define BK_COLL(j) ((int)((sa[j] >> kCS) & ((1u << kCB) - 1u)) - 1)
+#define BK_WINS(j) (NB == 8 ? 0 : (int)((sa[j] >> 10) & 15u))
 #define BK_NXT(j) ((int)(sa[j] >> 16))
 #define BK_NEWH(j) ((sa[j] & kSaNewH) != 0u)
 #pragma unroll
@@ -1504,26 +1557,29 @@ void learn_batch_kernel(LearnArgs a) {
         const int x = fdiv(BK_P(j), a.mW), y = BK_P(j) - x * W;
         const unsigned long long sk = encode_v(a, variant, smc, x, y);
         if (KEYS) skey[j] = sk;
-        int coord[5], valid[5], inb[5];
-        int cls[5];
-        moves5_grid(a, x, y, grid, coord, valid, inb, cls);
+        int coord[NA], valid[NA], inb[NA];
+        int cls[NA];
+        moves_grid<NB>(a, x, y, grid, coord, valid, inb, cls);
         int ex = -1;                               // first exit among the neighbours
 #pragma unroll
-        for (int k = 3; k >= 0; k--) ex = inb[k] && cls[k] == 3 ? k : ex;
-        Policy P;
+        for (int k = NB - 1; k >= 0; k--) ex = inb[k] && cls[k] == 3 ? k : ex;
+        PolicyN<NA> P;
         if (FFM_LABLATE & 4) {
             req[i * D] = (uint16_t)BK_P(j);
-            sa[j] = 5u | 8u;
+            sa[j] = (uint32_t)NA | kSaValid;
             continue;
         }
         if (variant == kVarAC) {
             // ffm_core candidates: free neighbours, then stay if any (:126-164)
-            if ((valid[0] | valid[1] | valid[2] | valid[3]) == 0) continue;
+            int anyv = 0;
+#pragma unroll
+            for (int k = 0; k < NB; k++) anyv |= valid[k];
+            if (anyv == 0) continue;
             int exv = -1;
 #pragma unroll
-            for (int k = 3; k >= 0; k--) exv = valid[k] && cls[k] == 3 ? k : exv;
+            for (int k = NB - 1; k >= 0; k--) exv = valid[k] && cls[k] == 3 ? k : exv;
             if (exv >= 0) {
-                sa[j] |= 16u;
+                sa[j] |= kSaWexit;
                 req[i] = (uint16_t)coord[exv];
                 continue;
             }
@@ -1536,7 +1592,7 @@ void learn_batch_kernel(LearnArgs a) {
         if (D == 1) {
             int k;
             if (ex >= 0) {
-                sa[j] |= 16u;
+                sa[j] |= kSaWexit;
                 k = ex;
             } else {
                 if (trained) {
@@ -1547,15 +1603,18 @@ void learn_batch_kernel(LearnArgs a) {
                     const int h = (int)dense_slot(sk, a.Ht);
                     if (KEYS) hsl[j] = h;
                     // the record's key with the row (one line): present rows skip the bitmap
-                    const ulonglong2 r0 = trec16(a.Ht, h, 0), r1 = trec16(a.Ht, h, 1), r2 = trec16(a.Ht, h, 2);
-                    const double hr[5] = {__longlong_as_double((long long)r0.y), __longlong_as_double((long long)r1.x),
-                                          __longlong_as_double((long long)r1.y), __longlong_as_double((long long)r2.x),
-                                          __longlong_as_double((long long)r2.y)};
+                    ulonglong2 r[(NA + 2) / 2];
+#pragma unroll
+                    for (int q = 0; q < (NA + 2) / 2; q++) r[q] = trec16(a.Ht, h, q);
+                    double hr[NA];
+#pragma unroll
+                    for (int q = 0; q < NA; q++)
+                        hr[q] = __longlong_as_double((long long)((q & 1) ? r[(q + 1) / 2].x : r[(q + 1) / 2].y));
                     actor_policy(a, hr, coord, valid, dff, hs, false, P);
-                    if (r0.x == kEmptyKey && dense_ensure_new(a.Ht, (uint32_t)h, sk)) sa[j] |= kSaNewH;
+                    if (r[0].x == kEmptyKey && dense_ensure_new(a.Ht, (uint32_t)h, sk)) sa[j] |= kSaNewH;
                 } else {
-                    double hr[5];
-                    const int h = tab_get_row<5>(a.Ht, sk, a.overflow, hr);
+                    double hr[NA];
+                    const int h = tab_get_row<NA>(a.Ht, sk, a.overflow, hr);
                     if (KEYS) hsl[j] = h;
                     if (h < 0) continue;
                     actor_policy(a, hr, coord, valid, dff, hs, false, P);
@@ -1564,32 +1623,32 @@ void learn_batch_kernel(LearnArgs a) {
                 k = policy_draw(P, eps, rng);
             }
             req[i] = (uint16_t)coord[k];
-            sa[j] = (sa[j] & ~15u) | (uint32_t)(k + 1) | ((uint32_t)valid[k] << 3);
+            sa[j] = (sa[j] & ~(kSaValid | ((1u << kAB) - 1u))) | (uint32_t)(k + 1) | ((uint32_t)valid[k] << kAB);
         } else {
             // model/ffm_actor_only.py:214-355: decisions for the neighbours before the
             // first exit, then the exit for the rest; the last one is the agent's action.
             if (ex != 0) {
-                double hr[5];
-                const int h = tab_get_row<5>(a.Ht, sk, a.overflow, hr);
+                double hr[NA];
+                const int h = tab_get_row<NA>(a.Ht, sk, a.overflow, hr);
                 if (KEYS) hsl[j] = h;
                 if (h < 0) continue;
                 actor_policy(a, hr, coord, valid, dff, hs, true, P);
             }
-            int k = 4;
+            int k = NB;
             uint32_t kmi = 0u;
 #pragma unroll
-            for (int d = 0; d < 4; d++) {
+            for (int d = 0; d < D; d++) {
                 if (ex >= 0 && d >= ex) {
                     k = ex;
                 } else {
-                    DrawPh rng(a, genv, (uint32_t)(i * 4 + d));
+                    DrawPh rng(a, genv, (uint32_t)(i * D + d));
                     k = policy_draw(P, eps, rng);
                 }
-                req[i * 4 + d] = (uint16_t)coord[k];
-                kmi |= 1u << ((inb[k] ? k : 4) * 4 + d);   // off the map: the agent's own cell
+                req[i * D + d] = (uint16_t)coord[k];
+                if (D == 4) kmi |= 1u << ((inb[k] ? k : 4) * 4 + d);   // off the map: the agent's own cell
             }
-            km[i] = kmi;
-            sa[j] = (uint32_t)(k + 1) | ((uint32_t)valid[k] << 3) | ((ex >= 0 ? 1u : 0u) << 4);
+            if (D == 4) km[i] = kmi;
+            sa[j] = (uint32_t)(k + 1) | ((uint32_t)valid[k] << kAB) | (ex >= 0 ? kSaWexit : 0u);
         }
     }
     __syncthreads();
@@ -1613,8 +1672,9 @@ void learn_batch_kernel(LearnArgs a) {
             const int tx = fdiv(T, a.mW), ty = T - tx * W;
             int m = 0, owner = 0x7FFFFFFF, rank = 0;
 #pragma unroll
-            for (int c5 = 0; c5 < 5; c5++) {
-                const int cx = c5 < 4 ? tx + kNBx[c5] : tx, cy = c5 < 4 ? ty + kNBy[c5] : ty;
+            for (int c5 = 0; c5 < NA; c5++) {
+                const int cx = c5 < NB ? tx + (NB == 8 ? kMBx[c5] : kNBx[c5]) : tx,
+                          cy = c5 < NB ? ty + (NB == 8 ? kMBy[c5] : kNBy[c5]) : ty;
                 if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
                 const int b = grid[cx * W + cy] & kGIdx;
                 if (b == (int)kGIdx) continue;
@@ -1648,10 +1708,15 @@ void learn_batch_kernel(LearnArgs a) {
             if (rank == w) {
                 wnj++;
                 if (owner > best_won_owner) { best_won_owner = owner; nxj = T; }
+                if (NB == 8) {   // the win's deposit at the agent's own cell (no other lane writes it)
+                    float* c = dff + BK_P(j);
+                    *c = *c + 1.0f;
+                }
             }
         }
         }
-        sa[j] = (sa[j] & (0x1Fu | kSaNewH)) | ((uint32_t)(clj + 1) << 5) | ((uint32_t)wnj << 10) | ((uint32_t)nxj << 16);
+        sa[j] = (sa[j] & (kSaDecide | kSaNewH)) | ((uint32_t)(clj + 1) << kCS) |
+                (NB == 8 ? 0u : (uint32_t)wnj << 10) | ((uint32_t)nxj << 16);
     }
     // deposits at the winners' own cells (distinct per agent: no races); every
     // agent's next cell joins the next state map unless it is an exit
@@ -1768,7 +1833,7 @@ void learn_batch_kernel(LearnArgs a) {
                 rc.r = r; rc.sv = sv; rc.snv = sn; rc.hslot = hslj; rc.k = BK_AVALID(j) ? BK_ACT(j) : -1;
                 a.recs[e * A + i] = rc;
             } else if (BK_AVALID(j) && !(FFM_LABLATE & 1)) {
-                acc_add(acc_at(a.Ht, (size_t)hslj * 5 + BK_ACT(j)), fx(a.alpha_h * tdv));
+                acc_add(acc_at(a.Ht, (size_t)hslj * NA + BK_ACT(j)), fx(a.alpha_h * tdv));
             }
         } while (false);
         if (TILED) {
@@ -1825,8 +1890,8 @@ void learn_batch_kernel(LearnArgs a) {
             const int x = fdiv(c, a.mW), y = c - x * W;
             float acc = a.c0 * dff[c];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int nx = x + kNBx[k], ny = y + kNBy[k];
+            for (int k = 0; k < NB; k++) {
+                const int nx = x + (NB == 8 ? kMBx[k] : kNBx[k]), ny = y + (NB == 8 ? kMBy[k] : kNBy[k]);
                 const float v = (nx >= 0 && nx < H && ny >= 0 && ny < W) ? a.c0 * dff[nx * W + ny] : 0.0f;
                 const float t = a.c1 * v;
                 acc = acc + t;
@@ -2296,10 +2361,10 @@ __global__ __launch_bounds__(256) void learn_hstat_partial(LearnArgs a) {
     const uint32_t n = *a.Ht.n;
     double mn = __builtin_inf(), mx = -__builtin_inf();
     int nf = 0;
+    const int w = (int)a.Ht.accw;      // H rows: 5 values, 9 with the Moore neighbourhood
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const double* v = tval(a.Ht, a.Ht.order[i]);
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < w; k++) {
             nf |= !__builtin_isfinite(v[k]);
             mn = v[k] < mn ? v[k] : mn;
             mx = v[k] > mx ? v[k] : mx;
@@ -2439,7 +2504,7 @@ __global__ __launch_bounds__(256) void learn_post_kernel(LearnArgs a) {
     if (rc.k < 0) return;
     const double vn = rc.snv >= 0 ? tval(a.V, rc.snv)[0] : 0.0;
     const double td = (rc.r + a.gamma * vn) - tval(a.V, rc.sv)[0];
-    acc_add(acc_at(a.Ht, (size_t)rc.hslot * 5 + rc.k), fx(a.alpha_h * td));
+    acc_add(acc_at(a.Ht, (size_t)rc.hslot * a.Ht.accw + rc.k), fx(a.alpha_h * td));
 }
 
 // ===========================================================================
@@ -4146,12 +4211,13 @@ __global__ __launch_bounds__(64) void learn_reset_small_kernel(LearnArgs a, int 
 // nbr > 0: the last nbr workgroups re-place the ended envs as well (ra: the step's
 // arguments after the DFF swap; independent of the tables), four waves of
 // kResetSmallEnvs envs each -- the reset launch's work without its dispatch.
+template <int HWIDTH>
 __global__ __launch_bounds__(256) void learn_apply_vh_kernel(LearnTable V, LearnTable Ht, double* hpart, unsigned nbv,
                                                              unsigned nbh, LearnArgs ra) {
     if (blockIdx.x < nbv) {
         apply_hashed<1, false>(V, nullptr, blockIdx.x, nbv);
     } else if (blockIdx.x < nbv + nbh) {
-        apply_hashed<5, true>(Ht, hpart, blockIdx.x - nbv, nbh);
+        apply_hashed<HWIDTH, true>(Ht, hpart, blockIdx.x - nbv, nbh);
     } else {
         __shared__ __attribute__((aligned(16))) unsigned long long keys[4][kResetSmallF + 2];
         const unsigned w = threadIdx.x >> 6;
@@ -4372,20 +4438,21 @@ void launch_sep_stencil(const LearnArgs& a, hipStream_t s) {
     }
 }
 
-template <int BS, int EPB, int APT, int D, bool DL, int VK = 0>
+template <int BS, int EPB, int APT, int D, bool DL, int VK = 0, int NB = 4>
 hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     LearnArgs a = a0;
-    // the DFF lives in global memory (not DL) and the map is large: stencil apart
-    a.sep_stencil = !DL && a.HW >= kSepStencilHW && (long long)((a.HW + 255) / 256) * a.E < (1ll << 31);
+    // the DFF lives in global memory (not DL) and the map is large: stencil apart (the
+    // separate stencil kernels are Neumann's; Moore's stays fused)
+    a.sep_stencil = NB == 4 && !DL && a.HW >= kSepStencilHW && (long long)((a.HW + 255) / 256) * a.E < (1ll << 31);
     const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D, DL, VK>),
+            reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D, DL, VK, NB>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
     const unsigned blocks = (unsigned)((a.E + EPB - 1) / EPB);
-    learn_batch_kernel<BS, EPB, APT, D, DL, VK><<<dim3(blocks), dim3(BS), smem, s>>>(a);
+    learn_batch_kernel<BS, EPB, APT, D, DL, VK, NB><<<dim3(blocks), dim3(BS), smem, s>>>(a);
     if (a.sep_stencil) launch_sep_stencil(a, s);
     else if (a.tstart_out) (void)launch_learn_tstart_transpose(a, a.tstart_out, s);   // stencil fused: its own launch
     return hipGetLastError();
@@ -4488,7 +4555,28 @@ hipError_t launch_learn_exact(const LearnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The Moore neighbourhood: one workgroup per env (64, 256 or 1,024 lanes, the DFF in LDS
+// when it fits), agents per lane by powers of four beyond 1,024 (fewer shapes to build;
+// no reference driver runs Moore, so it gets the general shapes only).
+template <int D>
+hipError_t launch_batch_moore(const LearnArgs& a, hipStream_t s) {
+    const int A = a.A, HW = a.HW;
+    constexpr size_t kLds = 64 * 1024;
+    if (A <= 64) {
+        if (batch_carve(HW, A, D, 1, true).shared <= kLds) return launch_batch_t<64, 1, 1, D, true, 0, 8>(a, s);
+        return launch_batch_t<64, 1, 1, D, false, 0, 8>(a, s);
+    }
+    if (A <= 256) {
+        if (batch_carve(HW, A, D, 1, true).shared <= kLds) return launch_batch_t<256, 1, 1, D, true, 0, 8>(a, s);
+        return launch_batch_t<256, 1, 1, D, false, 0, 8>(a, s);
+    }
+    if (A <= 1024) return launch_batch_t<1024, 1, 1, D, false, 0, 8>(a, s);
+    if (A <= 4096) return launch_batch_t<1024, 1, 4, D, false, 0, 8>(a, s);
+    return launch_batch_t<1024, 1, 16, D, false, 0, 8>(a, s);
+}
+
 hipError_t launch_learn_batch(const LearnArgs& a, hipStream_t s) {
+    if (a.nb == 8) return a.D == 8 ? launch_batch_moore<8>(a, s) : launch_batch_moore<1>(a, s);
     return a.D == 4 ? launch_batch_d<4>(a, s) : launch_batch_d<1>(a, s);
 }
 
@@ -4498,7 +4586,8 @@ bool learn_reset_small(const LearnArgs& a) { return a.F <= kResetSmallF && a.N <
 hipError_t launch_learn_apply_reset(const LearnArgs& a, const LearnArgs& ra, hipStream_t s) {
     const unsigned nb = kHstatBlocks / 4;
     const unsigned nbr = (unsigned)((ra.E + 4 * kResetSmallEnvs - 1) / (4 * kResetSmallEnvs));
-    learn_apply_vh_kernel<<<dim3(512 + nb + nbr), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, ra);
+    if (a.Ht.accw == 9) learn_apply_vh_kernel<9><<<dim3(512 + nb + nbr), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, ra);
+    else learn_apply_vh_kernel<5><<<dim3(512 + nb + nbr), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, ra);
     learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, (int)nb);
     return hipGetLastError();
 }
@@ -4506,7 +4595,8 @@ hipError_t launch_learn_apply_reset(const LearnArgs& a, const LearnArgs& ra, hip
 hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s) {
     if (v && h && !a.V.dense_by && !a.Ht.dense_by) {     // hashed V and H together
         const unsigned nb = kHstatBlocks / 4;
-        learn_apply_vh_kernel<<<dim3(512 + nb), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, a);
+        if (a.Ht.accw == 9) learn_apply_vh_kernel<9><<<dim3(512 + nb), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, a);
+        else learn_apply_vh_kernel<5><<<dim3(512 + nb), dim3(256), 0, s>>>(a.V, a.Ht, a.hpart, 512u, nb, a);
         learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, (int)nb);
         return hipGetLastError();
     }
@@ -4518,7 +4608,10 @@ hipError_t launch_learn_apply(const LearnArgs& a, bool v, bool h, hipStream_t s)
         // dense: a streaming pass over every slot wants the whole chip; hashed: the
         // insertion-order pass over n entries needs far fewer partials
         const int nb = a.Ht.dense_by ? kHstatBlocks : kHstatBlocks / 4;
-        if (a.Ht.dense_by) learn_apply_dense_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        // (H rows: 5 values, 9 with the Moore neighbourhood)
+        if (a.Ht.dense_by && a.Ht.accw == 9) learn_apply_dense_kernel<9, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        else if (a.Ht.dense_by) learn_apply_dense_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
+        else if (a.Ht.accw == 9) learn_apply_kernel<9, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
         else learn_apply_kernel<5, true><<<dim3(nb), dim3(256), 0, s>>>(a.Ht, a.hpart);
         learn_hstat_final<<<dim3(1), dim3(64), 0, s>>>(a, nb);
     }
@@ -4693,6 +4786,7 @@ hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
 hipError_t launch_learn_delta_export(const LearnTable& T, int width, unsigned long long* keys, long long* acc,
                                     long long cap, unsigned long long* count, hipStream_t s) {
     if (width == 2) learn_delta_export_kernel<2><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
+    else if (width == 9) learn_delta_export_kernel<9><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
     else learn_delta_export_kernel<5><<<dim3(1024), dim3(256), 0, s>>>(T, keys, acc, cap, count);
     return hipGetLastError();
 }
@@ -4703,6 +4797,7 @@ hipError_t launch_learn_delta_merge(const LearnTable& T, int width, const unsign
     if (n <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)std::min<long long>(4096, (n + 255) / 256);
     if (width == 2) learn_delta_merge_kernel<2><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
+    else if (width == 9) learn_delta_merge_kernel<9><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
     else learn_delta_merge_kernel<5><<<dim3(blocks), dim3(256), 0, s>>>(T, keys, acc, n, overflow, dn);
     return hipGetLastError();
 }

@@ -521,7 +521,10 @@ class Learner:
         d.variant = _LEARN_VARIANTS[variant]
         d.H, d.W = self.H, self.W
         d.map, d.sff, d.sff_dtype = self.map.ctypes.data, self.sff.ctypes.data, sdt
-        d.neighborhood = 4 if p.get("neighborhood", "neumann") == "neumann" else 8
+        nbn = p.get("neighborhood", "neumann")
+        if nbn not in ("neumann", "moore"):
+            raise ValueError(f"neighborhood must be 'neumann' or 'moore', got {nbn!r}")
+        d.neighborhood = 4 if nbn == "neumann" else 8
         # H rows: one value per move (the neighbours, then stay)
         self.n_actions = d.neighborhood + 1
         d.k_S, d.k_D = float(p.get("k_S", 0.0)), float(p["k_D"])

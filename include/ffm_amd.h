@@ -189,8 +189,9 @@ int ffm_engine_set_step_index(ffm_engine* eng, uint32_t t);
  * (DESIGN.md section 9): all envs in parallel against the tables as they were at
  * the start of the step, increments summed in 2^-32 fixed point, on-device
  * episode ends (emptied or max_steps) with Philox placement.
- * Learning variants require neighborhood 4 (all of the reference's learning
- * drivers use "neumann") and map values in 0..3.  Table keys are packed u64
+ * Learning variants take neighborhood 4 ("neumann", every reference driver) or 8
+ * ("moore": nine moves and nine-value H rows, model/ffm_unified.py:173-185,
+ * model/ffm_actor_only.py:87-93; in both rng modes) and map values in 0..3.  Table keys are packed u64
  * (ffm_amd/learn_keys.py): 2 bits per cell / rank in [0,26), bx in [26,45),
  * by in [45,64).
  */

@@ -993,7 +993,7 @@ void ffo_lbatch_post(ffo_lbatch* b) {
             if (!q->valid) continue;
             const double vn = q->snv >= 0 ? b->V->vals[q->snv] : 0.0;
             const double td = (q->r + c->gamma * vn) - b->V->vals[q->sv];
-            b->Ht->acc[(int64_t)q->hslot * 5 + q->k] += fx(c->alpha_h * td);
+            b->Ht->acc[(int64_t)q->hslot * b->Ht->width + q->k] += fx(c->alpha_h * td);
         }
 }
 

@@ -88,8 +88,12 @@ def test_learner_validation_before_device(lib):
         Learner(m, s, "nope", n_envs=1, n_agents=4)
     with pytest.raises(ValueError):
         Learner(m, s, "ac", n_envs=1, n_agents=101)
+    with pytest.raises(ValueError):
+        Learner(m, s, "ac", n_envs=1, n_agents=4, params={"neighborhood": "hex"})
+    odd = m.copy()
+    odd[5, 5] = 4            # a map value outside the learning variants' state keys
     with pytest.raises(NotImplementedError):
-        Learner(m, s, "ac", n_envs=1, n_agents=4, params={"neighborhood": "moore"})
+        Learner(odd, s, "ac", n_envs=1, n_agents=4)
     bad = m.copy()
     bad[5, 0] = 0
     with pytest.raises(ValueError):

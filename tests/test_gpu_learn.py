@@ -120,14 +120,15 @@ def test_learner_replays_reference_goldens(name):
 # ---------------------------------------------------------------------------
 # Philox (batched) mode: GPU == CPU restatement
 # ---------------------------------------------------------------------------
-def _random_rank_table(H, W, bs, seed=0, frac=0.6):
-    """A trained-actor-like H over the rank keys of an H x W map (ffm_trained_core input)."""
+def _random_rank_table(H, W, bs, seed=0, frac=0.6, width=5):
+    """A trained-actor-like H over the rank keys of an H x W map (ffm_trained_core input;
+    width 9 for the Moore neighbourhood)."""
     from ffm_amd import learn_keys as K
     rs = np.random.RandomState(seed)
     keys = [K.pack(((c >> 0) & 3, (c >> 2) & 3, (c >> 4) & 3, (c >> 6) & 3), bx, by)
             for bx in range((H - 1) // bs + 1) for by in range((W - 1) // bs + 1) for c in range(256)
             if rs.uniform() < frac]
-    return np.array(keys, np.uint64), rs.standard_normal((len(keys), 5)) * 3.0
+    return np.array(keys, np.uint64), rs.standard_normal((len(keys), width)) * 3.0
 
 
 def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
@@ -142,7 +143,8 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
                  rng="philox", seed=seed, auto_reset=True, max_steps=max_steps, env_base=env_base)
     cpu = LO.Learn(m, s, variant, mode, params, log2_cap=log2_cap)
     if variant == "trained":
-        hk, hv = _random_rank_table(H, W, int(params.get("block_size", 5)), seed=seed)
+        hk, hv = _random_rank_table(H, W, int(params.get("block_size", 5)), seed=seed,
+                                    width=9 if params.get("neighborhood") == "moore" else 5)
         L.import_table("H", hk, hv)
         cpu.Ht.load(hk, hv)
     core = O.Core(m, s, {"neighborhood": "neumann"})
@@ -221,6 +223,23 @@ def test_learner_philox_large_rooms(variant, mode):
     p = {"block_size": 5}
     _philox_compare(variant, mode, p, 40, 40, 200, 64, 40, max_steps=30, seed=3)
     _philox_compare(variant, mode, p, 64, 64, 600, 16, 25, max_steps=20, seed=4)
+
+
+@pytest.mark.parametrize("variant,mode", VARIANTS + [("trained", None)])
+def test_learner_philox_moore_matches_cpu(variant, mode):
+    """The Moore neighbourhood in the batched learner (model/ffm_unified.py:173-185,
+    model/ffm_actor_only.py:87-93): nine moves, nine-value H rows, requesters on a
+    target's eight neighbours, eight decisions per ffm_actor_only agent, the
+    eight-neighbour stencil.  12x12 / 32 agents at 2,048 envs; then the 256-lane,
+    1,024-lane and four-agents-per-lane workgroup shapes (odd room, env ids offset)."""
+    p = {"neighborhood": "moore", "epsilon": 0.1, "block_size": 1} if variant != "ac" else {"neighborhood": "moore"}
+    _, eps = _philox_compare(variant, mode, p, 12, 12, 32, 2048, 120)
+    assert eps.sum() > 0
+    p = dict(p, block_size=5)
+    _philox_compare(variant, mode, p, 40, 40, 200, 64, 40, max_steps=30, seed=3)
+    _philox_compare(variant, mode, p, 64, 64, 600, 16, 25, max_steps=20, seed=4)
+    _philox_compare(variant, mode, dict(p, k_D=2), 50, 77, 1300, 6, 16, A=2000, max_steps=10, seed=6,
+                    env_base=77)
 
 
 @pytest.mark.parametrize("mode", ["critic_only", "actor_only", "both"])
