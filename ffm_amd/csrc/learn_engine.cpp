@@ -76,6 +76,9 @@ struct ffm_learner {
     unsigned char* d_scratch = nullptr;
     uint32_t dense_bx = 0;             // dense tables: x blocks (import validation)
     bool hstat_valid = false;          // d_hstat holds the H statistics of the current table
+    long long hx_n = 0;                // ffm_learner_set_h_extra: values outside the table
+    int hx_nf = 0;
+    double hx_mn = 0.0, hx_mx = 0.0;
     int phase = 0;                     // batched step in phases: 0 idle, 1 local done, 2 V applied
     unsigned long long* d_count = nullptr;   // delta export record counter
     int32_t* d_eplog = nullptr;              // [eplog_cap][4] ended episodes
@@ -243,6 +246,7 @@ static ffm::LearnArgs make_args(ffm_learner* l) {
     a.counters = l->d_ctr;
     a.V = l->V.t; a.Ht = l->H.t;
     a.hstat = l->d_hstat; a.hpart = l->d_hpart; a.recs = l->d_recs; a.overflow = l->d_overflow;
+    a.hx_n = l->hx_n; a.hx_nf = l->hx_nf; a.hx_mn = l->hx_mn; a.hx_mx = l->hx_mx;
     a.key0 = (uint32_t)d.seed; a.key1 = (uint32_t)(d.seed >> 32); a.t = l->t;
     a.auto_reset = d.auto_reset && !l->mt; a.max_steps = l->L.max_steps;
     a.mt_np = l->d_mt_np; a.mt_py = l->d_mt_py; a.scratch = l->d_scratch;
@@ -869,6 +873,19 @@ int ffm_learner_get_counters(ffm_learner* l, uint64_t* counters, void* stream) {
 int ffm_learner_set_epsilon(ffm_learner* l, double epsilon) {
     if (!l) return fail(FFM_E_INVALID, "null learner");
     l->L.epsilon = std::min(std::max(epsilon, 0.0), 1.0);      // np.clip (model/ffm_unified.py:867)
+    return FFM_OK;
+}
+
+int ffm_learner_set_h_extra(ffm_learner* l, int64_t n_values, double mn, double mx, int32_t nonfinite) {
+    if (!l) return fail(FFM_E_INVALID, "null learner");
+    if (!l->trained) return fail(FFM_E_INVALID, "extra H statistics are ffm_trained_core's (FFM_VARIANT_TRAINED)");
+    if (n_values < 0) return fail(FFM_E_INVALID, "n_values must be >= 0");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "a phased step is in progress");
+    l->hx_n = n_values;
+    l->hx_nf = n_values > 0 && nonfinite ? 1 : 0;
+    l->hx_mn = n_values > 0 ? mn : 0.0;
+    l->hx_mx = n_values > 0 ? mx : 0.0;
+    l->hstat_valid = false;            // the next step recomputes the statistics with them
     return FFM_OK;
 }
 

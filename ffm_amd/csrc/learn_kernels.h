@@ -105,6 +105,11 @@ struct LearnArgs {
     unsigned long long* counters;  // [E][4] agent_steps, exits, resets, steps
     LearnTable V, Ht;
     double* hstat;              // [4] has, nonfinite, min, max of H (step start)
+    // ffm_trained_core: values of rows held outside the table (ffm_learner_set_h_extra),
+    // joined into every H statistics pass
+    long long hx_n;
+    int hx_nf;
+    double hx_mn, hx_mx;
     double* hpart;              // [2 * kHstatBlocks * 4] partials
     LearnRec* recs;             // [E][A]
     TileRec* trecs;             // [E][A] tiled step: per-agent records in raster order (nullptr: off)

@@ -692,6 +692,12 @@ __device__ void h_stats_seq(const LearnArgs& a, HStat& hs) {
             hs.mx = v[k] > hs.mx ? v[k] : hs.mx;
         }
     }
+    if (a.hx_n > 0) {          // ffm_trained_core rows held outside the table
+        hs.has = 1;
+        hs.nonfinite |= a.hx_nf;
+        hs.mn = a.hx_mn < hs.mn ? a.hx_mn : hs.mn;
+        hs.mx = a.hx_mx > hs.mx ? a.hx_mx : hs.mx;
+    }
 }
 
 // A decision's policy, computed once per agent: the normalised cdf of
@@ -2389,7 +2395,12 @@ __global__ __launch_bounds__(64) void learn_hstat_final(LearnArgs a, int nb) {
         nf |= __shfl_xor(nf, o);
     }
     if (threadIdx.x == 0) {
-        a.hstat[0] = *a.Ht.n > 0 ? 1.0 : 0.0;
+        if (a.hx_n > 0) {      // ffm_trained_core rows held outside the table (ffm_learner_set_h_extra)
+            mn = a.hx_mn < mn ? a.hx_mn : mn;
+            mx = a.hx_mx > mx ? a.hx_mx : mx;
+            nf |= a.hx_nf;
+        }
+        a.hstat[0] = *a.Ht.n > 0 || a.hx_n > 0 ? 1.0 : 0.0;
         a.hstat[1] = nf ? 1.0 : 0.0;
         a.hstat[2] = mn;
         a.hstat[3] = mx;

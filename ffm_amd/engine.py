@@ -45,7 +45,7 @@ EXPORTED = [
     "ffm_learner_set_tile_owners", "ffm_learner_owner_buffers", "ffm_learner_step_owner_local",
     "ffm_learner_step_owner_v", "ffm_learner_step_owner_h", "ffm_learner_step_owner_end",
     "ffm_learner_set_epsilon_stride", "ffm_learner_set_episode_caps", "ffm_learner_set_owner_capacity",
-    "ffm_learner_set_owner_send_buffer", "ffm_learner_set_owner_output_buffers",
+    "ffm_learner_set_owner_send_buffer", "ffm_learner_set_owner_output_buffers", "ffm_learner_set_h_extra",
 ]
 
 VARIANT_AC, VARIANT_UNIFIED, VARIANT_ACTOR_ONLY, VARIANT_TRAINED = 1, 2, 3, 4
@@ -144,6 +144,7 @@ def load_library():
     L.ffm_learner_get_counters.argtypes = [P, P, P]
     L.ffm_learner_set_epsilon.argtypes = [P, C.c_double]
     L.ffm_learner_set_v_default.argtypes = [P, C.c_double, P]
+    L.ffm_learner_set_h_extra.argtypes = [P, C.c_int64, C.c_double, C.c_double, C.c_int32]
     L.ffm_learner_table_size.argtypes = [P, i32, C.POINTER(i64), P]
     L.ffm_learner_export_table.argtypes = [P, i32, P, P, i64, C.POINTER(i64), P]
     L.ffm_learner_import_table.argtypes = [P, i32, P, P, i64, P]
@@ -577,6 +578,19 @@ class Learner:
 
     def set_epsilon(self, eps: float):
         _check(self._L.ffm_learner_set_epsilon(self._h, float(eps)))
+
+    def set_h_extra(self, values):
+        """ffm_trained_core: the values of trained H rows whose length is not the move count
+        (model/ffm_trained_core.py:228-267: such a state scores as a missing row, but its
+        values join the whole-table min / max of the normalisation)."""
+        v = np.asarray(values, dtype=np.float64).ravel()
+        if len(v) == 0:
+            _check(self._L.ffm_learner_set_h_extra(self._h, 0, 0.0, 0.0, 0))
+            return
+        fin = np.isfinite(v)
+        nf = int(not fin.all())
+        mn, mx = (float(v[fin].min()), float(v[fin].max())) if fin.any() else (0.0, 0.0)
+        _check(self._L.ffm_learner_set_h_extra(self._h, len(v), mn, mx, nf))
 
     def set_placement(self, cells=None, n_agents: int | None = None):
         """Placement candidates of later resets (cell indices x*W+y; None = every free

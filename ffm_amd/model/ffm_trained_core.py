@@ -44,17 +44,20 @@ class FloorFieldModel(LearnModel):
             ranks = tuple(int(r) for r in original[0])
             block = (int(original[1][0]), int(original[1][1]))
             self.H[(ranks, block)] = v
-        # one preference per move: the neighbours then stay, 5 (neumann) or 9 (moore, :76-85);
-        # the reference reads a row of another length as zeros but still counts its values in
-        # the table's min / max (:228-267), which this table layout cannot hold
+        # one preference per move: the neighbours then stay, 5 (neumann) or 9 (moore, :76-85).
+        # A row of another length scores as a missing state (zeros, :228-239) but its values
+        # still join the table's min / max (:242-267): they go to the learner's extra
+        # statistics instead of the table.
         width = len(self.neighbors) + 1
-        rows = [(K.from_rank_tuple(k), v) for k, v in self.H.items() if isinstance(v, list) and len(v) == width]
-        if len(rows) != len(self.H):
-            raise NotImplementedError(f"trained H rows must be lists of {width} preferences "
-                                      f"({self.params['neighborhood']} neighbourhood)")
+        if any(not isinstance(v, list) for v in self.H.values()):
+            raise NotImplementedError("trained H rows must be lists of preferences (model/ffm_trained_core.py:242-249)")
+        rows = [(K.from_rank_tuple(k), v) for k, v in self.H.items() if len(v) == width]
         if rows:
             self._learner.import_table("H", np.array([k for k, _ in rows], np.uint64),
                                        np.array([[float(x) for x in v] for _, v in rows], np.float64))
+        odd = [float(x) for v in self.H.values() if len(v) != width for x in v]
+        if odd:
+            self._learner.set_h_extra(np.array(odd, np.float64))
         print(f"✓ 学習済みHテーブルを読み込みました: {len(self.H)}状態")
 
     def initialize_agents(self):

@@ -256,6 +256,12 @@ int ffm_learner_export_table(ffm_learner* l, int32_t which, uint64_t* keys, doub
 /* Replace the table by these entries, inserted in the given order. */
 int ffm_learner_import_table(ffm_learner* l, int32_t which, const uint64_t* keys, const double* vals,
                              int64_t n, void* stream);
+/* ffm_trained_core (FFM_VARIANT_TRAINED only): values of trained H rows the table cannot
+ * hold -- rows whose length is not the move count (model/ffm_trained_core.py:228-249: such
+ * a state scores as a missing row, zeros) -- that still join the whole-table min / max of
+ * the normalisation (:242-267).  n_values values with these min / max (nonfinite: any of
+ * them NaN or inf); n_values = 0 clears.  Kept across import_table. */
+int ffm_learner_set_h_extra(ffm_learner* l, int64_t n_values, double min, double max, int32_t nonfinite);
 /* The batched (Philox) step in phases, for multi-rank runs whose ranks share
  * the tables (ffm_amd/dist.py TableSync):
  *   step_local -> exchange V (and H unless unified actor_only) -> step_apply(V)

@@ -38,6 +38,12 @@ struct ffo_tab {
     double* vals;
     int64_t* acc;          /* batched fixed-point accumulators */
     int64_t* order;        /* slot of the i-th inserted key */
+    /* ffm_trained_core: values of rows whose length is not the move count (a state with
+     * such a row scores as missing, yet its values join the table's min / max,
+     * model/ffm_trained_core.py:228-267) */
+    int64_t xn;
+    int xnf;
+    double xmn, xmx;
 };
 
 static uint64_t mix64(uint64_t z) {
@@ -364,7 +370,8 @@ typedef struct {
 } hstats;
 
 static void h_stats(const ffo_tab* Ht, hstats* s) {
-    s->has = Ht->n > 0; s->nonfinite = 0; s->mn = INFINITY; s->mx = -INFINITY;
+    s->has = Ht->n > 0 || Ht->xn > 0; s->nonfinite = Ht->xnf; s->mn = INFINITY; s->mx = -INFINITY;
+    if (Ht->xn > 0) { s->mn = Ht->xmn; s->mx = Ht->xmx; }
     for (int64_t i = 0; i < Ht->n; i++) {
         const double* v = Ht->vals + Ht->order[i] * Ht->width;
         for (int k = 0; k < Ht->width; k++) {
@@ -372,6 +379,17 @@ static void h_stats(const ffo_tab* Ht, hstats* s) {
             if (v[k] < s->mn) s->mn = v[k];
             if (v[k] > s->mx) s->mx = v[k];
         }
+    }
+}
+
+/* The values of the rows the table cannot hold (all_h_values' other entries,
+ * model/ffm_trained_core.py:242-249): their count, min, max and whether one is NaN/inf. */
+void ffo_tab_set_extra(ffo_tab* t, const double* vals, int64_t n) {
+    t->xn = n; t->xnf = 0; t->xmn = INFINITY; t->xmx = -INFINITY;
+    for (int64_t i = 0; i < n; i++) {
+        if (!isfinite(vals[i])) t->xnf = 1;
+        if (vals[i] < t->xmn) t->xmn = vals[i];
+        if (vals[i] > t->xmx) t->xmx = vals[i];
     }
 }
 

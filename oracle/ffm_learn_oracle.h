@@ -108,6 +108,7 @@ int32_t ffo_tab_accw(const ffo_tab* t);
 void ffo_tab_set_alpha(ffo_tab* t, double alpha);
 int ffo_tab_delta_merge(ffo_tab* t, const uint64_t* keys, const int64_t* acc, int64_t n, const double* init);
 void ffo_tab_apply(ffo_tab* t);
+void ffo_tab_set_extra(ffo_tab* t, const double* vals, int64_t n);
 
 /* Deterministic float64 exp (fdlibm's algorithm, +,*,/ only): the f64
  * softmax of the actor modes on CPU and GPU alike. */

@@ -95,6 +95,7 @@ def _lib():
         L.ffo_encode_rank.restype = C.c_uint64
         L.ffo_encode_cells13.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
         L.ffo_encode_cells13.restype = C.c_uint64
+        L.ffo_tab_set_extra.argtypes = [P, P, C.c_int64]
         _done = True
     return L
 
@@ -125,6 +126,11 @@ class Table:
         v = np.ascontiguousarray(vals, np.float64).reshape(len(k), self.width)
         if _lib().ffo_tab_import(self.h, O._ptr(k), O._ptr(v), len(k)):
             raise RuntimeError("table full")
+
+    def set_extra(self, vals):
+        """ffm_trained_core: values of rows of another length (they join the min / max only)."""
+        v = np.ascontiguousarray(vals, np.float64).ravel()
+        _lib().ffo_tab_set_extra(self.h, O._ptr(v) if len(v) else None, len(v))
 
 
 class Learn:

@@ -175,9 +175,15 @@ def run_trained_case(name, cls, map_array, sff, params, N, seeds, n_ep, max_step
         v_keys=np.zeros(0, np.uint64), v_vals=np.zeros(0, np.float64), v_n=np.zeros(len(seeds), np.int64),
         h_keys=np.zeros(0, np.uint64), h_vals=np.zeros((0, width), np.float64), h_n=np.zeros(len(seeds), np.int64),
         np_tail=np.stack(np_tail), py_tail=np.stack(py_tail),
-        pre_h_keys=np.asarray([K.from_rank_tuple(k) for k in h_table], np.uint64),
-        pre_h_vals=np.asarray([list(map(float, v)) for v in h_table.values()], np.float64).reshape(-1, width),
+        pre_h_keys=np.asarray([K.from_rank_tuple(k) for k, v in h_table.items() if len(v) == width], np.uint64),
+        pre_h_vals=np.asarray([list(map(float, v)) for v in h_table.values() if len(v) == width],
+                              np.float64).reshape(-1, width),
     )
+    odd = [(k, v) for k, v in h_table.items() if len(v) != width]
+    if odd:   # rows of another length: scored as missing, counted in the min / max (:228-267)
+        out["pre_h_odd_keys"] = np.asarray([K.from_rank_tuple(k) for k, _ in odd], np.uint64)
+        out["pre_h_odd_lens"] = np.asarray([len(v) for _, v in odd], np.int32)
+        out["pre_h_odd_vals"] = np.asarray([float(x) for _, v in odd for x in v], np.float64)
     path = os.path.join(HERE, f"learn_{name}.npz")
     np.savez_compressed(path, **out)
     print(f"{name}: seeds={len(seeds)} episodes={len(nsteps)} steps={sum(nsteps)} |H|={len(h_table)} "
@@ -285,7 +291,7 @@ def main():
 
     # ffm_trained_core with an H trained by the reference's unified actor
     # (run_trained_ffm.py loads such a table, :141-203)
-    if not only or "trained_12x12_N24" in only or "trained_12x12_N40_bs5" in only:
+    if not only or {"trained_12x12_N24", "trained_12x12_N40_bs5", "trained_oddrows_12x12_N24"} & only:
         np.random.seed(17)
         random.seed(17)
         with tempfile.TemporaryDirectory() as td, contextlib.redirect_stdout(io.StringIO()):
@@ -304,6 +310,25 @@ def main():
             run_trained_case("trained_12x12_N24", TR, m12, s12, tr_p, 24, [18, 19], 3, 300, tables[1])
         if not only or "trained_12x12_N40_bs5" in only:
             run_trained_case("trained_12x12_N40_bs5", TR, m12, s12, {}, 40, [20], 3, 300, tables[5])
+        if not only or "trained_oddrows_12x12_N24" in only:
+            # rows of other lengths (model/ffm_trained_core.py:228-249): every fourth state's
+            # row shortened or lengthened, with the table's extremes among them; a few states
+            # the actor never stored; one empty row
+            rs = np.random.RandomState(31)
+            t1 = dict(tables[1])
+            vals = np.concatenate([np.asarray(v, np.float64) for v in t1.values()])
+            lo, hi = float(vals.min()), float(vals.max())
+            for i, k in enumerate(list(t1)):
+                if i % 4 == 1:
+                    n = int(rs.choice([1, 3, 4, 6, 9]))
+                    t1[k] = [float(x) for x in rs.uniform(lo, hi, n)]
+            ks = list(t1)
+            t1[ks[2]] = [hi + 7.5, 0.25, lo]
+            t1[ks[6]] = [lo - 3.25]
+            t1[ks[10]] = []
+            for c in range(6):
+                t1[((3, 3, c % 4, (c + 1) % 4), (100 + c, 200 - c))] = [float(x) for x in rs.uniform(lo, hi, 2)]
+            run_trained_case("trained_oddrows_12x12_N24", TR, m12, s12, tr_p, 24, [24, 25], 3, 300, t1)
 
     # ffm_trained_core with the Moore neighbourhood (:76-85, nine-value rows :228-236), driven
     # by the nine-value H of a Moore unified actor

@@ -58,9 +58,14 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
     kw = {}
     if "pre_h_keys" in z:            # a trained actor, pickled as run_trained_ffm.py loads it
         kw["h_table_path"] = str(tmp_path / "h.pkl")
+        rows = {pickle.dumps(K.to_rank_tuple(k)): [float(x) for x in v]
+                for k, v in zip(z["pre_h_keys"], z["pre_h_vals"])}
+        if "pre_h_odd_keys" in z:    # rows of other lengths (model/ffm_trained_core.py:228-267)
+            ends = np.cumsum(z["pre_h_odd_lens"])
+            for k, e, n in zip(z["pre_h_odd_keys"], ends, z["pre_h_odd_lens"]):
+                rows[pickle.dumps(K.to_rank_tuple(k))] = [float(x) for x in z["pre_h_odd_vals"][e - n:e]]
         with open(kw["h_table_path"], "wb") as f:
-            pickle.dump({pickle.dumps(K.to_rank_tuple(k)): [float(x) for x in v]
-                         for k, v in zip(z["pre_h_keys"], z["pre_h_vals"])}, f)
+            pickle.dump(rows, f)
     if "pre_keys" in z:
         kw["pretrained_v_path"] = str(tmp_path / "v.pkl")
         if variant == "unified":
@@ -112,7 +117,7 @@ def test_dropin_class_reproduces_reference_driver_loop(name, tmp_path):
         if variant == "trained":
             assert list(np.random.mtrand._rand._bit_generator.random_raw(4)) == list(z["np_tail"][si])
             assert [random.getrandbits(32) for _ in range(4)] == list(z["py_tail"][si])
-            assert len(model.H) == len(z["pre_h_keys"])
+            assert len(model.H) == len(z["pre_h_keys"]) + len(z.get("pre_h_odd_keys", ()))
             model.close()
             continue
         V = model.get_v_table()

@@ -62,7 +62,8 @@ def test_learner_replays_reference_goldens(name):
     for si, seed in enumerate(z["seeds"]):
         L = _learner(z["map"], z["sff"], variant, n_envs=1, n_agents=0, agent_capacity=max(N, 1), mode=mode,
                      params=params, rng="mt", auto_reset=False)
-        inert_k, inert_v = pretrained(z, variant, lambda k, v, w="V": L.import_table(w, k, v))
+        inert_k, inert_v = pretrained(z, variant, lambda k, v, w="V": L.set_h_extra(v) if w == "Hx"
+                                      else L.import_table(w, k, v))
         np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
         for ep in range(n_ep):
             if ep > 0 and int(z["reload_v"]):

@@ -33,6 +33,8 @@ def pretrained(z, variant, load):
     none = (np.zeros(0, np.uint64), np.zeros(0, np.float64))
     if "pre_h_keys" in z:                # ffm_trained_core: the trained H (model/ffm_trained_core.py:51-68)
         load(z["pre_h_keys"], z["pre_h_vals"], "H")
+        if "pre_h_odd_vals" in z:        # rows of another length: only their values' min / max (:228-267)
+            load(None, z["pre_h_odd_vals"], "Hx")
         return none
     if "pre_keys" not in z:
         return none
@@ -53,7 +55,8 @@ def replay(z, make_step):
     v_off = h_off = 0
     for si, seed in enumerate(z["seeds"]):
         L = LO.Learn(z["map"], z["sff"], variant, mode, params)
-        inert_k, inert_v = pretrained(z, variant, lambda k, v, w="V": (L.V if w == "V" else L.Ht).load(k, v))
+        inert_k, inert_v = pretrained(z, variant, lambda k, v, w="V": L.Ht.set_extra(v) if w == "Hx"
+                                      else (L.V if w == "V" else L.Ht).load(k, v))
         np_rng, py_rng = O.seeded_np(int(seed)), O.seeded_py(int(seed))
         for ep in range(n_ep):
             if ep > 0 and int(z["reload_v"]):
