@@ -407,6 +407,21 @@ __device__ unsigned long long encode(const LearnArgs& a, const SM& sm, int x, in
     return encode_v(a, a.variant, sm, x, y);
 }
 
+// enc13 from packed state rows (learn_batch_kernel's batch_rows: row x + 2 holds map row x,
+// cell y at bits 2 (y + 2), two halo rows / columns of the out-of-map value): the 3 x 3
+// block's rows shifted into place, then the four cells two steps away -- the key enc13
+// builds cell by cell.
+__device__ __forceinline__ unsigned long long enc13_rows(const uint32_t* rw, int x, int y, uint32_t mbs) {
+    const uint32_t r0 = rw[x], r1 = rw[x + 1], r2 = rw[x + 2], r3 = rw[x + 3], r4 = rw[x + 4];
+    const int s1 = 2 * (y + 1);
+    const unsigned long long cells =
+        (unsigned long long)((r1 >> s1) & 0x3Fu) | ((unsigned long long)((r2 >> s1) & 0x3Fu) << 6) |
+        ((unsigned long long)((r3 >> s1) & 0x3Fu) << 12) | ((unsigned long long)((r0 >> (s1 + 2)) & 3u) << 18) |
+        ((unsigned long long)((r4 >> (s1 + 2)) & 3u) << 20) | ((unsigned long long)((r2 >> (s1 - 2)) & 3u) << 22) |
+        ((unsigned long long)((r2 >> (s1 + 6)) & 3u) << 24);
+    return pack_key(cells, fdiv(x, mbs), fdiv(y, mbs));
+}
+
 // ---- random draws -----------------------------------------------------------
 __device__ uint32_t mt_interval(uint32_t* mt, uint32_t max) {     // NumPy legacy randint(max + 1)
     if (max == 0) return 0;
@@ -1354,15 +1369,22 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 // the map, SFF and DFF in LDS as well measured slower at config 4, 324 vs 295 us:
 // they are L1/L2 hits, and the staging delays every short-lived workgroup.)
 struct BatchCarve {
-    size_t dff, grid, bits, req, km, ws, total;  // per env
-    size_t shared;                               // per block: EPB env regions
+    size_t dff, rows, grid, bits, req, km, ws, total;  // per env
+    size_t shared;                                     // per block: EPB env regions
 };
+// Packed state rows (the 13-cell encoders of ffm_ac_core / ffm_actor_only on maps at most
+// 12 wide): per env two arrays of H + 4 words, the current and the next state, row x + 2
+// holding map row x's 2-bit states at bits 2 (y + 2) and the out-of-map value in the two
+// halo rows / columns on each side, so a key is five word reads and a few shifts.
+__host__ __device__ inline int batch_rows(int H, int W, bool DL) { return DL && W <= 12 ? H + 4 : 0; }
+
 // DL: the env's DFF is staged in LDS (small maps): the policy's reads, the
 // deposits and the stencil stay on chip; only the stencil's output goes to HBM.
-__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB, bool DL = false) {
+__host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB, bool DL = false, int RH = 0) {
     BatchCarve c;
     size_t o = 0;
     c.dff = o; o += DL ? align16((size_t)HW * 4) : 0;
+    c.rows = o; o += align16((size_t)RH * 2 * 4);
     c.grid = o; o += align16((size_t)HW * 2);
     c.bits = o; o += align16((size_t)((HW + 31) / 32) * 4);
     c.req = o; o += align16((size_t)A * D * 2);
@@ -1393,9 +1415,12 @@ void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LPE = BS / EPB;
     const int H = a.H, W = a.W, HW = a.HW, A = a.A;
-    const BatchCarve cv = batch_carve(HW, A, D, EPB, DL);
+    const int RH = batch_rows(H, W, DL);
+    const BatchCarve cv = batch_carve(HW, A, D, EPB, DL, RH);
     const int sub = threadIdx.x / LPE, tid = threadIdx.x % LPE;
     unsigned char* base = smem + (size_t)sub * cv.total;
+    uint32_t* crow = reinterpret_cast<uint32_t*>(base + cv.rows);   // current state rows (RH > 0)
+    uint32_t* nrow = crow + RH;                                     // next state rows
     uint16_t* grid = reinterpret_cast<uint16_t*>(base + cv.grid);
     uint32_t* bits = reinterpret_cast<uint32_t*>(base + cv.bits);
     uint16_t* req = reinterpret_cast<uint16_t*>(base + cv.req);
@@ -1410,6 +1435,10 @@ void learn_batch_kernel(LearnArgs a) {
     const bool vchain = a.v_chain && live && a.ep_steps[e] > 0;   // every V(s) was inserted as a V(s')
     constexpr bool UNI = VK == 1;
     const int variant = UNI ? (int)kVarUnified : a.variant;
+    // the 13-cell encoders read the packed rows (out of the map: 2 for ffm_ac_core, 0 for
+    // ffm_actor_only)
+    const bool rows = !UNI && RH > 0 && (variant == kVarAC || variant == kVarActorOnly);
+    const uint32_t oob = variant == kVarAC ? 2u : 0u;
     const bool actor = UNI || variant == kVarActorOnly || (variant == kVarUnified && a.mode != kModeCritic);
     const bool post_update = variant == kVarUnified && a.mode == kModeActor;
     const bool vdense = UNI || a.V.dense_by, hdense = UNI || a.Ht.dense_by;
@@ -1432,6 +1461,22 @@ void learn_batch_kernel(LearnArgs a) {
         for (int c = tid; c < HW; c += LPE) dff[c] = src[c];
     }
     for (int c = tid; c < (HW + 31) / 32; c += LPE) bits[c] = 0u;
+    if (rows)       // static rows: map classes (16 per map2 word), halo = the out-of-map value
+        for (int r = tid; r < RH; r += LPE) {
+            const uint32_t fill = oob * 0x55555555u;
+            uint32_t v = fill;
+            const int x = r - 2;
+            if (x >= 0 && x < H) {
+                const int c0 = x * W, w0 = c0 >> 4, sh = 2 * (c0 & 15);
+                const unsigned long long m = (unsigned long long)a.map2[w0] |
+                                             ((unsigned long long)(sh + 2 * W > 32 ? a.map2[w0 + 1] : 0u) << 32);
+                const uint32_t cls = (uint32_t)(m >> sh) & (uint32_t)((1ull << (2 * W)) - 1);
+                const uint32_t mid = (uint32_t)((1ull << (2 * W)) - 1) << 4;
+                v = (fill & ~mid) | (cls << 4);
+            }
+            crow[r] = v;
+            nrow[r] = v;
+        }
     for (int c = tid; c < A * D; c += LPE) req[c] = kNone16;
     if (D == 4)
         for (int c = tid; c < A; c += LPE) km[c] = 0u;
@@ -1477,6 +1522,10 @@ void learn_batch_kernel(LearnArgs a) {
         if (i < n) {
             grid[pj] = (uint16_t)((grid[pj] & ~kGIdx) | (uint32_t)i);
             if (RASTER) atomicOr(&bits[pj >> 5], 1u << (pj & 31));   // occupancy, for the raster pass
+            if (rows) {     // an agent's free cell (class 0) reads 1
+                const int x = fdiv(pj, a.mW);
+                atomicOr(&crow[x + 2], 1u << (2 * (pj - x * W + 2)));
+            }
         }
     }
     if (RASTER) {
@@ -1561,7 +1610,7 @@ void learn_batch_kernel(LearnArgs a) {
         if (KEYS) { skey[j] = 0; hsl[j] = -1; }
         if (tid + j * LPE >= n) continue;
         const int x = fdiv(BK_P(j), a.mW), y = BK_P(j) - x * W;
-        const unsigned long long sk = encode_v(a, variant, smc, x, y);
+        const unsigned long long sk = rows ? enc13_rows(crow, x, y, a.mBS) : encode_v(a, variant, smc, x, y);
         if (KEYS) skey[j] = sk;
         int coord[NA], valid[NA], inb[NA];
         int cls[NA];
@@ -1735,7 +1784,13 @@ void learn_batch_kernel(LearnArgs a) {
             for (int q = 0; q < BK_WINS(j); q++) v = v + 1.0f;
             *c = v;
         }
-        if ((grid[BK_NXT(j)] >> 14) != 3) atomicOr(&bits[BK_NXT(j) >> 5], 1u << (BK_NXT(j) & 31));
+        if ((grid[BK_NXT(j)] >> 14) != 3) {
+            atomicOr(&bits[BK_NXT(j) >> 5], 1u << (BK_NXT(j) & 31));
+            if (rows) {
+                const int x = fdiv(BK_NXT(j), a.mW);
+                atomicOr(&nrow[x + 2], 1u << (2 * (BK_NXT(j) - x * W + 2)));
+            }
+        }
     }
     __syncthreads();
     LSTAMP(3);
@@ -1757,7 +1812,7 @@ void learn_batch_kernel(LearnArgs a) {
                 skj = skey[j];
             } else {
                 const int px = fdiv(BK_P(j), a.mW);
-                skj = encode_v(a, variant, smc, px, BK_P(j) - px * W);
+                skj = rows ? enc13_rows(crow, px, BK_P(j) - px * W, a.mBS) : encode_v(a, variant, smc, px, BK_P(j) - px * W);
             }
             double r = a.step_penalty;
             if (BK_WEXIT(j)) r = r + a.exit_reward;
@@ -1767,7 +1822,7 @@ void learn_batch_kernel(LearnArgs a) {
             unsigned long long nk = 0;
             if (!BK_WEXIT(j)) {
                 const int nx = fdiv(BK_NXT(j), a.mW), ny = BK_NXT(j) - nx * W;
-                nk = encode_v(a, variant, smn, nx, ny);
+                nk = rows ? enc13_rows(nrow, nx, ny, a.mBS) : encode_v(a, variant, smn, nx, ny);
             }
             if (vdense) {
                 if (!BK_WEXIT(j)) {
@@ -4455,7 +4510,7 @@ hipError_t launch_batch_t(const LearnArgs& a0, hipStream_t s) {
     // the DFF lives in global memory (not DL) and the map is large: stencil apart (the
     // separate stencil kernels are Neumann's; Moore's stays fused)
     a.sep_stencil = NB == 4 && !DL && a.HW >= kSepStencilHW && (long long)((a.HW + 255) / 256) * a.E < (1ll << 31);
-    const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL).shared;
+    const size_t smem = batch_carve(a.HW, a.A, D, EPB, DL, batch_rows(a.H, a.W, DL)).shared;
     if (smem > 65536) {
         const hipError_t e = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&learn_batch_kernel<BS, EPB, APT, D, DL, VK, NB>),
