@@ -67,6 +67,10 @@
     do {         \
     } while (0)
 #endif
+#ifndef FFM_BLOCK_ABLATE
+#define FFM_BLOCK_ABLATE 0   // diagnostic builds only: bit k replaces / skips one phase of the block kernel
+#endif
+
 #ifndef FFM_ABLATE
 #define FFM_ABLATE 0   // diagnostic builds only (tools/ablate.sh): bit k skips one phase
 #endif
@@ -813,8 +817,10 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         } else {
             // the agent's draw block; its words z, w are the friction draw if it owns a
             // contested target (the resolve reads them instead of recomputing the block)
-            const uint4 pb = philox(make_uint4(a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i, kPurDecide << 28),
-                                    a.key0, a.key1);
+            const uint4 pb = (FFM_BLOCK_ABLATE & 1)   // diagnostic: a cheap hash instead of Philox
+                                 ? make_uint4((uint32_t)i * 0x9E3779B1u ^ a.t, (uint32_t)k * 0x85EBCA6Bu, (uint32_t)i, 7u)
+                                 : philox(make_uint4(a.t, (uint32_t)(a.env_base + e0 + k), (uint32_t)i, kPurDecide << 28),
+                                          a.key0, a.key1);
             reinterpret_cast<uint2*>(gbase + cv.u)[it] = make_uint2(pb.z, pb.w);
             if (F64) {
                 r = req_cell<NB, CT>(decide<NB, F64, GT>(pp, PW, grid + k * PHW, psff32, psff64, tile + k * PHW, 0, 0,
@@ -824,7 +830,8 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
                 // double conversion; the tile has the grid's layout: DWS = 0), the exact NumPy
                 // pass only when u lies within the margin of a cdf boundary (identical results)
                 bool to_exit = false;
-                uint32_t slot = lane_decide<NB, false, false, 0>(pp, PW, grid + k * PHW, psff32, tile + k * PHW, 0,
+                uint32_t slot = (FFM_BLOCK_ABLATE & 8) ? (uint32_t)NB   // diagnostic: everyone stays
+                                : lane_decide<NB, false, false, 0>(pp, PW, grid + k * PHW, psff32, tile + k * PHW, 0,
                                                                  a.kS32, a.kD32, pb.x, to_exit);
                 if (slot == kPending)
                     slot = NB == 4 ? lane_decide_exact<NB, false, 0>(pp, PW, grid + k * PHW, psff32, tile + k * PHW, 0,
@@ -899,6 +906,11 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
         const int pp = spos[it];
         if (r == pp) {
             dk[pp] += 1.0f;                                                           // :91-93 (stay)
+            continue;
+        }
+        if (FFM_BLOCK_ABLATE & 2) {   // diagnostic: no requester scan (every mover granted)
+            snxt[it] = (CT)r;
+            dk[pp] += 1.0f;
             continue;
         }
         uint16_t who[NB];
@@ -1004,6 +1016,9 @@ __global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
                 for (int j = -1; j <= 4; j++) b[dx + 1][j + 1] = (NB == 4 && dx != 0 && (j < 0 || j > 3)) ? 0.0f
                                                                   : c0 * p[dx * PW + j];
             float o[4];
+            if (FFM_BLOCK_ABLATE & 4) {   // diagnostic: no stencil arithmetic
+                o[0] = b[1][1]; o[1] = b[1][2]; o[2] = b[1][3]; o[3] = b[1][4];
+            } else
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 float acc = b[1][j + 1];
