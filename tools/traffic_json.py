@@ -68,7 +68,7 @@ if cfg in (4, 5):
                     with open(os.path.join(root, fn)) as fh:
                         for r in csv.DictReader(fh):
                             if r["Counter_Name"] == counter and "learn_" in r["Kernel_Name"]:
-                                name = r["Kernel_Name"].split("(")[0]
+                                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
                                 acc.setdefault(name, []).append(float(r["Counter_Value"]))
         return {k: sum(v[10:] or v) / len(v[10:] or v) for k, v in acc.items()}
     fb, wb = by_kernel(os.path.join(out, "fetch"), "FETCH_SIZE"), by_kernel(os.path.join(out, "write"), "WRITE_SIZE")
@@ -76,6 +76,16 @@ if cfg in (4, 5):
     res["per_kernel_bytes_per_launch"] = per
     res["note"] = ("per-kernel means include kernels that do not run every step (resets); "
                    "hbm_bytes_per_launch is learn_batch_kernel's")
+    # FETCH_SIZE counts random 64-B lines once and streams / 128-B lines half
+    # (profiles/r05/fetch_calibration.json): the batch kernel mixes both
+    lo = fk * 1024 + wk * 1024
+    res["hbm_bytes_per_launch_if_all_reads_random_64B"] = lo
+    res["traffic_over_algorithmic_range"] = [lo / alg, res["traffic_over_algorithmic"]]
+    res["calibration"] = ("profiles/r05/fetch_calibration.json (tools/fetchbench.hip, 2 GiB table, every line "
+                          "once): FETCH_SIZE = 0.5 x the bytes of 16-B/lane streaming reads and of random 128-B "
+                          "lines, 1.0 x the bytes of random 64-B lines, 64 B per random 8-B or 16-B read. This "
+                          "kernel mixes streamed bytes (x2) with random 64-B table lines (x1), so its traffic lies "
+                          "in traffic_over_algorithmic_range; hbm_bytes_per_launch keeps the x2 upper bound.")
 print(json.dumps(res, indent=1))
 with open(os.path.join(out, "traffic.json"), "w") as fh:
     json.dump(res, fh, indent=1)
