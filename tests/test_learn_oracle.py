@@ -170,6 +170,20 @@ def _batched(variant, mode, params, E, T, nthreads, N=16, max_steps=60):
     return pos, counts, dff, eps, tot, vk[ov], vv[ov], hk[oh], hv[oh]
 
 
+@pytest.mark.parametrize("variant,mode", [("ac", None), ("unified", "actor_only"), ("actor_only", None)])
+def test_batched_moore_semantics_independent_of_threads(variant, mode):
+    """The batched step with the Moore neighbourhood (nine moves, nine-value H rows, eight
+    ffm_actor_only decisions per agent): the same fixed-point sums whatever the threads."""
+    p = {"epsilon": 0.1, "block_size": 1, "neighborhood": "moore"} if variant != "ac" else {"neighborhood": "moore"}
+    a = _batched(variant, mode, p, 64, 70, 1)
+    b = _batched(variant, mode, p, 64, 70, 5)
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    assert a[3].sum() > 0
+    if variant != "ac":
+        assert np.asarray(a[8]).shape[1] == 9     # nine-value H rows
+
+
 @pytest.mark.parametrize("variant,mode", [("ac", None), ("unified", "critic_only"), ("unified", "actor_only"),
                                           ("unified", "both"), ("actor_only", None)])
 def test_batched_semantics_independent_of_threads(variant, mode):
