@@ -548,16 +548,24 @@ __host__ __device__ inline BlockCarve block_carve(int PHW, int A, int K, int F, 
     (void)f64;
     const size_t ix = big ? 4 : 2;
     const size_t misc = align16((size_t)(8 * K + 64) * 4);
-    c.grid = o; o += align16((size_t)K * PHW * 2);
+    // the DFF tile and the misc words live through the whole step; the grid and the agent
+    // arrays are dead once the exits are compacted, so the auto-reset's placement keys
+    // (used only after that) share their bytes -- 11 KB less LDS at C3, a fourth block per CU
     c.dff = o;  o += align16((size_t)K * PHW * 4);
+    c.misc = big ? 0 : o;
+    o += big ? 0 : misc;
+    const size_t dead = o;
+    c.grid = o; o += align16((size_t)K * PHW * 2);
     c.pos = o;  o += align16((size_t)K * A * ix);
     c.req = o;  o += align16((size_t)K * A * ix);
     c.nxt = o;  o += align16((size_t)K * A * ix);
-    c.misc = big ? 0 : o;
-    o += big ? 0 : misc;
     c.u = o;    o += align16((size_t)K * A * 8);   // MT: the pending draws; Philox: the friction words
     c.flag = o; o += mt ? align16((size_t)K * A * 2) : 0;
-    c.keys = o; o += reset ? align16((size_t)block_keys_cap(A, F) * 8) : 0;
+    c.keys = dead;
+    if (reset) {
+        const size_t kb = align16((size_t)block_keys_cap(A, F) * 8);
+        if (dead + kb > o) o = dead + kb;
+    }
     c.total = o;
     c.lds = big ? misc : o;
     return c;
@@ -699,8 +707,16 @@ __device__ __forceinline__ CT req_cell(uint32_t slot, int pp, int PW) {
            : slot == kPending ? ReqCodes<CT>::kWait : ReqCodes<CT>::kNone;
 }
 
+#ifndef FFM_BLOCK_WAVES
+#define FFM_BLOCK_WAVES 8   // Neumann float32: minimum waves per SIMD asked of the register allocator
+#endif
+
+// The Neumann float32 kernels fit 8 waves per SIMD (57 VGPRs, 78 SGPRs, no spills) and with
+// the placement keys sharing the dead arrays' LDS (block_carve) four 512-lane blocks fit a
+// CU: C3 137.3 -> 129.7 us.  Moore and float64 would spill under that bound: theirs stays 1.
 template <int NB, bool F64, bool MT, int BS, bool BIG>
-__global__ __launch_bounds__(BS) void core_block_kernel(CoreStepArgs a) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(NB == 4 && !F64 ? FFM_BLOCK_WAVES : 1, 8)))
+void core_block_kernel(CoreStepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     using GT = uint16_t;
     using CT = typename std::conditional<BIG, uint32_t, uint16_t>::type;

@@ -347,9 +347,6 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     }
     if (d.n_agents > (int)fl.size())
         return fail(FFM_E_INVALID, "Cannot take a larger sample than population when 'replace=False'");
-    // On-device placement sorts <= 16384 candidates in LDS (learn_reset_kernel).
-    if (d.rng_mode == FFM_RNG_PHILOX && d.n_agents > 12288 && (int)fl.size() > 16384)
-        return fail(FFM_E_UNSUPPORTED, "on-device placement supports n_agents <= 12288 on maps with > 16384 free cells");
 
     ffm_learner* l = new ffm_learner();
     l->d = d;
@@ -1005,8 +1002,6 @@ int ffm_learner_set_placement(ffm_learner* l, const uint16_t* cells, int32_t cou
         for (int i = 0; i < l->HW; i++)
             if (map[i] == 0) fl.push_back((uint16_t)i);
     }
-    if (!l->mt && (int)fl.size() > 16384 && n_agents > 12288)
-        return fail(FFM_E_UNSUPPORTED, "on-device placement supports n_agents <= 12288 above 16384 candidates");
     HIP_TRY(hipDeviceSynchronize());
     if (!fl.empty()) HIP_TRY(hipMemcpy(l->d_free_cells, fl.data(), fl.size() * 2, hipMemcpyHostToDevice));
     l->F = (int)fl.size();

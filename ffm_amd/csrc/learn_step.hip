@@ -4041,6 +4041,7 @@ __global__ __launch_bounds__(256) void learn_capture_kernel(LearnArgs a, TrajCap
 // chosen so that N <= expected count << capacity) are bitonic-sorted in LDS.
 constexpr int kResetBS = 256;
 constexpr int kResetCap = 16384;
+constexpr int kResetBin = 256;    // keys of one histogram bin (the exact-threshold fallback)
 
 __device__ __forceinline__ void reset_env(const LearnArgs& a, int all, long long e) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -4075,9 +4076,59 @@ __device__ __forceinline__ void reset_env(const LearnArgs& a, int all, long long
     }
     __syncthreads();
     int C = take_all ? F : cnt;
+    // fallback: the keys of the threshold bin, and how many of them the placement still takes
+    __shared__ unsigned long long sbk[kResetBin];
+    __shared__ int sbn;
+    int need = 0;
     if (C > kResetCap || C < N) {
-        if (tid == 0) atomicOr(a.overflow, 2);
-        C = C > kResetCap ? kResetCap : C;
+        // the sampled threshold kept too few or too many (N close to the capacity): the
+        // exact threshold from a histogram of the keys' top 12 bits -- bin b, the first whose
+        // cumulative count reaches N.  The keys of the bins below b (fewer than N) are sorted
+        // as usual; the N - (their count) smallest keys of bin b follow them, ranked apart
+        // (a bin holds ~F / 4096 <= 16 keys on average).  Block-uniform.
+        __shared__ int sb, sc;
+        uint32_t* hist = reinterpret_cast<uint32_t*>(smem);   // 4,096 bins over the key area
+        __syncthreads();
+        for (int i = tid; i < 4096; i += kResetBS) hist[i] = 0u;
+        __syncthreads();
+        for (int j = tid; j < F; j += kResetBS)
+            atomicAdd(&hist[philox(make_uint4(a.t, genv, (uint32_t)j, kPurReset << 28), a.key0, a.key1).x >> 20], 1u);
+        __syncthreads();
+        if (tid < 64) {         // one wave: 64 bins per lane, a lane scan, the crossing lane
+            int loc = 0;
+            for (int q = 0; q < 64; q++) loc += (int)hist[tid * 64 + q];
+            int incl = loc;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(incl, o);
+                if (tid >= o) incl += u;
+            }
+            if (N > 0 && incl >= N && incl - loc < N) {
+                int c = incl - loc, q = tid * 64;
+                while (c + (int)hist[q] < N) c += (int)hist[q++];
+                sb = q;
+                sc = c;
+            }
+            if (N == 0 && tid == 0) { sb = -1; sc = 0; }
+        }
+        __syncthreads();
+        const int bb = sb;
+        C = sc;                 // < N: fits the key area
+        need = N - C;
+        if (tid == 0) { cnt = 0; sbn = 0; }
+        __syncthreads();
+        for (int j = tid; j < F; j += kResetBS) {
+            const uint32_t k = philox(make_uint4(a.t, genv, (uint32_t)j, kPurReset << 28), a.key0, a.key1).x;
+            const unsigned long long kj = ((unsigned long long)k << 32) | (unsigned)j;
+            if ((int)(k >> 20) < bb) {
+                keys[atomicAdd(&cnt, 1)] = kj;
+            } else if ((int)(k >> 20) == bb) {
+                const int q = atomicAdd(&sbn, 1);
+                if (q < kResetBin) sbk[q] = kj;
+            }
+        }
+        __syncthreads();
+        if (tid == 0 && sbn > kResetBin) atomicOr(a.overflow, 2);   // a bin of > 256 keys: not seen at F <= 65,536
     }
     int P = 1;
     while (P < C) P <<= 1;
@@ -4095,8 +4146,18 @@ __device__ __forceinline__ void reset_env(const LearnArgs& a, int all, long long
             }
             __syncthreads();
         }
-    const int NN = N < C ? N : C;
+    int NN = N < C ? N : C;
     for (int r = tid; r < NN; r += kResetBS) a.pos[e * a.A + r] = a.free_cells[(int)(keys[r] & 0xFFFFFFFFu)];
+    if (need > 0) {             // the threshold bin's smallest keys, ranked among themselves
+        const int hb = sbn < kResetBin ? sbn : kResetBin;
+        for (int i = tid; i < hb; i += kResetBS) {
+            const unsigned long long ki = sbk[i];
+            int rank = 0;
+            for (int q = 0; q < hb; q++) rank += sbk[q] < ki ? 1 : 0;
+            if (rank < need) a.pos[e * a.A + NN + rank] = a.free_cells[(int)(ki & 0xFFFFFFFFu)];
+        }
+        NN += need < hb ? need : hb;
+    }
     float* d = a.dff_in + e * (long long)a.HW;
     for (int c = tid; c < a.HW; c += kResetBS) d[c] = 0.0f;
     if (tid == 0) {

@@ -243,6 +243,16 @@ def test_learner_philox_moore_matches_cpu(variant, mode):
                     env_base=77)
 
 
+def test_learner_philox_large_placement_matches_cpu():
+    """On-device placement of more agents than the sampled threshold holds (16,383 -- the
+    batched learner's agent capacity -- of the 21,904 free cells of a 150x150 room: the exact
+    histogram threshold of reset_env), then three tiled steps at sixteen agents per lane:
+    positions, DFF and tables equal the CPU restatement.  (A 256x256 env of this many
+    agents exceeds the batch kernel's LDS; its placement limit is the kernel's.)"""
+    _philox_compare("unified", "actor_only", {"epsilon": 0.1, "block_size": 1}, 150, 150, 16383, 2, 3,
+                    max_steps=20, seed=11, log2_cap=24)
+
+
 @pytest.mark.parametrize("mode", ["critic_only", "actor_only", "both"])
 def test_learner_philox_tiled_step_matches_cpu(mode):
     """The tiled step (ffm_unified at block size 1 on the raster batch kernel, DESIGN.md
