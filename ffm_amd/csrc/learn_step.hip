@@ -1409,8 +1409,13 @@ constexpr uint32_t kSaNewH = 1u << 15;
 // NB = 8: the Moore neighbourhood (model/ffm_unified.py:173-185, model/ffm_actor_only.py:
 // 87-93): nine moves, nine-value H rows, requesters of a target on its eight neighbours,
 // ffm_actor_only's eight decisions per agent (D = 8), the eight-neighbour stencil.
+#ifndef FFM_LBATCH_SMALL_WAVES
+#define FFM_LBATCH_SMALL_WAVES 1   // the same for the several-envs-per-workgroup shapes
+#endif
+
 template <int BS, int EPB, int APT, int D, bool DL, int VK = 0, int NB = 4>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(FFM_LBATCH_WAVES, 8)))
+__global__ __launch_bounds__(BS)
+__attribute__((amdgpu_waves_per_eu(EPB > 1 && NB == 4 ? FFM_LBATCH_SMALL_WAVES : FFM_LBATCH_WAVES, 8)))
 void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LPE = BS / EPB;
