@@ -2953,8 +2953,13 @@ __device__ __forceinline__ unsigned long long dense_key(uint32_t slot, int qsh, 
 }
 
 // V: visit-averaged TD(0) of every touched state (learn_apply_dense_kernel's update).
+#ifndef FFM_TILE_V_WAVES
+#define FFM_TILE_V_WAVES 1   // minimum waves per SIMD asked of the register allocator (V pass)
+#endif
+
 template <bool TM>
-__global__ __launch_bounds__(kTileThreads) void learn_tile_v_kernel(LearnArgs a) {
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(FFM_TILE_V_WAVES, 8)))
+void learn_tile_v_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
     __shared__ long long qs[NS];
     __shared__ uint32_t ks[NS];
