@@ -1409,13 +1409,16 @@ constexpr uint32_t kSaNewH = 1u << 15;
 // NB = 8: the Moore neighbourhood (model/ffm_unified.py:173-185, model/ffm_actor_only.py:
 // 87-93): nine moves, nine-value H rows, requesters of a target on its eight neighbours,
 // ffm_actor_only's eight decisions per agent (D = 8), the eight-neighbour stencil.
+// The several-envs-per-workgroup ffm_actor_only shapes (D = 4) are asked for 8 waves
+// per SIMD (64 VGPRs, 78 SGPRs, a few bytes of spill): 211.7 -> 204.6 us per config-4
+// step in A/B; the D = 1 variants lose 0.7 % at 8 (a 100 B spill) and keep the default.
 #ifndef FFM_LBATCH_SMALL_WAVES
-#define FFM_LBATCH_SMALL_WAVES 1   // the same for the several-envs-per-workgroup shapes
+#define FFM_LBATCH_SMALL_WAVES 8
 #endif
 
 template <int BS, int EPB, int APT, int D, bool DL, int VK = 0, int NB = 4>
 __global__ __launch_bounds__(BS)
-__attribute__((amdgpu_waves_per_eu(EPB > 1 && NB == 4 ? FFM_LBATCH_SMALL_WAVES : FFM_LBATCH_WAVES, 8)))
+__attribute__((amdgpu_waves_per_eu(EPB > 1 && NB == 4 && D == 4 ? FFM_LBATCH_SMALL_WAVES : FFM_LBATCH_WAVES, 8)))
 void learn_batch_kernel(LearnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LPE = BS / EPB;
@@ -2954,7 +2957,7 @@ __device__ __forceinline__ unsigned long long dense_key(uint32_t slot, int qsh, 
 
 // V: visit-averaged TD(0) of every touched state (learn_apply_dense_kernel's update).
 #ifndef FFM_TILE_V_WAVES
-#define FFM_TILE_V_WAVES 1   // minimum waves per SIMD asked of the register allocator (V pass)
+#define FFM_TILE_V_WAVES 8   // 106 -> 78 SGPRs, occupancy 7 -> 8: config-5 step 767 -> 764 us in A/B
 #endif
 
 template <bool TM>
