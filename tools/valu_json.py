@@ -39,6 +39,11 @@ res = {"config": f"{H}x{W}_A{A}_E{E}", "kernel": kern, "valu_issue_frac": frac,
                                   if "SQ_LDS_IDX_ACTIVE" in med else None),
        "counters": med,
        "formula": "SQ_ACTIVE_INST_VALU / (8 * SQ_BUSY_CYCLES), median per dispatch"}
+if frac > 0.97:
+    res["note"] = ("saturated: the SIMDs' vector pipes issue on (nearly) every cycle; SQ_INSTS_VALU x 4 "
+                   "clocks / 1024 SIMDs = %.0f clocks per SIMD against SQ_BUSY_CYCLES / 32 = %.0f, so a "
+                   "value at or just above 1 is counter skew, and the kernel is VALU-issue-bound"
+                   % (med["SQ_INSTS_VALU"] * 4 / 1024, med["SQ_BUSY_CYCLES"] / 32))
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                     f"valu_{H}x{W}_A{A}_E{E}.json")
 with open(path, "w") as f:
