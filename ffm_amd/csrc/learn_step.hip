@@ -3236,17 +3236,26 @@ __device__ __forceinline__ void tile_h_end(const LearnArgs& a, int t, TileHCtx& 
 // learn_tile_v_kernel) for learn_tile_h_wide_kernel.
 constexpr int kTilePairs = 256 * kTileCells * 5;
 
+#ifndef FFM_TILE_H_WAVES
+#define FFM_TILE_H_WAVES 1
+#endif
+
 template <bool TM>
-__global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a) {
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(FFM_TILE_H_WAVES, 8)))
+void learn_tile_h_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
+    static_assert(kTileList * 4 <= kTilePairs * 2, "the window's list fits the pair map");
     __shared__ long long hq[kTileList];             // per touched (slot, action) pair
-    __shared__ uint16_t pid[kTilePairs];            // pair -> index into hq (valid where pbit is set)
+    // pair -> index into hq (valid where pbit is set); until the records are loaded, the
+    // window's record list (tile_window) -- one region, 19 KB of LDS per workgroup
+    __shared__ uint32_t pidl[kTilePairs / 2];
+    uint16_t* const pid = reinterpret_cast<uint16_t*>(pidl);
+    uint32_t* const list = pidl;
     __shared__ uint32_t pbit[kTilePairs / 32];
     __shared__ uint32_t touched[NS / 32];
     __shared__ uint32_t newb[NS / 32];               // rows another rank's step inserted (kTileNewH)
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
-    __shared__ uint32_t list[kTileList];
     __shared__ int wsum[kTileWaves + 1];
     __shared__ uint32_t rs[kMaxOwners + 1], rb[kMaxOwners];
     __shared__ int npair;
@@ -3274,6 +3283,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_kernel(LearnArgs a)
 #pragma unroll
     for (int j = 0; j < kTileJ; j++)
         if (tid + j * kTileThreads < m) rc[j] = a.trecs[list[tid + j * kTileThreads]];
+    __syncthreads();                        // the list is read: its LDS becomes the pair map
     bool own[kTileJ], pown[kTileJ];
     int ix[kTileJ], pr[kTileJ];
     double hv[kTileJ][5], vn[kTileJ], vs[kTileJ];
