@@ -2985,8 +2985,9 @@ void learn_tile_v_kernel(LearnArgs a) {
     tile_of_launch<TM>(a, k, t);
     if (blockIdx.x == 0 && tid == 0) a.tcand[0] = 0;    // the H pass's queue of wide tiles
     if (k >= launch_tiles<TM>(a)) return;
+    // (tile_window / tile_records pass a barrier -- tm_spans', tile_ranges' -- before any
+    // use of these)
     for (int i = tid; i < NS; i += kTileThreads) { qs[i] = 0; ks[i] = 0u; }
-    __syncthreads();
     const uint32_t Q = (a.V.mask + 1u) >> 8;
     const int qsh = __builtin_ctz(Q), c0 = t * kTileCells;
     // the record's td (rec_target: the target, minus V(s) at step start, read before any
