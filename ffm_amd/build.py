@@ -34,8 +34,10 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=(), only=None) -> str:
     """Compile the library; `out`/`defines` make diagnostic variants (tools/ablate.sh).
+    `only` (with `out`): compile just those sources with the defines and link them with the
+    product build's objects of the others (diagnostic builds of one kernel file).
 
     Each source compiles to its own object in parallel (the kernels' translation
     units are independent), then hipcc links the shared library."""
@@ -57,8 +59,10 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
         subprocess.run(cmd, check=True, cwd=CSRC)
         return obj
 
+    todo = [src for src in SOURCES if only is None or src in only]
     with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
+        done = dict(zip(todo, ex.map(compile_one, todo)))
+    objs = [done.get(src) or os.path.join(LIB_PATH + ".obj", src + ".o") for src in SOURCES]
     tmp = target + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:

@@ -344,8 +344,10 @@ __device__ __forceinline__ uint32_t reset_threshold(int N, int F) {
     return t >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
-// n / d for n < 2^17 and d < 2^16 by one multiply-high: m = ceil(2^32 / d) (magic_div); the
-// rounding error n * (m - 2^32 / d) / 2^32 < 2^-15 stays below the 1 / d gap to the next integer.
+// n / d by one multiply-high, m = ceil(2^32 / d) (magic_div), exact whenever n * d < 2^32:
+// m = (2^32 + r) / d with r < d, so n * m / 2^32 = n / d + n * r / (d * 2^32), and the error
+// term n * r / (d * 2^32) < n * d / (d * 2^32) < 1 / d stays below the gap to the next integer.
+// (n < 2^17 alone is not enough: d = 65535, n = 131069 gives 2.)  Checked on the host.
 __device__ __forceinline__ int mdiv(int n, uint32_t m) { return (int)__umulhi((uint32_t)n, m); }
 
 // unpad with a runtime row width: the quotient by magic_div(PW)

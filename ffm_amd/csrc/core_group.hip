@@ -97,6 +97,17 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 #define FFM_GROUP_TAIL 1    // the stencil's partial last slot, one cell per lane
 #endif
 
+// Skeleton ladder (diagnostic builds only; results invalid, timing only; profiles/r06/c2/):
+//   0: the group loop streams the state in and stores it back unchanged (no prologue, no LDS)
+//   1: + the block prologue (map / SFF term / free list staging, tile clears, grid init)
+//   2: + the group staged in LDS and the DFF stencil (positions and counts stored back)
+//   3: + count prefix, mark, unmark, compaction and stores (every agent stays: no decide,
+//        no resolve)
+//   4: the product kernel
+#ifndef FFM_GROUP_LADDER
+#define FFM_GROUP_LADDER 4
+#endif
+
 #ifndef FFM_GROUP_WAVES
 #define FFM_GROUP_WAVES 1   // minimum waves per SIMD asked of the register allocator
 #endif
@@ -180,9 +191,11 @@ void core_group_kernel(CoreStepArgs a) {
             st.d[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, q < Q ? q * 16 : kOOB, 0, 0));
         }
     };
+    constexpr int LAD = FFM_GROUP_LADDER;
     GState cur;
     load(g < ngroups ? g : -1, cur);
 
+    if (LAD >= 1) {
     for (int i = threadIdx.x; i < PHW; i += 256) {
         const uint8_t mv = a.pmap[i];
         pmap[i] = mv;
@@ -200,6 +213,7 @@ void core_group_kernel(CoreStepArgs a) {
         for (int i = lane; i < PHW / 2; i += 64)
             reinterpret_cast<uint32_t*>(grid)[s * (PHW / 2) + i] = reinterpret_cast<const uint32_t*>(pmap16)[i];
     wave_sync();
+    }
 
     unsigned c_steps = 0, c_exits = 0, c_resets = 0;
     constexpr uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W, c < 2^16
@@ -207,11 +221,35 @@ void core_group_kernel(CoreStepArgs a) {
     for (int iter = 0; g < ngroups; g += wstride, iter++) {
         const long long e0 = (long long)g * G;
         const int nenv = (int)min((long long)G, E - e0);
+        if (LAD <= 2) {   // ladder rungs 0-2: positions and counts stored back unchanged
+            const __amdgpu_buffer_rsrc_t rq = pair_rsrc(a.pos + e0 * A, (nenv * A * 2 + 3) & ~3);
+            __builtin_amdgcn_raw_buffer_store_b32(cur.p0, rq, lane < PWORDS ? lane * 4 : kOOB, 0, 0);
+            if (PWORDS > 64)
+                __builtin_amdgcn_raw_buffer_store_b32(cur.p1, rq, 64 + lane < PWORDS ? 256 + lane * 4 : kOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32((unsigned)cur.c, pair_rsrc(a.cnt + e0, nenv * 4),
+                                                  lane < G ? lane * 4 : kOOB, 0, 0);
+            c_steps += (unsigned)A * (unsigned)nenv;
+        }
+        if (LAD <= 1) {   // rungs 0-1: the DFF stored back from registers
+            const __amdgpu_buffer_rsrc_t rq = pair_rsrc(a.dff + e0 * HW, nenv * HW * 4);
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                const int q = k * 64 + lane;
+                buf_st4(rq, q < Q ? q * 16 : kOOB, cur.d[k]);
+            }
+            GState nx;
+            load(g + wstride < ngroups ? g + wstride : -1, nx);
+            cur = nx;
+            continue;
+        }
 
         // ---- stage the group (prefetched by the previous iteration or the prologue) -------
 #pragma unroll
         for (int k = 0; k < NS; k++)
             if (toff[k] >= 0) *reinterpret_cast<float4*>(tile + toff[k]) = cur.d[k];
+        unsigned long long rsm = 0ull;   // envs re-placed at the end of this step
+        if (LAD == 2) wave_sync();       // ladder rung 2: the staged tile before the stencil reads it
+        if (LAD >= 3) {
         if (lane < PWORDS) posst32[lane] = cur.p0;
         if (PWORDS > 64 && 64 + lane < PWORDS) posst32[64 + lane] = cur.p1;
         int S[G + 1];   // exclusive prefix of the counts (wave-uniform)
@@ -253,7 +291,8 @@ void core_group_kernel(CoreStepArgs a) {
         // ---- decide (model/ffm_core.py:40-88) -------------------------------------------
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
-            if (c * 64 < T) {
+            if (LAD == 3) cr[c] = DirCodes::kNoDir;   // ladder: every agent stays, no request
+            if (LAD >= 4 && c * 64 < T) {
                 const uint32_t v = cs[c];
                 const int pp = cs_pp(v), al = cs_al(v), s = cs_s(v);
                 const bool live = cs_live(v);
@@ -297,7 +336,7 @@ void core_group_kernel(CoreStepArgs a) {
                 const bool req = slot <= (uint32_t)NB;
                 const bool moving = req && r != pp;
                 bool granted = req && !moving;   // a stay is always granted
-                {
+                if (LAD >= 4) {
                     const int rt = moving ? r : pp;
                     int m = 0, k = 0, o = 0x7F;
                     uint32_t zo = 0u;
@@ -373,7 +412,7 @@ void core_group_kernel(CoreStepArgs a) {
         }
         const int nk = (int)kp[Sh] - (int)kp[Sl];
         const bool rs = a.auto_reset && lane < nenv && nk == 0;
-        const unsigned long long rsm = __ballot(rs);
+        rsm = __ballot(rs);
         __builtin_amdgcn_raw_buffer_store_b32((unsigned)(rs ? a.N : nk), pair_rsrc(a.cnt + e0, nenv * 4),
                                               lane < G ? lane * 4 : kOOB, 0, 0);
         if (rsm) {   // wave-uniform, rare
@@ -381,6 +420,7 @@ void core_group_kernel(CoreStepArgs a) {
             if (a.episodes && rs) a.episodes[e0 + lane] += 1;
             if (lane == 0) pend[iter >> 2] |= (uint32_t)rsm << (8 * (iter & 3));
         }
+        }   // LAD >= 3
 
         // ---- next group's HBM loads, in flight across the stencil, the stores and the
         // next group's head ------------------------------------------------------------
@@ -444,7 +484,7 @@ void core_group_kernel(CoreStepArgs a) {
 
     // ---- deferred auto-reset placements ------------------------------
     wave_sync();
-    for (int w = 0; w < kGroupPendWords; w++) {
+    for (int w = 0; w < (LAD >= 1 ? kGroupPendWords : 0); w++) {   // ladder rung 0: pend never initialised
         uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend[w]);
         while (m) {
             const int bit = w * 32 + __builtin_ctz(m);

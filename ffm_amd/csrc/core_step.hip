@@ -1068,11 +1068,19 @@ void core_block_kernel(CoreStepArgs a) {
 // ===========================================================================
 // Reset every env (Philox placement, counts = N); DFF zeroed by the host.
 // ===========================================================================
-__global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
+// mask (device, [E] bytes; ffm_engine_reset_envs): only the envs with a nonzero byte are
+// re-placed, their DFF row zeroed and their position row cleared here (the whole-engine reset
+// clears every row by memset beforehand).
+__global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a, const uint8_t* mask) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     uint16_t* fl = reinterpret_cast<uint16_t*>(smem + align16((size_t)a.F * 8));
     const long long e = blockIdx.x;
+    if (mask) {
+        if (!mask[e]) return;   // workgroup-uniform
+        for (int i = threadIdx.x; i < a.HW; i += 64) a.dff[e * a.HW + i] = 0.0f;
+        for (int i = threadIdx.x; i < a.A; i += 64) a.pos[e * a.A + i] = 0xFFFFu;
+    }
     for (int i = threadIdx.x; i < a.F; i += 64) fl[i] = a.free_padded[i];
     wave_sync();
     wave_reset_env(a, (uint32_t)(a.env_base + e), keys, fl, a.pos + e * a.A, threadIdx.x);
@@ -1081,9 +1089,15 @@ __global__ __launch_bounds__(64) void core_reset_kernel(CoreStepArgs a) {
 
 // Reset every env of a map whose free list does not fit the wave reset's LDS
 // (big maps): one workgroup per env, keys in the env block's global scratch.
-__global__ __launch_bounds__(1024) void core_block_reset_kernel(CoreStepArgs a) {
+__global__ __launch_bounds__(1024) void core_block_reset_kernel(CoreStepArgs a, const uint8_t* mask) {
     __shared__ int swsum[16];
     const long long e = blockIdx.x;
+    if (mask) {   // as core_reset_kernel
+        if (!mask[e]) return;
+        for (int i = threadIdx.x; i < a.HW; i += 1024) a.dff[e * a.HW + i] = 0.0f;
+        for (int i = threadIdx.x; i < a.A; i += 1024) a.pos[e * a.A + i] = 0xFFFFu;
+        __syncthreads();
+    }
     const BlockCarve cv = block_carve((a.H + 2) * (a.W + 2), a.A, 1, a.F, false, false, true, true);
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(a.scratch + (size_t)e * a.scratch_stride + cv.keys);
     block_place_env<1024>(a, e, keys, block_keys_cap(a.A, a.F), swsum);
@@ -1196,15 +1210,15 @@ hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, i
     return mt ? launch_block_t<8, false, true>(a, block, s) : launch_block_t<8, false, false>(a, block, s);
 }
 
-hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s) {
-    core_block_reset_kernel<<<dim3((unsigned)a.E), dim3(1024), 0, s>>>(a);
+hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s, const uint8_t* mask) {
+    core_block_reset_kernel<<<dim3((unsigned)a.E), dim3(1024), 0, s>>>(a, mask);
     return hipGetLastError();
 }
 
-hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s) {
+hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s, const uint8_t* mask) {
     const size_t smem = align16((size_t)(a.F > 0 ? a.F : 1) * 8) + align16((size_t)(a.N > 0 ? a.N : 1) * 2) +
                         align16((size_t)(a.F > 0 ? a.F : 1) * 2);
-    core_reset_kernel<<<dim3((unsigned)a.E), dim3(64), smem, s>>>(a);
+    core_reset_kernel<<<dim3((unsigned)a.E), dim3(64), smem, s>>>(a, mask);
     return hipGetLastError();
 }
 

@@ -122,6 +122,9 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     // border, so up to 65,536 cells (256 x 256) every stored cell is < 0xFFFF.
     if (d.H < 3 || d.W < 3 || (long long)d.H * d.W > 65536)
         return fail(FFM_E_INVALID, "map must be at least 3x3 and at most 65536 cells");
+    // the kernels divide padded cell indices (< (H + 2)(W + 2)) by W and W + 2 by multiply-high
+    if (!ffm::magic_div_ok((uint64_t)(d.H + 2) * (d.W + 2), (uint32_t)d.W + 2u))
+        return fail(FFM_E_INVALID, "map too large for the kernels' magic divisors");
     if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
     if (d.neighborhood != 4 && d.neighborhood != 8) return fail(FFM_E_INVALID, "neighborhood must be 4 or 8");
     if (d.sff_dtype != FFM_SFF_F32 && d.sff_dtype != FFM_SFF_F64) return fail(FFM_E_INVALID, "sff_dtype");
@@ -426,6 +429,23 @@ int ffm_engine_reset(ffm_engine* e, void* stream) {
     }
     e->t++;
     if (e->cap.n_sel) HIP_TRY(ffm::launch_core_capture_init(make_args(e), e->cap, s));
+    return FFM_OK;
+}
+
+int ffm_engine_reset_envs(ffm_engine* e, const uint8_t* mask, void* stream) {
+    if (!e || !mask) return fail(FFM_E_INVALID, "null engine or mask");
+    if (e->mt) return fail(FFM_E_UNSUPPORTED, "reset_envs: MT mode places agents on the host (set_state)");
+    hipStream_t s = (hipStream_t)stream;
+    // the masked envs only: Philox placement keyed by the current t (as ffm_engine_reset),
+    // DFF row zeroed, count = N; the episode counters are left alone (not an episode end)
+    if (e->block_reset) {
+        ffm::CoreStepArgs a = make_args(e);
+        a.scratch = e->d_scratch;
+        HIP_TRY(ffm::launch_core_block_reset(a, s, mask));
+    } else {
+        HIP_TRY(ffm::launch_core_reset(make_args(e), s, mask));
+    }
+    e->t++;
     return FFM_OK;
 }
 

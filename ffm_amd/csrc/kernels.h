@@ -6,8 +6,12 @@
 
 namespace ffm {
 
-// ceil(2^32 / d): n / d == mulhi(n, magic_div(d)) for n < 2^17, d < 2^16 (core_common.h mdiv)
+// ceil(2^32 / d): n / d == mulhi(n, magic_div(d)) whenever n * d < 2^32 (core_common.h mdiv).
+// Callers check it on the host (magic_div_ok): the engine's padded cell indices, and the
+// learner's cell indices and coordinates, all stay below it for maps of <= 65,536 cells.
 __host__ __device__ inline uint32_t magic_div(uint32_t d) { return (uint32_t)((0x100000000ull + d - 1) / d); }
+// every n < n_end divides exactly by magic_div(d)
+__host__ __device__ inline bool magic_div_ok(uint64_t n_end, uint32_t d) { return n_end * (uint64_t)d <= 0x100000000ull; }
 
 struct CoreStepArgs {
     int H, W, HW;          // map shape
@@ -70,9 +74,9 @@ size_t core_multi_smem_bytes(int H, int W, int F, int waves);
 hipError_t launch_core_multi(const CoreStepArgs& a, int nb, int nsteps, int blocks, hipStream_t s);
 int core_multi_blocks_per_cu(const CoreStepArgs& a, int nb);
 hipError_t launch_core_block(const CoreStepArgs& a, int nb, bool f64, bool mt, int block, hipStream_t s);
-hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s);
+hipError_t launch_core_reset(const CoreStepArgs& a, hipStream_t s, const uint8_t* mask = nullptr);
 size_t core_big_scratch_bytes(int H, int W, int A, int F, bool mt);
-hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s);
+hipError_t launch_core_block_reset(const CoreStepArgs& a, hipStream_t s, const uint8_t* mask = nullptr);
 hipError_t launch_update_dff(const float* src, float* dst, long long E, int H, int W, int nb, float c0,
                              float c1, hipStream_t s);
 hipError_t launch_core_capture_init(const CoreStepArgs& a, const CoreCapture& c, hipStream_t s);

@@ -320,6 +320,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     // last one a wall (the border must be walls anyway).
     if (d.H < 3 || d.W < 3 || (long long)d.H * d.W > 65536)
         return fail(FFM_E_INVALID, "map must be at least 3x3 and at most 65536 cells");
+    // cell indices (< H W) are divided by W by multiply-high (LearnArgs::mW)
+    if ((uint64_t)d.H * d.W * (uint64_t)d.W > 0x100000000ull)
+        return fail(FFM_E_INVALID, "map too large for the kernels' magic divisors");
     if (!d.map || !d.sff) return fail(FFM_E_INVALID, "map and sff are required");
     if ((long long)d.H * d.W == 65536 && (d.map[65535] == 0 || d.map[65535] == 3))
         return fail(FFM_E_UNSUPPORTED, "the last cell of a 65536-cell map must be blocked");
@@ -527,6 +530,15 @@ int ffm_learner_reset(ffm_learner* l, void* stream) {
     HIP_TRY(ffm::launch_learn_reset(make_args(l), true, s));
     l->t++;
     return check_overflow(l, s);
+}
+
+int ffm_learner_reset_envs(ffm_learner* l, const uint8_t* mask, void* stream) {
+    if (!l || !mask) return fail(FFM_E_INVALID, "null learner or mask");
+    if (l->mt) return fail(FFM_E_UNSUPPORTED, "reset_envs: MT mode places agents on the host (set_state)");
+    if (l->phase != 0) return fail(FFM_E_INVALID, "reset_envs inside a phased step");
+    HIP_TRY(ffm::launch_learn_reset_mask(make_args(l), mask, (hipStream_t)stream));
+    l->t++;
+    return FFM_OK;
 }
 
 // The batched step in phases (multi-rank runs exchange the table deltas between

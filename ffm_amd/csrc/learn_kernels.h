@@ -233,7 +233,8 @@ hipError_t launch_learn_v_scatter(const LearnTable& T, const uint32_t* slots, co
 hipError_t launch_learn_h_deltas(const LearnTable& T, const uint32_t* keys, const long long* q, long long stride,
                                  const long long* counts, int ranks, int self, int* overflow, hipStream_t s);
 hipError_t launch_learn_tsum_unpack(const LearnArgs& a, const double* tsum, long long stride, hipStream_t s);
-hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s);
+hipError_t launch_learn_reset(const LearnArgs& a, int all, hipStream_t s);   // all: 0 ended envs, 1 every env
+hipError_t launch_learn_reset_mask(const LearnArgs& a, const uint8_t* mask, hipStream_t s);   // the masked envs
 hipError_t launch_learn_fill_default(const LearnArgs& a, hipStream_t s);
 hipError_t launch_learn_capture(const LearnArgs& a, const TrajCapture& c, hipStream_t s);
 hipError_t launch_learn_clear(const LearnTable& T, int width, double dflt, hipStream_t s);

@@ -4082,7 +4082,7 @@ __device__ __forceinline__ void reset_env(const LearnArgs& a, int all, long long
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     __shared__ int cnt;
-    if (!all && !a.done[e]) return;
+    if (all != 1 && !a.done[e]) return;   // all: 0 the step's ended envs, 1 every env, 2 a mask in done
     const int tid = threadIdx.x, F = a.F;
     // episode quota (ffm_learner_set_episode_caps): an env past it stays empty; the episode
     // that reaches it ends with no re-placement (logged and counted like any other)
@@ -4310,7 +4310,7 @@ template <bool WAVE>
 __device__ __forceinline__ void reset_small_wave(const LearnArgs& a, int all, long long e0, unsigned long long* keys) {
     const int lane = (int)(threadIdx.x & 63);
     const long long me = e0 + lane;
-    bool want = lane < kResetSmallEnvs && me < a.E && (all || a.done[me]);
+    bool want = lane < kResetSmallEnvs && me < a.E && (all == 1 || a.done[me]);
     if (want && a.ep_cap && !all && a.episodes[me] >= a.ep_cap[me]) {   // past its quota: stays empty
         a.done[me] = 0;
         want = false;
@@ -4927,10 +4927,22 @@ hipError_t launch_learn_post(const LearnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
+// a reset_envs mask (bytes) into the done flags the reset kernels select by
+__global__ __launch_bounds__(256) void learn_mask_done_kernel(const uint8_t* mask, int* done, long long E) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e < E) done[e] = mask[e] ? 1 : 0;
+}
+
+hipError_t launch_learn_reset_mask(const LearnArgs& a, const uint8_t* mask, hipStream_t s) {
+    learn_mask_done_kernel<<<dim3((unsigned)((a.E + 255) / 256)), dim3(256), 0, s>>>(mask, a.done, a.E);
+    const hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : launch_learn_reset(a, 2, s);
+}
+
+hipError_t launch_learn_reset(const LearnArgs& a, int all, hipStream_t s) {
     if (a.F <= kResetSmallF && a.N <= a.F) {
         learn_reset_small_kernel<<<dim3((unsigned)((a.E + kResetSmallEnvs - 1) / kResetSmallEnvs)), dim3(64), 0, s>>>(
-            a, all ? 1 : 0);
+            a, all);
         return hipGetLastError();
     }
     int P = 1;
@@ -4941,7 +4953,7 @@ hipError_t launch_learn_reset(const LearnArgs& a, bool all, hipStream_t s) {
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    learn_reset_kernel<<<dim3((unsigned)a.E), dim3(kResetBS), smem, s>>>(a, all ? 1 : 0);
+    learn_reset_kernel<<<dim3((unsigned)a.E), dim3(kResetBS), smem, s>>>(a, all);
     return hipGetLastError();
 }
 

@@ -90,6 +90,8 @@ class OwnerCaps:
     below what any observed step needed; a count past its capacity is an error reported at the
     next sync point (never a silent drop).  `fixed` = (records, v, h) disables the adaptation."""
 
+    exact_floor = 1 << 16    # records: 1 MB per destination block
+
     def __init__(self, world: int, e_max: int, agents: int, n_tiles: int, fixed=None, headroom=(1.25, 1.5, 1.5),
                  adapt_every: int = 8, lag: int = 4, granule: int = 4096):
         # records per destination move slowly (agents are conserved, the rows dealt round-robin);
@@ -97,15 +99,30 @@ class OwnerCaps:
         self.world, self.granule = int(world), int(granule)
         self.headroom = tuple(float(h) for h in headroom) if isinstance(headroom, (tuple, list)) else (float(headroom),) * 3
         self.adapt_every, self.lag = int(adapt_every), int(lag)
-        self.rmax = max(1, int(e_max) * int(agents))        # one rank's records, all to one destination
+        self.e_max = int(e_max)
         ntk = max(owner_tiles(int(n_tiles), self.world, q) for q in range(self.world))
         self.vmax = max(1, ntk * 1024)                       # slots one rank owns
         self.hmax = 5 * self.vmax
         self.adaptive = fixed is None
         if fixed is not None:
+            self.rmax = max(1, self.e_max * int(agents))
+            self.rfloor = 0
             self.caps = tuple(int(x) for x in fixed)
         else:
-            r0 = min(self.rmax, self._round(2.0 * self.rmax / self.world))
+            self.reconfigure(agents)
+
+    def reconfigure(self, agents: int):
+        """A new configuration (agent count or placement region) starts: restart the adaptation
+        from the shape bounds of `agents` agents per env.  The counts observed under the old
+        configuration say nothing about the new one (a radius-3 crowd lands on one owner's rows,
+        a full room spreads over all), so they are dropped rather than scaled.  The record
+        capacity never falls below `exact_floor` records: up to that size it is the exact bound
+        (every record of this rank to one destination), so small configurations cannot
+        overflow however their crowd is dealt.  Every rank calls it at the same step."""
+        self.rmax = max(1, self.e_max * int(agents))         # one rank's records, all to one destination
+        self.rfloor = min(self.rmax, self.exact_floor)
+        if self.adaptive:
+            r0 = min(self.rmax, max(self.rfloor, self._round(2.0 * self.rmax / self.world)))
             v0 = min(self.vmax, self.world * r0)
             self.caps = (r0, v0, min(self.hmax, 5 * v0))
         self.max_seen = [0, 0, 0]
@@ -150,7 +167,7 @@ class OwnerCaps:
                 if h is not None:
                     self.max_seen[i] = max(self.max_seen[i], int(h.max()))
         hr, hv, hh = self.headroom
-        new = (min(self.rmax, self._round(hr * self.max_seen[0])),
+        new = (min(self.rmax, max(self.rfloor, self._round(hr * self.max_seen[0]))),
                min(self.vmax, self._round(hv * self.max_seen[1])),
                min(self.hmax, self._round(hh * max(self.max_seen[2], 1))))
         changed = new != self.caps
@@ -331,6 +348,20 @@ class TableSync:
             self.caps[w] = min(self.max_capacity, -(-int(self.caps[w] * factor) // 4096) * 4096)
             self.max_count[w] = max(self.max_count[w], int(self.caps[w] / self.headroom))
         self.capacity = max(self.caps.values())
+
+    def reconfigure(self, agents: int, prev_agents: int | None = None):
+        """A driver starts a new configuration of `agents` agents per env (a curriculum's next
+        (radius, N), a per-N driver's next N).  Owner mode restarts its capacities from the
+        new shape bounds (OwnerCaps.reconfigure); the hashed record exchange scales its
+        capacity up front when N grows (`rescale`).  Collective in effect: every rank calls it
+        with the same arguments at the same step (no communication of its own)."""
+        if self.owner:
+            if self.ocaps.adaptive:
+                self.ocaps.reconfigure(agents)
+                self.ocaps.apply([self.shard])
+            return
+        if prev_agents:
+            self.rescale(agents / prev_agents)
 
     def _exchange_dense(self, which: str):
         acc, present = self.shard.dense_buffers(which)

@@ -24,12 +24,12 @@ SFF_F32, SFF_F64 = 0, 1
 
 EXPORTED = [
     "ffm_last_error", "ffm_abi_version", "ffm_engine_create", "ffm_engine_destroy",
-    "ffm_engine_reset", "ffm_engine_step", "ffm_engine_update_dff", "ffm_engine_set_state",
+    "ffm_engine_reset", "ffm_engine_reset_envs", "ffm_engine_step", "ffm_engine_update_dff", "ffm_engine_set_state",
     "ffm_engine_get_state", "ffm_engine_set_mt_state", "ffm_engine_get_mt_state",
     "ffm_engine_get_counters", "ffm_engine_device_buffers", "ffm_engine_get_step_index",
     "ffm_engine_set_step_index", "ffm_engine_set_fused_steps", "ffm_np_expf_device",
     "ffm_engine_set_trajectory_capture", "ffm_engine_drain_trajectory",
-    "ffm_learner_create", "ffm_learner_destroy", "ffm_learner_reset", "ffm_learner_step",
+    "ffm_learner_create", "ffm_learner_destroy", "ffm_learner_reset", "ffm_learner_reset_envs", "ffm_learner_step",
     "ffm_learner_set_state", "ffm_learner_get_state", "ffm_learner_get_episodes",
     "ffm_learner_set_mt_state", "ffm_learner_get_mt_state", "ffm_learner_get_counters",
     "ffm_learner_set_epsilon", "ffm_learner_set_v_default", "ffm_learner_table_size",
@@ -118,6 +118,7 @@ def load_library():
     L.ffm_engine_create.argtypes = [C.POINTER(EngineDesc), C.POINTER(P)]
     L.ffm_engine_destroy.argtypes = [P]
     L.ffm_engine_reset.argtypes = [P, P]
+    L.ffm_engine_reset_envs.argtypes = [P, P, P]
     L.ffm_engine_step.argtypes = [P, i32, P]
     L.ffm_engine_update_dff.argtypes = [P, P]
     L.ffm_engine_set_state.argtypes = [P, i64, i64, P, P, P, P]
@@ -135,6 +136,7 @@ def load_library():
     L.ffm_learner_create.argtypes = [C.POINTER(EngineDesc), C.POINTER(LearnDesc), C.POINTER(P)]
     L.ffm_learner_destroy.argtypes = [P]
     L.ffm_learner_reset.argtypes = [P, P]
+    L.ffm_learner_reset_envs.argtypes = [P, P, P]
     L.ffm_learner_step.argtypes = [P, i32, P]
     L.ffm_learner_set_state.argtypes = [P, i64, i64, P, P, P, P]
     L.ffm_learner_get_state.argtypes = [P, i64, i64, P, P, P, P]
@@ -214,6 +216,17 @@ def _stream_handle(stream):
     return int(getattr(stream, "cuda_stream"))
 
 
+def _device_mask(mask, n: int, device: int):
+    """reset_envs' mask as n bytes on the device (a torch CUDA tensor is used in place)."""
+    import torch
+    dev = torch.device("cuda", device)
+    m = mask if isinstance(mask, torch.Tensor) else torch.as_tensor(np.asarray(mask))
+    if m.numel() != n:
+        raise ValueError(f"mask must have n_envs = {n} entries, got {m.numel()}")
+    m = m.reshape(-1).to(device=dev)
+    return (m != 0).to(torch.uint8).contiguous() if m.dtype != torch.uint8 else m.contiguous()
+
+
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
@@ -282,6 +295,7 @@ class Engine:
         d.env_base = int(env_base)
         d.device = int(device)
         d.envs_per_block = int(envs_per_block)
+        self.device = int(device)
         h = C.c_void_p()
         _check(L.ffm_engine_create(C.byref(d), C.byref(h)))
         self._h = h
@@ -308,6 +322,14 @@ class Engine:
     # -- the hot path ------------------------------------------------------
     def reset(self, stream=None):
         _check(self._L.ffm_engine_reset(self._h, _stream_handle(stream)))
+
+    def reset_envs(self, mask, stream=None):
+        """reset(env_mask): re-place only the envs with a nonzero mask entry (n_envs entries:
+        a torch CUDA tensor on the engine's device is read in place, anything else is
+        uploaded).  See ffm_engine_reset_envs."""
+        m = _device_mask(mask, self.n_envs, self.device)
+        _check(self._L.ffm_engine_reset_envs(self._h, C.c_void_p(m.data_ptr()), _stream_handle(stream)))
+        self._mask_keep = m      # alive until the next call: the launch reads it asynchronously
 
     def step(self, n_steps: int = 1, stream=None):
         _check(self._L.ffm_engine_step(self._h, int(n_steps), _stream_handle(stream)))
@@ -572,6 +594,12 @@ class Learner:
     # -- stepping ------------------------------------------------------------------
     def reset(self, stream=None):
         _check(self._L.ffm_learner_reset(self._h, _stream_handle(stream)))
+
+    def reset_envs(self, mask, stream=None):
+        """reset(env_mask) of the batched learner: the masked envs only (ffm_learner_reset_envs)."""
+        m = _device_mask(mask, self.n_envs, self.device)
+        _check(self._L.ffm_learner_reset_envs(self._h, C.c_void_p(m.data_ptr()), _stream_handle(stream)))
+        self._mask_keep = m
 
     def step(self, n_steps: int = 1, stream=None):
         _check(self._L.ffm_learner_step(self._h, int(n_steps), _stream_handle(stream)))

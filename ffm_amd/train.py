@@ -128,6 +128,7 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
     rows, configs = [], []
     episode_num = 0
     n_traj = 0
+    prev_n = None
     t_start = time.time()
     tsel, tph = (trajectory_selection(E, per_env, trajectory_every, env_base) if trajectory_every > 0
                  else (np.zeros(0, np.int32), None))
@@ -141,6 +142,9 @@ def run_curriculum(learner: Learner, exit_pos, radius_list, n_list, episodes_per
         for N in n_list:
             if N > avail:                                # run_unified_critic_training.py:190-197
                 continue
+            if g.sync is not None:                       # the exchange sizes follow the configuration
+                g.sync.reconfigure(N, prev_n)
+            prev_n = N
             if radius is None:
                 L.set_placement(None, n_agents=N)        # every free cell: the full-room reset
             else:
@@ -311,9 +315,14 @@ class _Group:
             self.sync.flush()
 
     def table_size(self, L, which: str) -> int:
-        """The table's size on every rank: a sharded learner's key sets are merged first
-        (TableSync.flush: the owner exchange keeps V's key set lazily).  Collective."""
-        self.flush()
+        """The table's size on every rank.  The owner exchange keeps H's key set exact every
+        step and V's lazily, so only V's presence is merged first (collective: every rank
+        calls it together).  The other exchanges insert every rank's keys at each sync step;
+        with a sync period K > 1 the size between sync steps is that of the last one -- a
+        flush here would apply the pending increments early and change the apply schedule
+        (and so the learned values) against a single device with the same K."""
+        if self.sync is not None and which == "V" and getattr(self.sync, "owner", False):
+            self.sync.sync_presence()
         return L.table_size(which)
 
 
@@ -378,8 +387,8 @@ def run_per_n(learner: Learner, n_list, episodes_per_n: int, eps=None, out_dir: 
     L.set_episode_caps(caps)
     prev_n = None
     for pi, N in enumerate(n_list):
-        if g.sync is not None and prev_n:
-            g.sync.rescale(N / prev_n)                     # the touched records grow with N
+        if g.sync is not None:
+            g.sync.reconfigure(N, prev_n)                  # the touched records grow with N
         prev_n = N
         L.set_placement(None, n_agents=N)                  # every free cell: the full-room reset
         base = pi * P                                      # run episodes before this pattern

@@ -116,6 +116,15 @@ int ffm_engine_destroy(ffm_engine* eng);
  * draws the placement from its own generator (initialize_agents) and uploads it. */
 int ffm_engine_reset(ffm_engine* eng, void* stream);
 
+/* Re-place the envs whose byte in `mask` is nonzero (reset(env_mask); the
+ * reference's drivers reset one model per episode: run_unified_actor_training.py:263 ->
+ * model/ffm_unified.py:800-812 reset()).  `mask` is a DEVICE pointer to n_envs bytes on the
+ * engine's device, read on `stream`.  Philox only: the masked envs get the placement
+ * ffm_engine_reset would give them (keyed by the step counter, which then advances), a zero
+ * DFF and count n_agents; the other envs are untouched.  Episode counters are not changed
+ * (an abandoned episode is not a completed one).  MT mode: FFM_E_UNSUPPORTED. */
+int ffm_engine_reset_envs(ffm_engine* eng, const uint8_t* mask, void* stream);
+
 /* Advance every env by n_steps steps (model/ffm_core.py:36-104 each). */
 int ffm_engine_step(ffm_engine* eng, int32_t n_steps, void* stream);
 
@@ -228,6 +237,14 @@ int ffm_learner_destroy(ffm_learner* l);
  * zero the DFF and the per-env episode counters.  MT: zero the DFF and counts only (the caller uploads
  * positions drawn from its own generators, like ffm_engine_reset). */
 int ffm_learner_reset(ffm_learner* l, void* stream);
+/* reset(env_mask) of the batched learner (model/ffm_unified.py:800-812 per env; the drivers'
+ * per-episode reset, run_unified_actor_training.py:263): the envs whose byte in the DEVICE
+ * array `mask` (n_envs bytes) is nonzero are re-placed as ffm_learner_reset places them
+ * (Philox keyed by the step counter, which then advances; an env past its episode quota
+ * stays empty), their DFF zeroed and their episode step count cleared.  Not an episode end:
+ * nothing is logged or counted, and the tables are untouched.  Between steps only; MT mode:
+ * FFM_E_UNSUPPORTED. */
+int ffm_learner_reset_envs(ffm_learner* l, const uint8_t* mask, void* stream);
 /* Asynchronous: returns once the steps are queued on `stream`.  A hashed V / H
  * table that passes 7/8 load drops the updates that would insert (the step goes
  * on); that condition (FFM_E_NOMEM) is reported exactly at the next sync point

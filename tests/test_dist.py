@@ -168,3 +168,24 @@ def test_gloo_world2_flush_mid_period_keeps_ranks_in_step(variant, mode, tmp_pat
     for k, v in mid.items():
         for r in (0, 1):
             assert np.array_equal(got[f"mid{r}_{k}"], v), f"rank {r} {k} after the flush"
+
+
+def test_owner_caps_reconfigure_restarts_from_shape_bounds():
+    """OwnerCaps (the owner-sharded exchange's fixed sizes): a new configuration drops the old
+    configuration's observations and restarts from the new shape bounds; a record capacity
+    below the exact floor is the exact bound (every record to one destination), so a small
+    radius curriculum whose crowd lands on one owner cannot overflow."""
+    import torch
+    from ffm_amd.dist import OwnerCaps
+    E, world, nt = 64, 8, 16384
+    oc = OwnerCaps(world, E, 10, nt, adapt_every=2, lag=1)
+    assert oc.caps[0] == E * 10                        # N = 10: the exact bound (640 records)
+    for _ in range(4):                                 # observed: every record to one owner
+        rc = torch.full((world, world), 0, dtype=torch.int64)
+        rc[0, 0] = E * 10
+        oc.observe(rc, torch.tensor([5000]), torch.tensor([9000]))
+    assert oc.caps[0] == E * 10                        # never below the exact floor
+    oc.reconfigure(90)                                 # the curriculum's next N: 9x the agents
+    assert oc.caps[0] == E * 90 and oc.max_seen == [0, 0, 0] and oc.seen == []
+    big = OwnerCaps(world, 512, 8192, nt)              # C5: the floor is 65,536 records
+    assert big.rfloor == OwnerCaps.exact_floor and big.caps[0] == 2 * 512 * 8192 // world

@@ -133,7 +133,10 @@ def _random_rank_table(H, W, bs, seed=0, frac=0.6, width=5):
 
 
 def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
-                    nthreads=16, sff_dtype=np.float32, log2_cap=22, chunks=1):
+                    nthreads=16, sff_dtype=np.float32, log2_cap=22, chunks=1, reset_at=None):
+    """reset_at = (T1, fraction): after T1 steps a random fraction of the envs is re-placed
+    through Learner.reset_envs (the CPU side: reset_philox at step index T1 + 1), then the
+    remaining T - T1 steps run."""
     from ffm_amd.data import make_room, l1_sff
     from oracle import learn as LO
     from oracle import oracle as O
@@ -161,12 +164,26 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     assert np.array_equal(gc, counts)
     assert np.array_equal(gp[:, :N], pos[:, :N]), "reset placement"
     tot = 0
-    for t in range(1, T + 1):
+    T1 = T if reset_at is None else int(reset_at[0])
+    for t in range(1, T1 + 1):
         tot += cpu.step_philox_batch(pos, counts, dff, eps, ep_steps, seed, t, True, N, max_steps, env_base,
                                      nthreads)
         if chunks > 1 and t % (T // chunks) == 0:
             print(f"  cpu step {t}/{T}", flush=True)   # progress of a long comparison
-    L.step(T)
+    L.step(T1)
+    if reset_at is not None:
+        import torch
+        mask = np.random.default_rng(T1).random(E) < float(reset_at[1])
+        L.reset_envs(torch.as_tensor(mask.astype(np.uint8)).cuda())
+        for e in np.flatnonzero(mask):
+            pos[e] = 0xFFFF
+            pos[e, :N] = core.reset_philox(N, seed, T1 + 1, env_base + e)
+            counts[e], ep_steps[e] = N, 0
+            dff[e] = 0.0
+        for t in range(T1 + 2, T + 2):
+            tot += cpu.step_philox_batch(pos, counts, dff, eps, ep_steps, seed, t, True, N, max_steps, env_base,
+                                         nthreads)
+        L.step(T - T1)
     gp, gc, gd = L.get_state()
     geps, gst = L.episodes()
     assert np.array_equal(gc, counts), "counts"
@@ -191,6 +208,18 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     assert c["steps"] == T
     L.close()
     return counts, eps
+
+
+@pytest.mark.parametrize("variant,mode,params,H,N,E", [
+    ("actor_only", None, {"epsilon": 0.2}, 12, 32, 4096),
+    ("unified", "actor_only", {"block_size": 1}, 12, 32, 2048),
+    ("unified", "actor_only", {"block_size": 1}, 64, 512, 16),
+])
+def test_learner_reset_envs_matches_cpu(variant, mode, params, H, N, E):
+    """reset(env_mask) of the batched learner (ffm_learner_reset_envs): a random half of the
+    envs re-placed mid-run; positions, counts, DFF, episode counters and the V / H tables equal
+    the CPU restatement re-placing the same envs (model/ffm_unified.py:800-812 per env)."""
+    _philox_compare(variant, mode, params, H, H, N, E, 60, max_steps=40, reset_at=(23, 0.5))
 
 
 def test_learner_philox_trained_matches_cpu():
@@ -1217,6 +1246,66 @@ def _c5_curriculum_worker(rank, world, port, out):
         _c5_curriculum_run(out, world, rank, sync=sync)
     finally:
         dist.destroy_process_group()
+
+
+def _growing_curriculum_run(tmp, world=1, rank=0, sync=None, envs=128):
+    """A radius / N curriculum whose crowd grows: radius 4 with N = 10 (a crowd on one
+    owner's rows), then radius 25 with N = 10 and N = 300, on the tiled 64x64 learner (agent
+    capacity above 256: the raster batch kernel, so the owner exchange)."""
+    from ffm_amd import train as T
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(64, 64)
+    d = T.driver_settings("unified")
+    E = envs // world
+    L = _learner(m, l1_sff(m), "unified", n_envs=E, n_agents=300, mode="actor_only", params=d["params"], seed=21,
+                 max_steps=60, env_base=rank * E)
+    g = T._Group(sync(L) if sync else None)
+    res = T.run_curriculum(L, (0, 32), [4, 25], [10, 300], envs, *d["eps"], tmp, verbose=False, group=g,
+                           global_envs=envs)
+    L.close()
+    return res
+
+
+def _growing_curriculum_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ffm_amd.dist import TableSync
+
+        def sync(L):
+            ts = TableSync(L, device="cuda", capacity=None)
+            assert ts.owner
+            return ts
+
+        _growing_curriculum_run(out, world, rank, sync=sync)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_growing_curriculum_sharded_gloo_world2_equals_single(tmp_path):
+    """the owner exchange's capacities adapt to the counts observed, so a
+    curriculum whose next configuration crowds more records onto one owner (radius 4, N = 10
+    -> radius 25, N = 300) overflowed them.  TableSync.reconfigure restarts them from the new
+    configuration's shape bounds: the two-rank run completes and writes the files of one
+    process stepping the same 128 global envs."""
+    import csv
+    import socket
+    import torch.multiprocessing as mp
+    one = tmp_path / "one"
+    res = _growing_curriculum_run(str(one))
+    assert [(c["radius"], c["N"]) for c in res["configs"]] == [(4, 10), (25, 10), (25, 300)]
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    two = tmp_path / "two"
+    mp.spawn(_growing_curriculum_worker, args=(2, port, str(two)), nprocs=2, join=True)
+    with open(one / "steps_per_episode.csv") as f:
+        a = list(csv.reader(f))
+    with open(two / "steps_per_episode.csv") as f:
+        b = list(csv.reader(f))
+    assert a == b and len(a) == 1 + 3 * 128
 
 
 def test_c5_curriculum_sharded_gloo_world2_equals_single(tmp_path):

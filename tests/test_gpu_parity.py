@@ -174,6 +174,58 @@ def test_philox_config2_full_size_matches_cpu(epb):
     assert eps.sum() > 0  # auto-reset exercised
 
 
+@pytest.mark.parametrize("H,N,E,epb", [(12, 32, 65536, 0), (12, 32, 4096, -2), (64, 512, 48, 0)])
+def test_engine_reset_envs_matches_cpu(H, N, E, epb):
+    """reset(env_mask) through the ABI (ffm_engine_reset_envs): mid-run, a random
+    third of the envs is re-placed (C2's 65,536 envs on the group kernel, the lane kernel, and
+    C3's 64x64 room); the oracle re-places the same envs with reset_philox at the same step
+    index.  Positions, counts, DFF bits and episode counters equal the oracle's, before and
+    after the reset, and the unmasked envs are untouched."""
+    import torch
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import oracle as O
+    params = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"}
+    m = make_room(H, H)
+    s = l1_sff(m)
+    seed, T1, T2 = 11, 25, 25
+    eng = _engine(map_array=m, sff=s, n_envs=E, n_agents=N, params=params, rng="philox", seed=seed,
+                  auto_reset=True, envs_per_block=epb)
+    core = O.Core(m, s, params)
+    pos = np.stack([core.reset_philox(N, seed, 0, e) for e in range(E)])
+    cnt = np.full(E, N, np.int32)
+    dff = np.zeros((E, H, H), np.float32)
+    eps = np.zeros(E, np.int32)
+    eng.reset()
+    for t in range(1, T1 + 1):
+        core.step_philox_batch(pos, cnt, dff, eps, seed, t, True, N, 0, 16)
+    eng.step(T1)
+    mask = np.random.default_rng(5).random(E) < 0.33
+    before = eng.get_state()
+    eng.reset_envs(torch.as_tensor(mask.astype(np.uint8)).cuda())   # device mask, read in place
+    tr = T1 + 1                                                      # the placement's step index
+    gpos, gcnt, gdff = eng.get_state()
+    for e in np.flatnonzero(mask):
+        pos[e] = core.reset_philox(N, seed, tr, e)
+        cnt[e] = N
+        dff[e] = 0.0
+    keep = ~mask
+    assert np.array_equal(gcnt[keep], before[1][keep]) and np.array_equal(gdff[keep], before[2][keep])
+    assert np.array_equal(gcnt, cnt), "counts after reset_envs"
+    for e in range(E):
+        assert np.array_equal(gpos[e, :cnt[e]], pos[e, :cnt[e]]), f"env {e} positions after reset_envs"
+    assert np.array_equal(gdff.view(np.uint32), dff.view(np.uint32)), "DFF after reset_envs"
+    for t in range(tr + 1, tr + 1 + T2):
+        core.step_philox_batch(pos, cnt, dff, eps, seed, t, True, N, 0, 16)
+    eng.step(T2)
+    gpos, gcnt, gdff = eng.get_state()
+    assert np.array_equal(gcnt, cnt), "counts"
+    for e in range(E):
+        assert np.array_equal(gpos[e, :cnt[e]], pos[e, :cnt[e]]), f"env {e} positions"
+    assert np.array_equal(gdff.view(np.uint32), dff.view(np.uint32)), "DFF bits"
+    assert eng.counters()["resets"] == int(eps.sum())
+    eng.close()
+
+
 @pytest.mark.parametrize("epb", [-3, -2, -1, 3])
 @pytest.mark.parametrize("N", [32, 60])
 @pytest.mark.parametrize("params", [
