@@ -58,6 +58,10 @@ def parse():
                          "(config 2), 300 (config 5: one whole episode, so the timed episodes start on "
                          "populated tables), else 0")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    ap.add_argument("--global-envs", type=int, default=None,
+                    help="configs 2/3: envs of the WHOLE job, split over the ranks (strong scaling: the "
+                         "metric's '64k envs' read as a global count; 'scaling' becomes 'strong'); "
+                         "default: --envs per GPU (weak scaling)")
     ap.add_argument("--size", type=int, default=None)
     ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--neighborhood", default="neumann")
@@ -124,6 +128,11 @@ def main():
     H = W = args.size
     A = args.agents
     E = args.envs
+    strong = args.global_envs is not None
+    if strong:   # strong scaling: the job's envs split over the ranks (global ids stay contiguous)
+        if args.global_envs % world:
+            raise SystemExit("--global-envs must divide by the number of ranks")
+        E = args.global_envs // world
     m = make_room(H, W)
     s = l1_sff(m)
     params = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": args.neighborhood}
@@ -185,13 +194,14 @@ def main():
         bytes_per_env_step = 2 * (2 * A + 4 * H * W + 4)
         mean_kernel_s = float(np.mean(kern_ms)) / 1e3
         achieved = E * bytes_per_env_step / mean_kernel_s / 1e9
-        traffic = None
+        traffic = traffic_src = None
         tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{H}x{W}_A{A}_E{E}.json")
         if os.path.exists(tpath):
             with open(tpath) as f:
                 tj = json.load(f)
             if tj.get("config") == f"{H}x{W}_A{A}_E{E}":
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = profile_source(tpath, tj)
         # the step kernel's VALU issue fraction (its real bound at 12x12) from a committed
         # PMC summary (tools/pmc.sh + tools/valu_json.py)
         valu = None
@@ -210,12 +220,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": (f"ffm_core step, {H}x{W} room, {A} agents/env, {E} envs/GPU, "
+                "workload": (f"ffm_core step, {H}x{W} room, {A} agents/env, {E} envs/GPU"
+                             + (f" ({E * world} envs for the whole job, split over {world} GPUs)" if strong else "")
+                             + ", "
                              f"{args.neighborhood}, Philox seed {args.seed}, on-device auto-reset, "
                              + (f"steady state (envs desynchronised by a {args.burn_in}-step untimed burn-in "
                                 f"after reset)" if args.burn_in else
@@ -235,11 +247,16 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch_algorithmic": E * bytes_per_env_step,
+                # BASELINE.md 3's form: env-steps/s of the timed windows (launch gaps included) x B
+                "frac_env_rate": E * world * args.steps / elapsed * bytes_per_env_step / 1e9 / world / PEAK_HBM_GBS,
                 "achievable_copy_GBs": copy_gbs,
                 "frac_of_copy": achieved / copy_gbs if copy_gbs else None,
                 **({"valu_issue_frac": valu["valu_issue_frac"], "valu_per_wave": valu["valu_per_wave"],
-                    "valu_source": f"profiles/valu_{H}x{W}_A{A}_E{E}.json ({valu['formula']})"} if valu else {}),
+                    "valu_source": profile_source(os.path.join(ROOT, "profiles", f"valu_{H}x{W}_A{A}_E{E}.json"),
+                                                  valu) + f"; {valu['formula']}",
+                    "valu_calibration": VALU_CALIBRATION} if valu else {}),
             },
             "cpu_baseline": None,
             "multi_step": multi,
@@ -263,6 +280,19 @@ LEARN_CONFIGS = {
                     "exit_reward": 100.0, "step_penalty": -1.0, "collision_penalty": -1.0,
                     "neighborhood": "neumann", "block_size": 1, "epsilon": 0.2}),
 }
+
+
+VALU_CALIBRATION = ("profiles/r06/alu/valu_calibration.json: saturated microkernels of known VALU count read "
+                     "0.995 (v_mul_hi/lo_u32), 1.014 (v_mad_u64_u32) and 0.985 (v_exp_f32) by this formula, but "
+                     "1.83 for plain xor/add: simple 32-bit ops issue faster than one per 4 clocks, so 1.0 is the "
+                     "ceiling of multiply/transcendental-bound code only")
+
+
+def profile_source(path, d):
+    """Where a derived bench field comes from: a committed PMC profile, not this run."""
+    rel = os.path.relpath(path, ROOT)
+    when = d.get("measured", "an earlier round")
+    return f"committed profile {rel} (measured {when}; not measured in this run)"
 
 
 def timed_repeats(args, world, dist, torch, run_k, counters):

@@ -33,6 +33,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "core_common.h"
 #include "kernels.h"
 #include "lane_common.h"
@@ -106,6 +109,18 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 //   4: the product kernel
 #ifndef FFM_GROUP_LADDER
 #define FFM_GROUP_LADDER 4
+#endif
+
+// Where the next group's HBM loads are issued (diagnostic A/B): 0 before the stencil, 1 after
+// decide, 2 after mark, 3 right after the staging.
+#ifndef FFM_GROUP_PF
+#define FFM_GROUP_PF 0
+#endif
+
+// Waves that step fewer groups than the most loaded ones start late by s_sleep(N) (64 N
+// clocks): their phases leave the others' (diagnostic A/B; 0 = off).
+#ifndef FFM_GROUP_STAGGER
+#define FFM_GROUP_STAGGER 0
 #endif
 
 #ifndef FFM_GROUP_WAVES
@@ -192,6 +207,12 @@ void core_group_kernel(CoreStepArgs a) {
         }
     };
     constexpr int LAD = FFM_GROUP_LADDER;
+    constexpr int PF = FFM_GROUP_PF;
+    if (FFM_GROUP_STAGGER > 0) {
+        const int mine = g < ngroups ? (ngroups - 1 - g) / wstride + 1 : 0;
+        const int most = (ngroups - 1) / wstride + 1;
+        if (mine < most) __builtin_amdgcn_s_sleep(FFM_GROUP_STAGGER);
+    }
     GState cur;
     load(g < ngroups ? g : -1, cur);
 
@@ -243,10 +264,13 @@ void core_group_kernel(CoreStepArgs a) {
             continue;
         }
 
+        GState nxt;
+        const int gn = g + wstride < ngroups ? g + wstride : -1;
         // ---- stage the group (prefetched by the previous iteration or the prologue) -------
 #pragma unroll
         for (int k = 0; k < NS; k++)
             if (toff[k] >= 0) *reinterpret_cast<float4*>(tile + toff[k]) = cur.d[k];
+        if (PF == 3) load(gn, nxt);
         unsigned long long rsm = 0ull;   // envs re-placed at the end of this step
         if (LAD == 2) wave_sync();       // ladder rung 2: the staged tile before the stencil reads it
         if (LAD >= 3) {
@@ -288,6 +312,7 @@ void core_group_kernel(CoreStepArgs a) {
         }
         wave_sync();
 
+        if (PF == 2) load(gn, nxt);
         // ---- decide (model/ffm_core.py:40-88) -------------------------------------------
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
@@ -318,6 +343,7 @@ void core_group_kernel(CoreStepArgs a) {
         }
         wave_sync();
 
+        if (PF == 1) load(gn, nxt);
         // ---- resolve (model/ffm_core.py:90-98), by each requester ------------------------
         unsigned long long km[MAXC];
         int kept = 0;
@@ -424,8 +450,7 @@ void core_group_kernel(CoreStepArgs a) {
 
         // ---- next group's HBM loads, in flight across the stencil, the stores and the
         // next group's head ------------------------------------------------------------
-        GState nxt;
-        load(g + wstride < ngroups ? g + wstride : -1, nxt);
+        if (PF == 0 || LAD < 3) load(gn, nxt);
 
         // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb],
         // then the DFF stores (an env reset this step starts its next episode at zero) ----
@@ -508,51 +533,69 @@ void core_group_kernel(CoreStepArgs a) {
 #ifndef FFM_GROUP_G
 #define FFM_GROUP_G 4
 #endif
-constexpr int kGroupG = FFM_GROUP_G;
+constexpr int kGroupG = FFM_GROUP_G;   // envs per group at large E
+constexpr int kGroupGSmall = 2;        // envs per group when the large-E groups fill less than half the waves
 
-size_t core_group_smem_bytes(int H, int W, int F, int waves) {
+size_t core_group_smem_bytes(int H, int W, int F, int waves, int G) {
     const int PHW = (H + 2) * (W + 2);
-    return group_shared_bytes(PHW, F) + (size_t)waves * group_carve<kGroupG>(PHW, lane_tile_floats(H, W), F).per_wave;
+    const size_t per_wave = G == kGroupGSmall ? group_carve<kGroupGSmall>(PHW, lane_tile_floats(H, W), F).per_wave
+                                              : group_carve<kGroupG>(PHW, lane_tile_floats(H, W), F).per_wave;
+    return group_shared_bytes(PHW, F) + (size_t)waves * per_wave;
 }
 
 bool core_group_supported(int H, int W) { return H == 12 && W == 12; }
-
-int core_group_envs() { return kGroupG; }
 
 int core_group_max_iters() { return kGroupMaxIters; }
 
 // KD1: k_D == 1 (the drivers' setting), where k_D * DFF is DFF itself: a kernel of its own
 // rather than a runtime flag, which the register allocator would keep (and spill) all launch.
-template <int NB, bool KD1>
+template <int NB, bool KD1, int G>
 static hipError_t group_op(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
-    const size_t smem = core_group_smem_bytes(a.H, a.W, a.F, 4);
+    const size_t smem = core_group_smem_bytes(a.H, a.W, a.F, 4, G);
     if (op) {
         *occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, core_group_kernel<NB, 12, 12, kGroupG, KD1>, 256,
-                                                         smem) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, core_group_kernel<NB, 12, 12, G, KD1>, 256, smem) !=
+            hipSuccess)
             *occ = 0;
         return hipSuccess;
     }
-    const long long groups = (a.E + kGroupG - 1) / kGroupG;
+    const long long groups = (a.E + G - 1) / G;
     if (a.H != 12 || a.W != 12 || a.A > 32 || (groups + (long long)blocks * 4 - 1) / ((long long)blocks * 4) > kGroupMaxIters)
         return hipErrorInvalidConfiguration;   // shapes the kernel and its grid assume
-    core_group_kernel<NB, 12, 12, kGroupG, KD1><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
+    core_group_kernel<NB, 12, 12, G, KD1><<<dim3((unsigned)blocks), dim3(256), smem, s>>>(a);
     return hipGetLastError();
 }
 
 template <int NB>
-static hipError_t group_op_kd(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ) {
-    return a.kD32 == 1.0f ? group_op<NB, true>(a, blocks, s, op, occ) : group_op<NB, false>(a, blocks, s, op, occ);
+static hipError_t group_op_kd(const CoreStepArgs& a, int blocks, hipStream_t s, int op, int* occ, int G) {
+    if (G == kGroupGSmall)
+        return a.kD32 == 1.0f ? group_op<NB, true, kGroupGSmall>(a, blocks, s, op, occ)
+                              : group_op<NB, false, kGroupGSmall>(a, blocks, s, op, occ);
+    return a.kD32 == 1.0f ? group_op<NB, true, kGroupG>(a, blocks, s, op, occ)
+                          : group_op<NB, false, kGroupG>(a, blocks, s, op, occ);
 }
 
-hipError_t launch_core_group(const CoreStepArgs& a, int nb, int blocks, hipStream_t s) {
-    return nb == 4 ? group_op_kd<4>(a, blocks, s, 0, nullptr) : group_op_kd<8>(a, blocks, s, 0, nullptr);
+hipError_t launch_core_group(const CoreStepArgs& a, int nb, int blocks, hipStream_t s, int G) {
+    return nb == 4 ? group_op_kd<4>(a, blocks, s, 0, nullptr, G) : group_op_kd<8>(a, blocks, s, 0, nullptr, G);
 }
 
-int core_group_blocks_per_cu(const CoreStepArgs& a, int nb) {
+int core_group_blocks_per_cu(const CoreStepArgs& a, int nb, int G) {
     int n = 0;
-    (void)(nb == 4 ? group_op_kd<4>(a, 0, nullptr, 1, &n) : group_op_kd<8>(a, 0, nullptr, 1, &n));
+    (void)(nb == 4 ? group_op_kd<4>(a, 0, nullptr, 1, &n, G) : group_op_kd<8>(a, 0, nullptr, 1, &n, G));
     return n;
+}
+
+// Envs per group for E envs: the large-E size, unless its groups would fill less than half the
+// resident waves -- then each wave's one group is the launch's critical path, and halving the
+// group (one agent chunk, half the DFF slots) shortens it (E-sweep, profiles/r06/c2: 8,192 envs
+// 13.8 -> 12.7 us; from 16,384 envs on G = 4 is faster).  FFM_GROUP_ENVS=2|4 forces it.
+int core_group_pick_envs(const CoreStepArgs& a, int nb, long long E, int cus) {
+    if (const char* ov = std::getenv("FFM_GROUP_ENVS")) {
+        const int v = std::atoi(ov);
+        if (v == kGroupGSmall || v == kGroupG) return v;
+    }
+    const long long waves = (long long)cus * std::max(1, core_group_blocks_per_cu(a, nb, kGroupG)) * 4;
+    return 2 * ((E + kGroupG - 1) / kGroupG) <= waves ? kGroupGSmall : kGroupG;
 }
 
 }  // namespace ffm

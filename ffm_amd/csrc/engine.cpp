@@ -54,6 +54,7 @@ struct ffm_engine {
     int lane_blocks = 0;    // persistent grid of the lane kernel
     bool group = false;     // group kernel (lane conditions at 12x12): core_group.hip
     int group_blocks = 0;   // persistent grid of the group kernel
+    int group_g = 4;        // envs per group (core_group_pick_envs)
     bool multi = false;     // multi-step kernel available (lane conditions): core_multi.hip
     int multi_blocks = 0;   // its persistent grid
     int fused = 1;          // steps per launch (ffm_engine_set_fused_steps)
@@ -276,8 +277,9 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
             e->multi_blocks = (int)std::max<long long>(1, std::min<long long>((pairs + 3) / 4, (long long)cus * per_cu));
         }
         if (e->group) {
-            const int per_cu = std::max(1, ffm::core_group_blocks_per_cu(a, d.neighborhood));
-            const long long G = ffm::core_group_envs();
+            e->group_g = ffm::core_group_pick_envs(a, d.neighborhood, d.n_envs, cus);
+            const int per_cu = std::max(1, ffm::core_group_blocks_per_cu(a, d.neighborhood, e->group_g));
+            const long long G = e->group_g;
             const long long groups = (d.n_envs + G - 1) / G;
             e->group_blocks = (int)std::max<long long>(1, std::min<long long>((groups + 3) / 4, (long long)cus * per_cu));
             if (const char* ov = std::getenv("FFM_WAVE_BLOCKS")) {   // diagnostic override of the grid
@@ -391,7 +393,7 @@ int ffm_engine_step(ffm_engine* e, int32_t n_steps, void* stream) {
     }
     for (int i = 0; i < n_steps; i++) {
         ffm::CoreStepArgs a = make_args(e);
-        if (e->group) HIP_TRY(ffm::launch_core_group(a, e->d.neighborhood, e->group_blocks, s));
+        if (e->group) HIP_TRY(ffm::launch_core_group(a, e->d.neighborhood, e->group_blocks, s, e->group_g));
         else if (e->lane) HIP_TRY(ffm::launch_core_lane(a, e->d.neighborhood, e->lane_blocks, s));
         else if (e->wave) HIP_TRY(ffm::launch_core_wave(a, e->d.neighborhood, e->mt, e->wave_blocks, s));
         else HIP_TRY(ffm::launch_core_block(a, e->d.neighborhood, e->f64, e->mt, e->block, s));

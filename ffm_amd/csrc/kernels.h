@@ -64,12 +64,12 @@ size_t core_lane_smem_bytes(int H, int W, int F, int waves);
 hipError_t launch_core_lane(const CoreStepArgs& a, int nb, int blocks, hipStream_t s);
 int core_lane_blocks_per_cu(const CoreStepArgs& a, int nb);
 int core_lane_max_pairs_per_wave();
-size_t core_group_smem_bytes(int H, int W, int F, int waves);
+size_t core_group_smem_bytes(int H, int W, int F, int waves, int G = 4);
 bool core_group_supported(int H, int W);
-int core_group_envs();
 int core_group_max_iters();
-hipError_t launch_core_group(const CoreStepArgs& a, int nb, int blocks, hipStream_t s);
-int core_group_blocks_per_cu(const CoreStepArgs& a, int nb);
+int core_group_pick_envs(const CoreStepArgs& a, int nb, long long E, int cus);   // envs per group (2 or 4)
+hipError_t launch_core_group(const CoreStepArgs& a, int nb, int blocks, hipStream_t s, int G);
+int core_group_blocks_per_cu(const CoreStepArgs& a, int nb, int G);
 size_t core_multi_smem_bytes(int H, int W, int F, int waves);
 hipError_t launch_core_multi(const CoreStepArgs& a, int nb, int nsteps, int blocks, hipStream_t s);
 int core_multi_blocks_per_cu(const CoreStepArgs& a, int nb);

@@ -7,6 +7,7 @@ it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
 """
 import csv
 import json
+import time
 import os
 import sys
 
@@ -86,6 +87,7 @@ if cfg in (4, 5):
                           "lines, 1.0 x the bytes of random 64-B lines, 64 B per random 8-B or 16-B read. This "
                           "kernel mixes streamed bytes (x2) with random 64-B table lines (x1), so its traffic lies "
                           "in traffic_over_algorithmic_range; hbm_bytes_per_launch keeps the x2 upper bound.")
+res["measured"] = os.environ.get("FFM_MEASURED", time.strftime("%Y-%m-%d"))   # e.g. "round 6, <commit>"
 print(json.dumps(res, indent=1))
 with open(os.path.join(out, "traffic.json"), "w") as fh:
     json.dump(res, fh, indent=1)
