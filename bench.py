@@ -449,11 +449,10 @@ def bench_learner(args, world, rank, torch, dist):
                                           "tiled records all-gather" if sync.tiled else
                                           "dense all-reduce" if sync.dense else "records (adaptive capacity)"),
                                  "bytes_per_rank_per_step": sent_timed / (reps["summary"]["n"] * args.steps),
-                                 **({"received_bytes_per_rank_per_step":
-                                     recv_timed / (reps["summary"]["n"] * args.steps)}
-                                    if getattr(sync, "owner", False) else {}),
-                                 "note": "bytes this rank contributes to the collectives per step, over the "
-                                         "timed regions"},
+                                 "received_bytes_per_rank_per_step": recv_timed / (reps["summary"]["n"] * args.steps),
+                                 "note": "bytes this rank contributes to / receives from the collectives per "
+                                         "step, over the timed regions (fixed-capacity buffers: the bytes on the "
+                                         "wire, not the touched counts)"},
                                 **({} if sync.dense or sync.tiled else {"record_capacity": dict(sync.caps),
                                                           "max_touched_records": dict(sync.max_count)}))
                            if world > 1 else {"period": args.sync_period}),

@@ -51,7 +51,7 @@ constexpr int kGroupMaxIters = 16;
 constexpr int kGroupPendWords = 8 * kGroupMaxIters / 32;
 
 struct GroupCarve {
-    size_t grid, tile, words, posst, kp, keys, pend, per_wave;
+    size_t grid, tile, words, posst, kp, keys, pend, dummy, per_wave;
 };
 
 // The staged positions are dead once the agents are marked, so the kept-prefix
@@ -70,6 +70,7 @@ __host__ __device__ inline GroupCarve group_carve(int PHW, int TS, int F) {
     c.posst = o;
     c.kp = o;    o += a16((size_t)(G * 32 + 1) * 2);
     c.pend = o;  o += kGroupPendWords * 4;
+    c.dummy = o; o += 4;   // the target of the idle lanes' LDS writes (no exec-mask branch per write)
     c.per_wave = a16(o);
     return c;
 }
@@ -124,7 +125,7 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 #endif
 
 #ifndef FFM_GROUP_WAVES
-#define FFM_GROUP_WAVES 1   // minimum waves per SIMD asked of the register allocator
+#define FFM_GROUP_WAVES 6   // minimum waves per SIMD asked of the register allocator (80 VGPRs at G = 4, no spill)
 #endif
 
 template <int NB, int HT, int WT, int G, bool KD1>
@@ -163,6 +164,8 @@ void core_group_kernel(CoreStepArgs a) {
     uint16_t* const kp = reinterpret_cast<uint16_t*>(wbase + cv.kp);
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(wbase + cv.keys);
     uint32_t* const pend = reinterpret_cast<uint32_t*>(wbase + cv.pend);
+    const int kDummy16 = (int)((cv.dummy - cv.grid) / 2);    // grid index of the dummy word
+    const int kDummy32 = (int)((cv.dummy - cv.words) / 4);   // words index of the dummy word
 
     // The lane's DFF float4 slots: q = 64 k + lane of the group's G * HW cells,
     // env q / Q4, cell 4 (q % Q4) of that env.
@@ -178,8 +181,16 @@ void core_group_kernel(CoreStepArgs a) {
         senv |= (uint32_t)(q < Q ? s : 15) << (4 * k);
     }
 
-    const long long E = a.E;                   // host-checked: E * HW * 4 < 2^31
+    const long long E = a.E;                   // host-checked: (E + 7) * HW * 4 < 2^31
     const uint32_t ebase = (uint32_t)a.env_base;
+    // Whole-array buffer resources, built once.  The engine pads pos / cnt / DFF to whole groups
+    // of 8 envs (zeroed), so a partial last group reads zero counts and DFF and its stores land
+    // in the padding; every access takes its group's byte base as the scalar offset, and lanes
+    // past the group's bytes use kOOB (dropped).
+    const int Epad = (int)((E + 7) & ~7LL);
+    const __amdgpu_buffer_rsrc_t rC = pair_rsrc(a.cnt, Epad * 4);
+    const __amdgpu_buffer_rsrc_t rP = pair_rsrc(a.pos, Epad * A * 2 + 4);   // + the dword of slack
+    const __amdgpu_buffer_rsrc_t rD = pair_rsrc(a.dff, Epad * HW * 4);
     const int ngroups = (int)((E + G - 1) / G);
     const int wstride = (int)gridDim.x * 4;
     int g = (int)blockIdx.x * 4 + wv;
@@ -190,20 +201,18 @@ void core_group_kernel(CoreStepArgs a) {
         int c;
     };
     auto load = [&](int gg, GState& st) {
-        const long long e0 = (long long)(gg < 0 ? 0 : gg) * G;
-        const int nenv = gg < 0 ? 0 : (int)min((long long)G, E - e0);
-        st.c = (int)__builtin_amdgcn_raw_buffer_load_b32(pair_rsrc(a.cnt + e0, nenv * 4), lane < G ? lane * 4 : kOOB, 0,
-                                                        0);
-        // the pos buffer carries a dword of slack, so the byte count rounds up to dwords
-        const __amdgpu_buffer_rsrc_t rp = pair_rsrc(a.pos + e0 * A, (nenv * A * 2 + 3) & ~3);
-        st.p0 = __builtin_amdgcn_raw_buffer_load_b32(rp, lane < PWORDS ? lane * 4 : kOOB, 0, 0);
-        st.p1 = PWORDS > 64 ? __builtin_amdgcn_raw_buffer_load_b32(rp, 64 + lane < PWORDS ? 256 + lane * 4 : kOOB, 0, 0)
+        if (gg < 0) return;   // wave-uniform: nothing past the last group (the loop ends first)
+        const int e0 = gg * G;
+        st.c = (int)__builtin_amdgcn_raw_buffer_load_b32(rC, lane < G ? lane * 4 : kOOB, e0 * 4, 0);
+        st.p0 = __builtin_amdgcn_raw_buffer_load_b32(rP, lane < PWORDS ? lane * 4 : kOOB, e0 * A * 2, 0);
+        st.p1 = PWORDS > 64 ? __builtin_amdgcn_raw_buffer_load_b32(rP, 64 + lane < PWORDS ? 256 + lane * 4 : kOOB,
+                                                                 e0 * A * 2, 0)
                             : 0u;
-        const __amdgpu_buffer_rsrc_t rd = pair_rsrc(a.dff + e0 * HW, nenv * HW * 4);
 #pragma unroll
         for (int k = 0; k < NS; k++) {
             const int q = k * 64 + lane;
-            st.d[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rd, q < Q ? q * 16 : kOOB, 0, 0));
+            st.d[k] = __builtin_bit_cast(float4,
+                                         __builtin_amdgcn_raw_buffer_load_b128(rD, q < Q ? q * 16 : kOOB, e0 * HW * 4, 0));
         }
     };
     constexpr int LAD = FFM_GROUP_LADDER;
@@ -214,6 +223,8 @@ void core_group_kernel(CoreStepArgs a) {
         if (mine < most) __builtin_amdgcn_s_sleep(FFM_GROUP_STAGGER);
     }
     GState cur;
+    cur.c = 0;
+    cur.p0 = cur.p1 = 0u;
     load(g < ngroups ? g : -1, cur);
 
     if (LAD >= 1) {
@@ -240,7 +251,7 @@ void core_group_kernel(CoreStepArgs a) {
     constexpr uint32_t mW = (uint32_t)(((1ull << 32) + (unsigned)W - 1) / (unsigned)W);   // x = c / W, c < 2^16
     const int g_first = g;
     for (int iter = 0; g < ngroups; g += wstride, iter++) {
-        const long long e0 = (long long)g * G;
+        const int e0 = g * G;
         const int nenv = (int)min((long long)G, E - e0);
         if (LAD <= 2) {   // ladder rungs 0-2: positions and counts stored back unchanged
             const __amdgpu_buffer_rsrc_t rq = pair_rsrc(a.pos + e0 * A, (nenv * A * 2 + 3) & ~3);
@@ -269,7 +280,7 @@ void core_group_kernel(CoreStepArgs a) {
         // ---- stage the group (prefetched by the previous iteration or the prologue) -------
 #pragma unroll
         for (int k = 0; k < NS; k++)
-            if (toff[k] >= 0) *reinterpret_cast<float4*>(tile + toff[k]) = cur.d[k];
+            if (k < NSF || toff[k] >= 0) *reinterpret_cast<float4*>(tile + toff[k]) = cur.d[k];
         if (PF == 3) load(gn, nxt);
         unsigned long long rsm = 0ull;   // envs re-placed at the end of this step
         if (LAD == 2) wave_sync();       // ladder rung 2: the staged tile before the stencil reads it
@@ -305,7 +316,7 @@ void core_group_kernel(CoreStepArgs a) {
                 const int x = (int)__umulhi(p, mW);
                 const int y = (int)p - x * W;
                 const int pp = live ? (x + 1) * PW + y + 1 : PW + 1;
-                if (live) grid[s * PHW + pp] = (uint16_t)(DirCodes::kAgent | (uint32_t)al | (DirCodes::kNoDir << 8));
+                grid[live ? s * PHW + pp : kDummy16] = (uint16_t)(DirCodes::kAgent | (uint32_t)al | (DirCodes::kNoDir << 8));
                 cs[c] = (uint32_t)pp | ((uint32_t)al << 16) | ((uint32_t)s << 21) | ((live ? 1u : 0u) << 24) |
                         ((uint32_t)(live ? x + 1 : 1) << 25);
             }
@@ -323,7 +334,7 @@ void core_group_kernel(CoreStepArgs a) {
                 const bool live = cs_live(v);
                 const uint32_t genv = ebase + (uint32_t)e0 + (uint32_t)s;
                 const uint4 pb = philox(make_uint4(a.t, genv, (uint32_t)al, kPurDecide << 28), a.key0, a.key1);
-                if (live) words[s * 32 + al] = pb.w;   // the friction draw, if this agent owns a contested target
+                words[live ? s * 32 + al : kDummy32] = pb.w;   // the friction draw, if this agent owns a contested target
                 const uint16_t* gk = grid + s * PHW;
                 const float* dk = tile + s * TS;
                 const int dd0 = 3 - 2 * cs_xp1(v);
@@ -336,8 +347,8 @@ void core_group_kernel(CoreStepArgs a) {
                                    : lane_decide_exact_arr<NB, true>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32,
                                                                u53(pb.x, pb.y));
                 const uint32_t sd = slot <= (uint32_t)NB ? slot : DirCodes::kNoDir;
-                if (live)
-                    grid[s * PHW + pp] = (uint16_t)(DirCodes::kAgent | (uint32_t)al | (sd << 8) | ((pb.z >> 31) << 12));
+                grid[live ? s * PHW + pp : kDummy16] =
+                    (uint16_t)(DirCodes::kAgent | (uint32_t)al | (sd << 8) | ((pb.z >> 31) << 12));
                 cr[c] = sd | ((to_exit ? 1u : 0u) << 4);
             }
         }
@@ -377,16 +388,13 @@ void core_group_kernel(CoreStepArgs a) {
                         zo = lower ? (cc >> 12) & 1u : zo;
                         o = lower ? who : o;
                     }
-                    if (moving) {
-                        if (m == 1) {
-                            granted = true;
-                        } else {
-                            const uint32_t w = words[s * 32 + o];
-                            const uint32_t genv = ebase + (uint32_t)e0 + (uint32_t)s;
-                            const int kk = philox_friction(zo << 31, w, (uint32_t)m, a.key0, a.key1, a.t, genv,
-                                                           (uint32_t)o);
-                            granted = kk == k;   // :95-96
-                        }
+                    granted = moving ? m == 1 : granted;   // an uncontested move is granted
+                    if (moving && m > 1) {
+                        const uint32_t w = words[s * 32 + o];
+                        const uint32_t genv = ebase + (uint32_t)e0 + (uint32_t)s;
+                        const int kk = philox_friction(zo << 31, w, (uint32_t)m, a.key0, a.key1, a.t, genv,
+                                                       (uint32_t)o);
+                        granted = kk == k;   // :95-96
                     }
                 }
                 // :91-98 -- the mover's source cell gains 1 (one agent per cell: no collisions)
@@ -407,16 +415,13 @@ void core_group_kernel(CoreStepArgs a) {
         for (int c = 0; c < MAXC; c++) {
             if (c * 64 < T) {
                 const uint32_t v = cs[c];
-                if (cs_live(v)) {
-                    kp[c * 64 + lane] = (uint16_t)(cr[c] >> 17);
-                    grid[cs_s(v) * PHW + cs_pp(v)] = 0;   // unmark: agents only ever stand on free cells
-                }
+                kp[c * 64 + lane] = (uint16_t)(cr[c] >> 17);   // idle lanes' entries are never read
+                grid[cs_live(v) ? cs_s(v) * PHW + cs_pp(v) : kDummy16] = 0;   // unmark: agents stand on free cells
             }
         }
         if (lane == 0) kp[T] = (uint16_t)kept;
         c_exits += (unsigned)(T - kept);
         wave_sync();
-        const __amdgpu_buffer_rsrc_t rp = pair_rsrc(a.pos + e0 * A, nenv * A * 2);
 #pragma unroll
         for (int c = 0; c < MAXC; c++) {
             if (c * 64 < T) {
@@ -426,8 +431,8 @@ void core_group_kernel(CoreStepArgs a) {
                 const bool keep = ((w >> 16) & 1u) != 0u;
                 const int start = j - cs_al(v);
                 const int newidx = (int)(w >> 17) - (int)kp[cs_live(v) ? start : 0];
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)unpad((int)(w & 0xFFFFu), PW), rp,
-                                                      keep ? (s * A + newidx) * 2 : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)unpad((int)(w & 0xFFFFu), PW), rP,
+                                                      keep ? (s * A + newidx) * 2 : kOOB, e0 * A * 2, 0);
             }
         }
         int Sl = T, Sh = T;   // lane s < G: [S[s], S[s+1])
@@ -439,8 +444,7 @@ void core_group_kernel(CoreStepArgs a) {
         const int nk = (int)kp[Sh] - (int)kp[Sl];
         const bool rs = a.auto_reset && lane < nenv && nk == 0;
         rsm = __ballot(rs);
-        __builtin_amdgcn_raw_buffer_store_b32((unsigned)(rs ? a.N : nk), pair_rsrc(a.cnt + e0, nenv * 4),
-                                              lane < G ? lane * 4 : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)(rs ? a.N : nk), rC, lane < G ? lane * 4 : kOOB, e0 * 4, 0);
         if (rsm) {   // wave-uniform, rare
             c_resets += (unsigned)__popcll(rsm);
             if (a.episodes && rs) a.episodes[e0 + lane] += 1;
@@ -454,7 +458,6 @@ void core_group_kernel(CoreStepArgs a) {
 
         // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb],
         // then the DFF stores (an env reset this step starts its next episode at zero) ----
-        const __amdgpu_buffer_rsrc_t rd = pair_rsrc(a.dff + e0 * HW, nenv * HW * 4);
         if (SCALAR_TAIL) {     // the last, partial float4 slot as one cell per lane (all lanes busy)
             const int q = 4 * 64 * NSF + lane;                 // the group's cell
             const int s = q / HW, c = q - s * HW, y = c % W;
@@ -470,12 +473,12 @@ void core_group_kernel(CoreStepArgs a) {
             acc = acc + a.c1 * br;
             const bool z = ((rsm >> s) & 1ull) != 0ull;
             const float o = z || acc < 1e-4f ? 0.0f : acc;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rd, q * 4, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rD, q * 4, e0 * HW * 4, 0);
         }
 #pragma unroll
         for (int k = 0; k < (SCALAR_TAIL ? NSF : NS); k++) {
             const int tb = toff[k];
-            if (tb < 0) continue;
+            if (k >= NSF && tb < 0) continue;
             const bool yl = ((yfl >> (2 * k)) & 1u) != 0u, yr = ((yfl >> (2 * k)) & 2u) != 0u;
             const float* p = tile + tb;
             float b[3][6];   // rows dx = -1..1, columns -1..4 (B values)
@@ -501,7 +504,8 @@ void core_group_kernel(CoreStepArgs a) {
             }
             const bool z = ((rsm >> ((senv >> (4 * k)) & 15u)) & 1ull) != 0ull;
             const float4 out = z ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(o[0], o[1], o[2], o[3]);
-            buf_st4(rd, (k * 64 + lane) * 16, out);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out),
+                                                   rD, (k * 64 + lane) * 16, e0 * HW * 4, 0);
         }
         wave_sync();
         cur = nxt;
@@ -534,7 +538,10 @@ void core_group_kernel(CoreStepArgs a) {
 #define FFM_GROUP_G 4
 #endif
 constexpr int kGroupG = FFM_GROUP_G;   // envs per group at large E
-constexpr int kGroupGSmall = 2;        // envs per group when the large-E groups fill less than half the waves
+#ifndef FFM_GROUP_G_SMALL
+#define FFM_GROUP_G_SMALL 2
+#endif
+constexpr int kGroupGSmall = FFM_GROUP_G_SMALL;   // envs per group when the large-E groups fill under half the waves
 
 size_t core_group_smem_bytes(int H, int W, int F, int waves, int G) {
     const int PHW = (H + 2) * (W + 2);

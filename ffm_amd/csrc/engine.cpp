@@ -182,7 +182,7 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     // block kernel), > 0 = block kernel with that many envs per workgroup,
     // -1 = wave kernel, -2 = lane kernel, -3 = group kernel.
     const bool lane_ok = !e->mt && !e->f64 && A <= 32 && W % 4 == 0 && HW <= 256 &&
-                         (long long)d.n_envs * HW * 4 < (1ll << 31);   // 32-bit buffer offsets
+                         ((long long)d.n_envs + 7) * HW * 4 < (1ll << 31);   // 32-bit buffer offsets (padded envs)
     e->group = (d.envs_per_block == 0 || d.envs_per_block == -3) && lane_ok && ffm::core_group_supported(H, W) &&
                ffm::core_group_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
     e->multi = lane_ok && ffm::core_multi_smem_bytes(H, W, e->F, 4) <= 64 * 1024;
@@ -234,9 +234,12 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
     ALLOC(e->d_sff, sff_bytes);
     ALLOC(e->d_free, std::max<size_t>(1, fl.size()) * 2);
     ALLOC(e->d_free_padded, std::max<size_t>(1, fl.size()) * 2);
-    ALLOC(e->d_pos, E * A * 2 + 16);   // + a dword: the lane kernel streams positions as dwords
-    ALLOC(e->d_cnt, E * 4);
-    ALLOC(e->d_dff, E * HW * 4);
+    // pos / cnt / DFF hold whole groups of 8 envs (zeroed padding beyond n_envs): the group kernel
+    // reads and writes a partial last group through whole-array buffer resources (core_group.hip)
+    const size_t Ep = (E + 7) & ~(size_t)7;
+    ALLOC(e->d_pos, Ep * A * 2 + 16);   // + a dword: the lane kernel streams positions as dwords
+    ALLOC(e->d_cnt, Ep * 4);
+    ALLOC(e->d_dff, Ep * HW * 4);
     ALLOC(e->d_eps, E * 4);
     if (e->big || e->block_reset) {
         e->scratch_stride = (ffm::core_big_scratch_bytes(H, W, A, e->F, e->mt) + 255) & ~(size_t)255;
@@ -317,9 +320,9 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
         for (size_t i = 0; i < fl.size(); i++) fp[i] = (uint16_t)((fl[i] / W + 1) * PW + fl[i] % W + 1);
         he = hipMemcpy(e->d_free_padded, fp.data(), fp.size() * 2, hipMemcpyHostToDevice);
     }
-    if (he == hipSuccess) he = hipMemset(e->d_pos, 0xFF, E * A * 2);
-    if (he == hipSuccess) he = hipMemset(e->d_cnt, 0, E * 4);
-    if (he == hipSuccess) he = hipMemset(e->d_dff, 0, E * HW * 4);
+    if (he == hipSuccess) he = hipMemset(e->d_pos, 0xFF, Ep * A * 2);
+    if (he == hipSuccess) he = hipMemset(e->d_cnt, 0, Ep * 4);
+    if (he == hipSuccess) he = hipMemset(e->d_dff, 0, Ep * HW * 4);
     if (he == hipSuccess) he = hipMemset(e->d_eps, 0, E * 4);
     if (he == hipSuccess) he = hipMemset(e->d_ctr, 0, e->ctr_slots * 32);
     if (he == hipSuccess) he = hipMemset(e->d_dbg, 0, 128);

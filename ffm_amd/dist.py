@@ -299,6 +299,7 @@ class TableSync:
             if r != self.rank:
                 self.shard.delta_merge_async(which, gk[r].data_ptr(), ga[r].data_ptr(), gc[r:r + 1].data_ptr(), cap)
         self.bytes_sent += 8 + keys.numel() * 8 + acc.numel() * 8
+        self.received_bytes += (self.world - 1) * (8 + keys.numel() * 8 + acc.numel() * 8)
         if self.adaptive:
             self._observe(which, gc)
 
@@ -377,6 +378,9 @@ class TableSync:
         self.shard.dense_adopt(which, uni.data_ptr())
         self._keep = uni                 # until the adopt kernel (same stream) has read it
         self.bytes_sent += acc.numel() * 8 + present.numel() * 4
+        # a ring all-reduce receives 2 (W - 1) / W of the array; the all-gather W - 1 bitmaps
+        self.received_bytes += (2 * (self.world - 1) * acc.numel() * 8) // self.world + \
+            (self.world - 1) * present.numel() * 4
 
     def _exchange(self, which: str):
         self.exchanges += 1
@@ -474,6 +478,8 @@ class TableSync:
         s.step_tiled_apply(g[0].data_ptr(), g[1].data_ptr(), self.world * s.n_envs)
         self.exchanges += 1
         self.bytes_sent += recs.numel() * recs.element_size() + tst.numel() * tst.element_size()
+        self.received_bytes += (self.world - 1) * (recs.numel() * recs.element_size() +
+                                                   tst.numel() * tst.element_size())
 
     def flush(self):
         """Apply the increments pending since the last apply (sync period K > 1) on every
