@@ -68,7 +68,9 @@ __host__ __device__ inline GroupCarve group_carve(int PHW, int TS, int F) {
     if (o < keys_end) o = keys_end;
     c.words = o; o += (size_t)G * 32 * 4;
     c.posst = o;
-    c.kp = o;    o += a16((size_t)(G * 32 + 1) * 2);
+    // the compaction writes an entry for every lane of every agent chunk (idle lanes too: no
+    // exec-mask branch), so the array spans whole chunks: (G * 32 + 63) / 64 * 64 + 1 entries
+    c.kp = o;    o += a16((size_t)(((G * 32 + 63) / 64) * 64 + 1) * 2);
     c.pend = o;  o += kGroupPendWords * 4;
     c.dummy = o; o += 4;   // the target of the idle lanes' LDS writes (no exec-mask branch per write)
     c.per_wave = a16(o);
@@ -145,6 +147,7 @@ void core_group_kernel(CoreStepArgs a) {
     constexpr int MAXC = (G * 32 + 63) / 64;   // agent chunks per group (A <= 32)
     constexpr int PWORDS = G * 16;             // position dwords per group (A <= 32)
     static_assert(G >= 1 && G <= 8 && HW % 4 == 0 && H + 1 < 128, "group geometry");
+    static_assert(MAXC * 64 >= G * 32 && PWORDS * 4 <= (MAXC * 64 + 1) * 2, "kp spans the chunks; posst fits in it");
     const int A = a.A;
     const int lane = (int)(threadIdx.x & 63);
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
