@@ -411,13 +411,14 @@ def bench_learner(args, world, rank, torch, dist):
         bpe = learner_bytes_per_env_step(H, W, A, D)
         achieved = E * bpe / (step_ms / 1e3) / 1e9
         # PMC HBM bytes of the batch kernel (tools/traffic.sh <out> --config 4|5)
-        traffic = None
+        traffic = traffic_src = None
         tpath = os.path.join(ROOT, "profiles", f"traffic_{H}x{W}_A{A}_E{E}_learn{args.config}.json")
         if os.path.exists(tpath):
             with open(tpath) as f:
                 tj = json.load(f)
             if tj.get("config") == f"{H}x{W}_A{A}_E{E}_learn{args.config}":
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = profile_source(tpath, tj)
         out = {
             "metric": METRIC, "value": agent_steps / elapsed, "unit": "agent-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -459,7 +460,10 @@ def bench_learner(args, world, rank, torch, dist):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                          "traffic_kernel": "learn_batch_kernel (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
                          "bytes_per_launch_algorithmic": E * bpe,
+                         # BASELINE.md 3's form: env-steps/s of the timed windows x the bytes per env-step
+                         "frac_env_rate": E * args.steps / elapsed * bpe / 1e9 / PEAK_HBM_GBS,
                          "note": "whole learning step (all kernels) timed with HIP events"},
             "cpu_baseline": None,
         }
