@@ -95,6 +95,13 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 
 }  // namespace
 
+#ifndef FFM_GROUP_PROBE_VALU
+#define FFM_GROUP_PROBE_VALU 0   // diagnostic builds only
+#endif
+#ifndef FFM_GROUP_PROBE_SALU
+#define FFM_GROUP_PROBE_SALU 0
+#endif
+
 #ifndef FFM_GROUP_ABLATE
 #define FFM_GROUP_ABLATE 0   // diagnostic builds only
 #endif
@@ -203,19 +210,24 @@ void core_group_kernel(CoreStepArgs a) {
         uint32_t p0, p1;
         int c;
     };
+    // past the last group (the loop's final prefetch) the loads go through empty resources:
+    // every lane's access is out of range, no bytes move, and no value is conditionally
+    // defined (a `return` there cost 8-14 VGPRs)
+    const __amdgpu_buffer_rsrc_t rZ = pair_rsrc(a.dff, 0);
     auto load = [&](int gg, GState& st) {
-        if (gg < 0) return;   // wave-uniform: nothing past the last group (the loop ends first)
-        const int e0 = gg * G;
-        st.c = (int)__builtin_amdgcn_raw_buffer_load_b32(rC, lane < G ? lane * 4 : kOOB, e0 * 4, 0);
-        st.p0 = __builtin_amdgcn_raw_buffer_load_b32(rP, lane < PWORDS ? lane * 4 : kOOB, e0 * A * 2, 0);
-        st.p1 = PWORDS > 64 ? __builtin_amdgcn_raw_buffer_load_b32(rP, 64 + lane < PWORDS ? 256 + lane * 4 : kOOB,
+        const bool ok = gg >= 0;
+        const int e0 = ok ? gg * G : 0;
+        const __amdgpu_buffer_rsrc_t rc = ok ? rC : rZ, rp = ok ? rP : rZ, rd = ok ? rD : rZ;
+        st.c = (int)__builtin_amdgcn_raw_buffer_load_b32(rc, lane < G ? lane * 4 : kOOB, e0 * 4, 0);
+        st.p0 = __builtin_amdgcn_raw_buffer_load_b32(rp, lane < PWORDS ? lane * 4 : kOOB, e0 * A * 2, 0);
+        st.p1 = PWORDS > 64 ? __builtin_amdgcn_raw_buffer_load_b32(rp, 64 + lane < PWORDS ? 256 + lane * 4 : kOOB,
                                                                  e0 * A * 2, 0)
                             : 0u;
 #pragma unroll
         for (int k = 0; k < NS; k++) {
             const int q = k * 64 + lane;
             st.d[k] = __builtin_bit_cast(float4,
-                                         __builtin_amdgcn_raw_buffer_load_b128(rD, q < Q ? q * 16 : kOOB, e0 * HW * 4, 0));
+                                         __builtin_amdgcn_raw_buffer_load_b128(rd, q < Q ? q * 16 : kOOB, e0 * HW * 4, 0));
         }
     };
     constexpr int LAD = FFM_GROUP_LADDER;
@@ -226,8 +238,6 @@ void core_group_kernel(CoreStepArgs a) {
         if (mine < most) __builtin_amdgcn_s_sleep(FFM_GROUP_STAGGER);
     }
     GState cur;
-    cur.c = 0;
-    cur.p0 = cur.p1 = 0u;
     load(g < ngroups ? g : -1, cur);
 
     if (LAD >= 1) {
@@ -459,14 +469,26 @@ void core_group_kernel(CoreStepArgs a) {
         // next group's head ------------------------------------------------------------
         if (PF == 0 || LAD < 3) load(gn, nxt);
 
+#if FFM_GROUP_PROBE_VALU > 0 || FFM_GROUP_PROBE_SALU > 0
+        {   // diagnostic issue probes (timing only): N extra VALU / SALU instructions per group
+            uint32_t pv = (uint32_t)lane, ps = (uint32_t)g;
+#pragma unroll
+            for (int i = 0; i < FFM_GROUP_PROBE_VALU; i++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(pv));
+#pragma unroll
+            for (int i = 0; i < FFM_GROUP_PROBE_SALU; i++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(ps));
+            asm volatile("" ::"v"(pv), "s"(ps));
+        }
+#endif
         // ---- update_dff (model/ffm_core.py:106-117): B = c0 * D, A = B + sum c1 * B[nb],
         // then the DFF stores (an env reset this step starts its next episode at zero) ----
         if (SCALAR_TAIL) {     // the last, partial float4 slot as one cell per lane (all lanes busy)
             const int q = 4 * 64 * NSF + lane;                 // the group's cell
             const int s = q / HW, c = q - s * HW, y = c % W;
             const float* p = tile + s * TS + 4 + W + c;
-            const float m0 = p[0], mu = p[-W], md = p[W];
-            const float ml = y == 0 ? 0.0f : p[-1], mr = y == W - 1 ? 0.0f : p[1];
+            // p[-1] / p[1] lie inside the tile at the map's edges too (the zero rows above and
+            // below): read them unconditionally, select the edge's zero (no exec-mask branch)
+            const float m0 = p[0], mu = p[-W], md = p[W], pl = p[-1], pr = p[1];
+            const float ml = y == 0 ? 0.0f : pl, mr = y == W - 1 ? 0.0f : pr;
             // B = c0 * D per operand, then A = B + sum c1 * B[nb] in neighbour order (:106-117)
             const float b0 = a.c0 * m0, bu = a.c0 * mu, bd = a.c0 * md, bl = a.c0 * ml, br = a.c0 * mr;
             float acc = b0;
@@ -474,8 +496,8 @@ void core_group_kernel(CoreStepArgs a) {
             acc = acc + a.c1 * bd;
             acc = acc + a.c1 * bl;
             acc = acc + a.c1 * br;
-            const bool z = ((rsm >> s) & 1ull) != 0ull;
-            const float o = z || acc < 1e-4f ? 0.0f : acc;
+            float o = acc < 1e-4f ? 0.0f : acc;
+            if (rsm && ((rsm >> s) & 1ull)) o = 0.0f;   // rsm wave-uniform and rare
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), rD, q * 4, e0 * HW * 4, 0);
         }
 #pragma unroll
@@ -505,8 +527,10 @@ void core_group_kernel(CoreStepArgs a) {
                 }
                 o[jj] = acc < 1e-4f ? 0.0f : acc;                                     // :116-117
             }
-            const bool z = ((rsm >> ((senv >> (4 * k)) & 15u)) & 1ull) != 0ull;
-            const float4 out = z ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(o[0], o[1], o[2], o[3]);
+            float4 out = make_float4(o[0], o[1], o[2], o[3]);
+            if (rsm) {   // wave-uniform, rare: an env re-placed this step starts its next episode at zero
+                if ((rsm >> ((senv >> (4 * k)) & 15u)) & 1ull) out = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out),
                                                    rD, (k * 64 + lane) * 16, e0 * HW * 4, 0);
         }

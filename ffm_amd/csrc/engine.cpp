@@ -284,7 +284,12 @@ int ffm_engine_create(const ffm_engine_desc* desc, ffm_engine** out) {
             const int per_cu = std::max(1, ffm::core_group_blocks_per_cu(a, d.neighborhood, e->group_g));
             const long long G = e->group_g;
             const long long groups = (d.n_envs + G - 1) / G;
-            e->group_blocks = (int)std::max<long long>(1, std::min<long long>((groups + 3) / 4, (long long)cus * per_cu));
+            // at most 6 blocks (6 waves per SIMD) per CU: the group kernel fits 7 (71 VGPRs), but 7
+            // waves per SIMD step slower (65,536 envs 36.0 vs 33.0 us, 32,768 envs 23.1 vs 21.6 us),
+            // and fewer blocks than 6 per CU are slower too (1,366 blocks 36.5 us; 1,024 blocks at
+            // 32,768 envs 23.6 us): profiles/r06/c2/ab_grid_balance*.log, ab_occupancy7.log
+            const long long bpc = std::min(per_cu, 6);
+            e->group_blocks = (int)std::max<long long>(1, std::min<long long>((groups + 3) / 4, (long long)cus * bpc));
             if (const char* ov = std::getenv("FFM_WAVE_BLOCKS")) {   // diagnostic override of the grid
                 const long long v = std::atoll(ov);
                 if (v > 0) e->group_blocks = (int)std::min<long long>(v, (groups + 3) / 4);
