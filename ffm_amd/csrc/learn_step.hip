@@ -1369,7 +1369,7 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 // the map, SFF and DFF in LDS as well measured slower at config 4, 324 vs 295 us:
 // they are L1/L2 hits, and the staging delays every short-lived workgroup.)
 struct BatchCarve {
-    size_t dff, rows, grid, bits, req, km, ws, total;  // per env
+    size_t dff, rows, grid, bits, req, km, flist, fw, ws, total;  // per env
     size_t shared;                                     // per block: EPB env regions
 };
 // Packed state rows (the 13-cell encoders of ffm_ac_core / ffm_actor_only on maps at most
@@ -1389,6 +1389,10 @@ __host__ __device__ inline BatchCarve batch_carve(int HW, int A, int D, int EPB,
     c.bits = o; o += align16((size_t)((HW + 31) / 32) * 4);
     c.req = o; o += align16((size_t)A * D * 2);
     c.km = o; o += D == 4 ? align16((size_t)A * 4) : 0;   // ffm_actor_only: request directions per agent
+    // ffm_actor_only (D = 4): the contested targets' owners listed for one friction draw each
+    // (flist, fcnt), the winners' ranks by owner request (fw)
+    c.flist = o; o += D == 4 ? align16((size_t)A * D * 2) + 16 : 0;
+    c.fw = o; o += D == 4 ? align16((size_t)A * D) : 0;
     c.ws = o; o += 64;
     c.total = o;
     c.shared = (size_t)EPB * o;
@@ -1416,6 +1420,19 @@ constexpr uint32_t kSaNewH = 1u << 15;
 #define FFM_LBATCH_SMALL_WAVES 8
 #endif
 
+// ffm_actor_only's resolve (D = 4, 32 lanes per env): the friction draw of a contested
+// target depends only on its owner request and its requester count, so the owners are listed
+// and each draw is computed once, by a lane of the list, instead of by every requester of
+// every decision (four wave-wide Philox passes, whichever lanes need them).  0 = the per-decision draws.
+#ifndef FFM_FRICTION_LIST
+#define FFM_FRICTION_LIST 1
+#endif
+
+__device__ __forceinline__ void bk_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int BS, int EPB, int APT, int D, bool DL, int VK = 0, int NB = 4>
 __global__ __launch_bounds__(BS)
 __attribute__((amdgpu_waves_per_eu(EPB > 1 && NB == 4 && D == 4 ? FFM_LBATCH_SMALL_WAVES : FFM_LBATCH_WAVES, 8)))
@@ -1436,6 +1453,9 @@ void learn_batch_kernel(LearnArgs a) {
     // neighbours, 4 stay or off the map: its own cell), read by the resolve phase
     uint32_t* km = reinterpret_cast<uint32_t*>(base + cv.km);
     int* ws = reinterpret_cast<int*>(base + cv.ws);
+    uint16_t* flist = reinterpret_cast<uint16_t*>(base + cv.flist);   // D = 4: contested owners | m << 8
+    int* fcnt = reinterpret_cast<int*>(base + cv.flist + align16((size_t)A * D * 2));
+    uint8_t* fw = reinterpret_cast<uint8_t*>(base + cv.fw);             // D = 4: winner rank by owner
     const long long e = (long long)blockIdx.x * EPB + sub;
     const bool live = e < a.E;
     const uint32_t genv = (uint32_t)(a.env_base + e);
@@ -1499,6 +1519,7 @@ void learn_batch_kernel(LearnArgs a) {
     for (int c = tid; c < A * D; c += LPE) req[c] = kNone16;
     if (D == 4)
         for (int c = tid; c < A; c += LPE) km[c] = 0u;
+    if (D == 4 && tid == 0) *fcnt = 0;
     __syncthreads();
     // Lane slot j of this thread is rank r = tid + j * LPE.  By default rank = agent
     // index; RASTER (global-memory DFF, >= one wave per env) instead hands rank r to
@@ -1732,8 +1753,76 @@ void learn_batch_kernel(LearnArgs a) {
     // Requesters of a target stand on it or next to it; a target's owner is its
     // smallest request seq (= the reference's dict order); every member draws
     // the winner rank from the owner's stream itself.
+    constexpr bool FLIST = FFM_FRICTION_LIST && D == 4 && NB == 4 && LPE <= 64 && 64 % LPE == 0 && LPE * APT * D <= 256;
+    if constexpr (FLIST) {
+        // 1. every decision's requester count m, owner request and rank among the requests;
+        //    the owner of a contested target lists it
+        uint32_t dr[APT][D];
 #pragma unroll
-    for (int j = 0; j < APT; j++) {
+        for (int j = 0; j < APT; j++) {
+            const int i = BK_IA(j);
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                dr[j][d] = 0xFFFFFFFFu;
+                if (tid + j * LPE >= n) continue;
+                const int T = req[i * D + d];
+                if (T == kNone16) continue;
+                const int tx = fdiv(T, a.mW), ty = T - tx * W;
+                int m = 0, owner = 0x7FFF, rank = 0;
+#pragma unroll
+                for (int c5 = 0; c5 < NA; c5++) {
+                    const int cx = c5 < NB ? tx + kNBx[c5] : tx, cy = c5 < NB ? ty + kNBy[c5] : ty;
+                    if (cx < 0 || cx >= H || cy < 0 || cy >= W) continue;
+                    const int b = grid[cx * W + cy] & kGIdx;
+                    if (b == (int)kGIdx) continue;
+                    // see the per-decision form below: one mask read per requester cell
+                    const uint32_t f = (km[b] >> ((c5 < 4 ? (c5 ^ 1) : 4) * 4)) & 15u;
+                    if (!f) continue;
+                    m += __popc(f);
+                    const int sq = b * D + (int)__builtin_ctz(f);
+                    owner = sq < owner ? sq : owner;
+                    rank += b < i ? __popc(f) : b == i ? __popc(f & ((1u << d) - 1u)) : 0;
+                }
+                dr[j][d] = (uint32_t)m | ((uint32_t)rank << 8) | ((uint32_t)owner << 16);
+                if (m > 1 && owner == i * D + d) flist[atomicAdd(fcnt, 1)] = (uint16_t)(owner | (m << 8));
+            }
+        }
+        bk_wave_sync();   // an env's lanes are one wave (LPE divides 64)
+        // 2. one friction draw per listed owner (model/ffm_actor_only.py:360-401)
+        const int nf = *fcnt;
+        for (int c = 0;; c += LPE) {
+            const bool has = c + tid < nf;
+            if (!__any(has)) break;
+            if (has) {
+                const uint32_t en = flist[c + tid];
+                PhiloxStream ps(a.key0, a.key1, a.t, genv, en & 0xFFu, kPurFriction);
+                fw[en & 0xFFu] = (uint8_t)ps.randbelow(en >> 8);
+            }
+        }
+        bk_wave_sync();
+        // 3. every request: won iff its rank is the owner's draw
+#pragma unroll
+        for (int j = 0; j < APT; j++) {
+            int nxj = BK_P(j), clj = -1, wnj = 0;
+            int best_owner = -1, best_won_owner = -1;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const uint32_t v = dr[j][d];
+                if (v == 0xFFFFFFFFu) continue;
+                const int m = (int)(v & 0xFFu), rank = (int)((v >> 8) & 0xFFu), owner = (int)(v >> 16);
+                const int w = m > 1 ? (int)fw[owner] : 0;
+                if (owner > best_owner) { best_owner = owner; clj = m == 1 ? 0 : m - 1; }
+                if (rank == w) {
+                    wnj++;
+                    if (owner > best_won_owner) { best_won_owner = owner; nxj = req[BK_IA(j) * D + d]; }
+                }
+            }
+            sa[j] = (sa[j] & (kSaDecide | kSaNewH)) | ((uint32_t)(clj + 1) << kCS) | ((uint32_t)wnj << 10) |
+                    ((uint32_t)nxj << 16);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < (FLIST ? 0 : APT); j++) {
         const int i = BK_IA(j);
         int nxj = BK_P(j), clj = -1, wnj = 0;
         if (tid + j * LPE < n) {

@@ -298,6 +298,15 @@ def test_philox_config3_64x64_matches_cpu():
                     {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"})
 
 
+@pytest.mark.timeout(600)
+def test_philox_config3_full_size_matches_cpu():
+    """BASELINE config 3 at its full size: 64x64, 512 agents, 8,192 envs (the bench's C3
+    grid and block geometry) for 40 steps, every env bit-exact vs the oracle (round 5 covered
+    this shape only through the bench's CPU leg)."""
+    _philox_compare(64, 64, 512, 8192, 40,
+                    {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"})
+
+
 def test_philox_big_maps_global_scratch():
     """Maps whose env state exceeds the LDS (the block kernel with its grid, DFF tile and
     u32 padded cells in a global scratch region; placement by workgroups): the BASELINE
