@@ -101,6 +101,9 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 #ifndef FFM_GROUP_PROBE_SALU
 #define FFM_GROUP_PROBE_SALU 0
 #endif
+#ifndef FFM_GROUP_PROBE_DUP
+#define FFM_GROUP_PROBE_DUP 0
+#endif
 
 #ifndef FFM_GROUP_ABLATE
 #define FFM_GROUP_ABLATE 0   // diagnostic builds only
@@ -363,6 +366,18 @@ void core_group_kernel(CoreStepArgs a) {
                 grid[live ? s * PHW + pp : kDummy16] =
                     (uint16_t)(DirCodes::kAgent | (uint32_t)al | (sd << 8) | ((pb.z >> 31) << 12));
                 cr[c] = sd | ((to_exit ? 1u : 0u) << 4);
+#if FFM_GROUP_PROBE_DUP
+                if (c == MAXC - 1) {   // diagnostic (timing only): the last chunk's draw and decide again
+                    uint32_t salt;
+                    asm volatile("v_mov_b32 %0, 0" : "=v"(salt));
+                    const uint4 pb2 = philox(make_uint4(a.t, genv, (uint32_t)al + salt, kPurDecide << 28), a.key0,
+                                             a.key1);
+                    bool te2 = false;
+                    const uint32_t slot2 =
+                        lane_decide<NB, true, KD1>(pp, PW, gk, psff, dk, dd0, a.kS32, a.kD32, pb2.x, te2);
+                    asm volatile("" ::"v"(slot2), "v"(pb2.w), "v"(te2 ? 1u : 0u));
+                }
+#endif
             }
         }
         wave_sync();

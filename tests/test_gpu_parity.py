@@ -226,6 +226,27 @@ def test_engine_reset_envs_matches_cpu(H, N, E, epb):
     eng.close()
 
 
+def test_engine_reset_envs_errors():
+    """reset_envs is Philox-only (MT engines draw placements on the host) and checks its mask."""
+    import torch
+    from ffm_amd.data import make_room, l1_sff
+    m = make_room(12, 12)
+    s = l1_sff(m)
+    mt = _engine(map_array=m, sff=s, n_envs=4, n_agents=8, rng="mt", seed=1)
+    with pytest.raises(NotImplementedError, match="MT mode"):
+        mt.reset_envs(torch.ones(4, dtype=torch.uint8, device="cuda"))
+    mt.close()
+    ph = _engine(map_array=m, sff=s, n_envs=4, n_agents=8, rng="philox", seed=1)
+    with pytest.raises(ValueError, match="n_envs"):
+        ph.reset_envs(np.ones(5, np.uint8))
+    ph.reset()
+    before = ph.get_state()
+    ph.reset_envs(np.zeros(4, np.uint8))          # an empty mask re-places nothing
+    after = ph.get_state()
+    assert all(np.array_equal(x, y) for x, y in zip(before, after))
+    ph.close()
+
+
 @pytest.mark.parametrize("epb", [-3, -2, -1, 3])
 @pytest.mark.parametrize("N", [32, 60])
 @pytest.mark.parametrize("params", [
