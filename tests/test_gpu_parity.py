@@ -174,13 +174,14 @@ def test_philox_config2_full_size_matches_cpu(epb):
     assert eps.sum() > 0  # auto-reset exercised
 
 
-@pytest.mark.parametrize("H,N,E,epb", [(12, 32, 65536, 0), (12, 32, 4096, -2), (64, 512, 48, 0)])
+@pytest.mark.parametrize("H,N,E,epb", [(12, 32, 65536, 0), (12, 32, 4096, -2), (64, 512, 48, 0), (110, 60, 6, 0)])
 def test_engine_reset_envs_matches_cpu(H, N, E, epb):
     """reset(env_mask) through the ABI (ffm_engine_reset_envs): mid-run, a random
     third of the envs is re-placed (C2's 65,536 envs on the group kernel, the lane kernel, and
     C3's 64x64 room); the oracle re-places the same envs with reset_philox at the same step
     index.  Positions, counts, DFF bits and episode counters equal the oracle's, before and
-    after the reset, and the unmasked envs are untouched."""
+    after the reset, and the unmasked envs are untouched.  The 110x110 room's free list exceeds
+    the wave reset's LDS, so it re-places through core_block_reset_kernel's masked form."""
     import torch
     from ffm_amd.data import make_room, l1_sff
     from oracle import oracle as O
