@@ -137,7 +137,7 @@ __device__ __forceinline__ int cs_xp1(uint32_t v) { return (int)(v >> 25); }
 #endif
 
 #ifndef FFM_GROUP_WAVES
-#define FFM_GROUP_WAVES 6   // minimum waves per SIMD asked of the register allocator (80 VGPRs at G = 4, no spill)
+#define FFM_GROUP_WAVES 6   // minimum waves per SIMD asked of the register allocator (G = 4 needs 71 VGPRs; the grid holds 6 per SIMD)
 #endif
 
 template <int NB, int HT, int WT, int G, bool KD1>
