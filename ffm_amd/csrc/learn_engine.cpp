@@ -88,6 +88,11 @@ struct ffm_learner {
     ffm::TrajCapture traj{};                 // trajectory capture (n_sel = 0: off)
     bool v_chain = false;                    // LearnArgs::v_chain: a batched step ran since the last
                                              // set_state / V import (agents' s are the last step's s')
+    // The chain holds only if every exit-forced agent wins its exit: true when no exit cell
+    // has two free cells among its neighbours (one possible requester).  Otherwise a loser
+    // stays on a cell whose state the reference inserts as V(s) at the next step although
+    // its V(s') was never looked up (a terminal transition): make_room's Moore exits.
+    bool chain_ok = true;
     int sync_period = 1;                     // tables applied every sync_period-th step
     int since_apply = 0;                     // steps since the last apply
     bool external_sync = false;              // driven by a multi-rank TableSync: no local flush
@@ -350,8 +355,22 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
     }
     if (d.n_agents > (int)fl.size())
         return fail(FFM_E_INVALID, "Cannot take a larger sample than population when 'replace=False'");
+    bool chain_ok = true;
+    for (int i = 0; i < HW && chain_ok; i++) {
+        if (d.map[i] != 3) continue;
+        const int x = i / W, y = i % W;
+        int nfree = 0;
+        for (int dx = -1; dx <= 1; dx++)
+            for (int dy = -1; dy <= 1; dy++) {
+                if ((dx == 0 && dy == 0) || (d.neighborhood == 4 && dx != 0 && dy != 0)) continue;
+                const int u = x + dx, v = y + dy;
+                if (u >= 0 && u < H && v >= 0 && v < W && d.map[u * W + v] == 0) nfree++;
+            }
+        chain_ok = nfree <= 1;
+    }
 
     ffm_learner* l = new ffm_learner();
+    l->chain_ok = chain_ok;
     l->d = d;
     l->d.map = nullptr;
     l->d.sff = nullptr;
@@ -449,8 +468,9 @@ int ffm_learner_create(const ffm_engine_desc* desc, const ffm_learn_desc* learn,
         return cleanup(fail(FFM_E_NOMEM, std::string("hipMalloc (tables): ") + hipGetErrorString(he)));
     {
         const char* ev = getenv("FFM_TILED");
+        // (Neumann or Moore: the tile passes take 5- or 9-value H rows; dense slots < 2^24)
         l->tiled_ok = !l->mt && d.variant == FFM_VARIANT_UNIFIED && dense_by && learn->block_size == 1 &&
-                      d.neighborhood == 4 &&
+                      l->V.cap <= ((size_t)1 << 24) && l->H.cap <= ((size_t)1 << 24) &&
                       ffm::learn_batch_raster(HW, d.agent_capacity, l->D) && !(ev && ev[0] == '0') &&
                       (unsigned long long)E * (unsigned long long)A < (1ull << 31);
     }
@@ -554,7 +574,7 @@ static int phase_local(ffm_learner* l, hipStream_t s) {
         l->hstat_valid = true;
     }
     HIP_TRY(ffm::launch_learn_batch(make_args(l), s));
-    l->v_chain = true;
+    l->v_chain = l->chain_ok;
     l->phase = 1;
     return FFM_OK;
 }
@@ -645,7 +665,7 @@ int ffm_learner_step(ffm_learner* l, int32_t n_steps, void* stream) {
             const bool tt = !l->single_tm && !tstart_t_off();
             if (tt) a.tstart_out = l->d_tstartT;
             HIP_TRY(ffm::launch_learn_batch(a, s));
-            l->v_chain = true;
+            l->v_chain = l->chain_ok;
             a.tstart_out = nullptr;
             if (l->single_tm) {      // records reordered tile-major, then the passes
                 a.ow = 1;
@@ -1054,7 +1074,7 @@ int ffm_learner_step_tiled_local(ffm_learner* l, void* stream) {
     ffm::LearnArgs a = make_args(l);
     a.trecs = l->d_trecs;
     HIP_TRY(ffm::launch_learn_batch(a, s));
-    l->v_chain = true;
+    l->v_chain = l->chain_ok;
     l->phase = 5;
     return FFM_OK;
 }
@@ -1208,7 +1228,7 @@ int ffm_learner_step_owner_local(ffm_learner* l, void* stream) {
     ffm::LearnArgs a = owner_args(l);
     a.trecs = l->d_trecs;
     HIP_TRY(ffm::launch_learn_batch(a, s));
-    l->v_chain = true;
+    l->v_chain = l->chain_ok;
     HIP_TRY(ffm::launch_learn_tile_pack(a, l->d_pe, l->d_ttot, l->d_toff, l->d_hdr, l->d_xcnt,
                                         l->x_opack ? l->x_opack : l->d_opack, s));
     l->phase = 7;

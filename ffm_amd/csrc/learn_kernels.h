@@ -27,16 +27,22 @@ struct LearnRec {
 struct TileRec {
     uint32_t svk;               // V / H slot of s (bits 0-26), H(s) inserted by this rank's step (27; owner
                                 // exchange: the row is new to every other rank), action k (28-31; 15 = none)
-    uint32_t snf;               // V slot of s' (bits 0-27; 0x0FFFFFFF = terminal), wexit (28), coll + 1 (29-31)
+    uint32_t snf;               // V slot of s' (bits 0-26; kTileTerminal = terminal), wexit (27), coll + 1
+                                // (28-31: Moore's up to eight requesters of one target)
     double td;                  // ffm_unified both: the TD error with the step-start V (the actor's td);
                                 // otherwise the TD target r + gamma V(s') (the V pass subtracts V(s))
 };
 constexpr int kTileCells = 4;   // cells per tile: a tile's slots are 256 rank patterns x 4 cells
-constexpr uint32_t kTileNoAct = 15u, kTileTerminal = 0x0FFFFFFFu;
+// Tiled tables are dense: cap = the smallest power of two >= 256 * cells <= 2^24, so every slot
+// is below 2^24 and the 27-bit fields never hold the terminal marker.
+constexpr uint32_t kTileNoAct = 15u, kTileTerminal = 0x07FFFFFFu;
 constexpr uint32_t kTileSlot = 0x07FFFFFFu, kTileNewH = 1u << 27;   // svk: slot bits, new-row flag
-// Owner outputs: an H increment's key is slot | action << 28; bit 31 marks the row's first
-// entry when the row is new this step (receivers insert it; q may then be 0).
-constexpr uint32_t kHoutNew = 1u << 31;
+constexpr int kTileExitBit = 27, kTileCollShift = 28;               // snf: wexit, coll + 1
+// Owner outputs: an H increment's key is slot (bits 0-23) | action << 24 (up to 8: Moore's
+// stay); bit 31 marks the row's first entry when the row is new this step (receivers insert
+// it; q may then be 0).
+constexpr uint32_t kHoutSlot = 0x00FFFFFFu, kHoutNew = 1u << 31;
+constexpr int kHoutActShift = 24;
 
 struct LearnTable {
     // [cap][stride] 64-bit words, one record per slot: the key (~0 = empty), then

@@ -2009,8 +2009,8 @@ void learn_batch_kernel(LearnArgs a) {
             if (vsl >= 0) {
                 TileRec rc;
                 rc.svk = (uint32_t)vsl | (newh ? kTileNewH : 0u) | ((uint32_t)kk << 28);
-                rc.snf = (snv >= 0 ? (uint32_t)snv : kTileTerminal) | ((uint32_t)BK_WEXIT(j) << 28) |
-                         ((uint32_t)(BK_COLL(j) + 1) << 29);
+                rc.snf = (snv >= 0 ? (uint32_t)snv : kTileTerminal) | ((uint32_t)BK_WEXIT(j) << kTileExitBit) |
+                         ((uint32_t)(BK_COLL(j) + 1) << kTileCollShift);
                 rc.td = tdv;
                 a.trecs[e * A + i] = rc;
             }
@@ -2489,7 +2489,8 @@ __device__ __forceinline__ void phase_learn_one(const LearnArgs& a, long long e,
     }
     TileRec rc;
     rc.svk = (uint32_t)sv | ((uint32_t)kk << 28);
-    rc.snf = (sn >= 0 ? (uint32_t)sn : kTileTerminal) | ((uint32_t)wexit << 28) | ((uint32_t)(coll + 1) << 29);
+    rc.snf = (sn >= 0 ? (uint32_t)sn : kTileTerminal) | ((uint32_t)wexit << kTileExitBit) |
+             ((uint32_t)(coll + 1) << kTileCollShift);
     rc.td = td;
     a.trecs[e * A + r] = rc;
 }
@@ -2882,14 +2883,17 @@ __device__ __forceinline__ void hout_reserve(const LearnArgs& a, const int (&n)[
 
 // nw: the row is new this step: its first entry carries kHoutNew (receivers insert the row),
 // and a new row without increments still sends one (q = 0; hout_count counts it).
-__device__ __forceinline__ int hout_count(const long long (&q)[5], bool nw) {
+// NA: values per H row (5 Neumann, 9 Moore).
+template <int NA>
+__device__ __forceinline__ int hout_count(const long long (&q)[NA], bool nw) {
     int n = 0;
 #pragma unroll
-    for (int k = 0; k < 5; k++) n += q[k] != 0 ? 1 : 0;
+    for (int k = 0; k < NA; k++) n += q[k] != 0 ? 1 : 0;
     return n == 0 && nw ? 1 : n;
 }
 
-__device__ __forceinline__ void hout_row(const LearnArgs& a, int base, uint32_t slot, const long long (&q)[5],
+template <int NA>
+__device__ __forceinline__ void hout_row(const LearnArgs& a, int base, uint32_t slot, const long long (&q)[NA],
                                          bool nw) {
     if (!a.hout_n) return;
     const int n = hout_count(q, nw);
@@ -2901,9 +2905,9 @@ __device__ __forceinline__ void hout_row(const LearnArgs& a, int base, uint32_t 
     uint32_t flag = nw ? kHoutNew : 0u;
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < 5; k++)
+    for (int k = 0; k < NA; k++)
         if (q[k] != 0) {
-            a.hout_key[base] = slot | ((uint32_t)k << 28) | flag;
+            a.hout_key[base] = slot | ((uint32_t)k << kHoutActShift) | flag;
             a.hout_q[base] = q[k];
             base++;
             flag = 0u;
@@ -3087,7 +3091,7 @@ void learn_tile_v_kernel(LearnArgs a) {
         atomicAdd(reinterpret_cast<unsigned long long*>(&qs[idx]), (unsigned long long)fx(td));
         if (a.tile_ensure) {     // another rank's agent: its s and s' join this rank's V
             dense_ensure(a.V, sv, dense_key(sv, qsh, Q, a.V.dense_by));
-            const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+            const uint32_t sn = rc.snf & kTileSlot;
             if (sn != kTileTerminal) dense_ensure(a.V, sn, dense_key(sn, qsh, Q, a.V.dense_by));
         }
     };
@@ -3176,6 +3180,7 @@ void learn_tile_v_kernel(LearnArgs a) {
 }
 
 // Exact min / max / non-finite of one tile's present H rows (a block-wide scan).
+template <int NA>
 __device__ void tile_rescan(const LearnArgs& a, int t, double* smn, double* smx, int* sfl) {
     constexpr int NS = 256 * kTileCells;
     const int tid = (int)threadIdx.x, wv = tid >> 6;
@@ -3189,7 +3194,7 @@ __device__ void tile_rescan(const LearnArgs& a, int t, double* smn, double* smx,
         any = 1;
         const double* vp = tval(a.Ht, slot);
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
+        for (int k = 0; k < NA; k++) {
             const double v = vp[k];
             nf |= !__builtin_isfinite(v);
             mn = v < mn ? v : mn;
@@ -3244,7 +3249,7 @@ __device__ __forceinline__ void tile_h_vpair(const LearnArgs& a, const TileRec& 
     vn = 0.0;
     vs = 0.0;
     if (a.mode != kModeActor || (rc.svk >> 28) == kTileNoAct) return;
-    const uint32_t sn = rc.snf & 0x0FFFFFFFu;
+    const uint32_t sn = rc.snf & kTileSlot;
     if (sn != kTileTerminal) vn = tval(a.V, sn)[0];
     vs = tval(a.V, sv)[0];
 }
@@ -3254,8 +3259,8 @@ __device__ __forceinline__ long long tile_h_q(const LearnArgs& a, const TileRec&
     double td = rc.td;
     if (a.mode == kModeActor) {     // _get_td_errors with the updated V (model/ffm_unified.py:568-574)
         double r0 = a.step_penalty;
-        if ((rc.snf >> 28) & 1u) r0 = r0 + a.exit_reward;
-        const int coll = (int)(rc.snf >> 29) - 1;
+        if ((rc.snf >> kTileExitBit) & 1u) r0 = r0 + a.exit_reward;
+        const int coll = (int)(rc.snf >> kTileCollShift) - 1;
         if (coll >= 0) r0 = r0 + (double)coll * a.collision_penalty;
         td = (r0 + a.gamma * vn) - vs;
     }
@@ -3263,11 +3268,12 @@ __device__ __forceinline__ long long tile_h_q(const LearnArgs& a, const TileRec&
 }
 
 // A touched row: new values, the summary's bounds and staleness.
-__device__ __forceinline__ void tile_h_apply(double* vp, const long long (&q)[5], const double* old5, TileHCtx& c) {
+template <int NA>
+__device__ __forceinline__ void tile_h_apply(double* vp, const long long (&q)[NA], const double* oldv, TileHCtx& c) {
     c.flags |= 4;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const double old = old5[k];
+    for (int k = 0; k < NA; k++) {
+        const double old = oldv[k];
         double v = old;
         if (q[k] != 0) {
             v = v + (double)q[k] * (1.0 / kFxOne);
@@ -3335,16 +3341,18 @@ __device__ __forceinline__ void tile_h_end(const LearnArgs& a, int t, TileHCtx& 
 //   3. (barrier) owners read their rows and apply them.
 // A tile whose records need more than one window is queued (tcand, count reset by
 // learn_tile_v_kernel) for learn_tile_h_wide_kernel.
-constexpr int kTilePairs = 256 * kTileCells * 5;
+// (slot, action) pairs of a tile: 256 * kTileCells rows of NA values
+template <int NA>
+constexpr int tile_pairs() { return 256 * kTileCells * NA; }
 
 #ifndef FFM_TILE_H_WAVES
 #define FFM_TILE_H_WAVES 1
 #endif
 
-template <bool TM>
+template <bool TM, int NA>
 __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(FFM_TILE_H_WAVES, 8)))
 void learn_tile_h_kernel(LearnArgs a) {
-    constexpr int NS = 256 * kTileCells;
+    constexpr int NS = 256 * kTileCells, kTilePairs = tile_pairs<NA>();
     static_assert(kTileList * 4 <= kTilePairs * 2, "the window's list fits the pair map");
     __shared__ long long hq[kTileList];             // per touched (slot, action) pair
     // pair -> index into hq (valid where pbit is set); until the records are loaded, the
@@ -3387,7 +3395,7 @@ void learn_tile_h_kernel(LearnArgs a) {
     __syncthreads();                        // the list is read: its LDS becomes the pair map
     bool own[kTileJ], pown[kTileJ];
     int ix[kTileJ], pr[kTileJ];
-    double hv[kTileJ][5], vn[kTileJ], vs[kTileJ];
+    double hv[kTileJ][NA], vn[kTileJ], vs[kTileJ];
 #pragma unroll
     for (int j = 0; j < kTileJ; j++) {     // owners' rows and the V reads, all in flight
         own[j] = false;
@@ -3403,7 +3411,7 @@ void learn_tile_h_kernel(LearnArgs a) {
         if (a.tile_ensure) dense_ensure(a.Ht, sv, dense_key(sv, qsh, Q, a.Ht.dense_by));
         const int act = (int)(rc[j].svk >> 28);
         if (act != (int)kTileNoAct) {
-            pr[j] = ix[j] * 5 + act;
+            pr[j] = ix[j] * NA + act;
             const uint32_t pb = 1u << (pr[j] & 31);
             pown[j] = !(atomicOr(&pbit[pr[j] >> 5], pb) & pb);
         }
@@ -3431,12 +3439,12 @@ void learn_tile_h_kernel(LearnArgs a) {
         if (!own[j]) continue;
         const double* vp = tval(a.Ht, rc[j].svk & kTileSlot);
 #pragma unroll
-        for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
+        for (int k = 0; k < NA; k++) hv[j][k] = vp[k];
     }
-    auto row_q = [&](int j, long long (&q)[5]) {
+    auto row_q = [&](int j, long long (&q)[NA]) {
 #pragma unroll
-        for (int kk = 0; kk < 5; kk++) {
-            const int p = ix[j] * 5 + kk;
+        for (int kk = 0; kk < NA; kk++) {
+            const int p = ix[j] * NA + kk;
             q[kk] = ((pbit[p >> 5] >> (p & 31)) & 1u) ? hq[pid[p]] : 0;
         }
     };
@@ -3450,7 +3458,7 @@ void learn_tile_h_kernel(LearnArgs a) {
         // a row another rank's step inserted joins this rank's table here, and goes out flagged
         nw[j] = TM && ((newb[ix[j] >> 5] >> (ix[j] & 31)) & 1u);
         if (TM && a.hout_n) {
-            long long q[5];
+            long long q[NA];
             row_q(j, q);
             hn[j] = hout_count(q, nw[j]);
         }
@@ -3459,7 +3467,7 @@ void learn_tile_h_kernel(LearnArgs a) {
 #pragma unroll
     for (int j = 0; j < kTileJ; j++) {
         if (!own[j]) continue;
-        long long q[5];
+        long long q[NA];
         row_q(j, q);
         const uint32_t sl = rc[j].svk & kTileSlot;
         if (nw[j]) dense_ensure(a.Ht, sl, dense_key(sl, qsh, Q, a.Ht.dense_by));
@@ -3472,10 +3480,10 @@ void learn_tile_h_kernel(LearnArgs a) {
 // The general form, for the tiles the fast form queued (more than one window of
 // records: a crowded tile, or more than 512 envs): every (slot, action) pair of the
 // tile has its word (40 KB), records stream through windows, then the touched rows.
-template <bool TM>
+template <bool TM, int NA>
 __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnArgs a) {
     constexpr int NS = 256 * kTileCells;
-    __shared__ long long hq[NS * 5];
+    __shared__ long long hq[NS * NA];
     __shared__ uint32_t touched[NS / 32];
     __shared__ uint32_t newb[NS / 32];
     __shared__ double smn[kTileWaves], smx[kTileWaves];
@@ -3489,7 +3497,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
     const int n = a.tcand[0];
     for (int ci = (int)blockIdx.x; ci < n; ci += (int)gridDim.x) {
         const int t = a.tcand[1 + ci], c0 = t * kTileCells, kt = TM ? own_local(a, t) : t;
-        for (int i = tid; i < NS * 5; i += kTileThreads) hq[i] = 0;
+        for (int i = tid; i < NS * NA; i += kTileThreads) hq[i] = 0;
         for (int i = tid; i < NS / 32; i += kTileThreads) {
             touched[i] = 0u;
             newb[i] = 0u;
@@ -3513,7 +3521,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
                     if (rc[j].svk & kTileNewH) atomicOr(&newb[idx >> 5], 1u << (idx & 31));
                     const int act = (int)(rc[j].svk >> 28);
                     if (act == (int)kTileNoAct) continue;
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + act]),
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * NA + act]),
                               (unsigned long long)tile_h_q(a, rc[j], vn[j], vs[j]));
                 }
             }
@@ -3529,13 +3537,13 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
                 if (act == (int)kTileNoAct) return;
                 double vn, vs;
                 tile_h_vpair(a, rc, sv, vn, vs);
-                atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * 5 + act]),
+                atomicAdd(reinterpret_cast<unsigned long long*>(&hq[idx * NA + act]),
                           (unsigned long long)tile_h_q(a, rc, vn, vs));
             });
         }
         // every touched row's loads are issued before the first is used (one latency, not four)
         constexpr int kPer = NS / kTileThreads;
-        double hv[kPer][5];
+        double hv[kPer][NA];
         bool tch[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
@@ -3544,7 +3552,7 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
             if (tch[j]) {
                 const double* vp = tval(a.Ht, (size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
 #pragma unroll
-                for (int k = 0; k < 5; k++) hv[j][k] = vp[k];
+                for (int k = 0; k < NA; k++) hv[j][k] = vp[k];
             }
         }
         int hn[kPer], hb[kPer];
@@ -3555,9 +3563,9 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
             hn[j] = 0;
             nw[j] = TM && tch[j] && ((newb[i >> 5] >> (i & 31)) & 1u);
             if (TM && a.hout_n && tch[j]) {
-                long long q[5];
+                long long q[NA];
 #pragma unroll
-                for (int kk = 0; kk < 5; kk++) q[kk] = hq[i * 5 + kk];
+                for (int kk = 0; kk < NA; kk++) q[kk] = hq[i * NA + kk];
                 hn[j] = hout_count(q, nw[j]);
             }
         }
@@ -3567,9 +3575,9 @@ __global__ __launch_bounds__(kTileThreads) void learn_tile_h_wide_kernel(LearnAr
             const int i = tid + j * kTileThreads;
             if (!tch[j]) continue;
             const uint32_t sl = (uint32_t)((size_t)(i / kTileCells) * Q + (size_t)(c0 + i % kTileCells));
-            long long q[5];
+            long long q[NA];
 #pragma unroll
-            for (int kk = 0; kk < 5; kk++) q[kk] = hq[i * 5 + kk];
+            for (int kk = 0; kk < NA; kk++) q[kk] = hq[i * NA + kk];
             if (nw[j]) dense_ensure(a.Ht, sl, dense_key(sl, qsh, Q, a.Ht.dense_by));
             tile_h_apply(tval(a.Ht, sl), q, hv[j], c);
             if (TM) hout_row(a, hb[j], sl, q, nw[j]);
@@ -3781,11 +3789,12 @@ void launch_tile_cands(const LearnArgs& a, hipStream_t s) {
     learn_tile_cand_list_kernel<<<dim3(nb), dim3(kCandPartThreads), 0, s>>>(a);
 }
 
+template <int NA>
 __global__ __launch_bounds__(kTileThreads) void learn_tile_rescan_kernel(LearnArgs a) {
     __shared__ double smn[kTileWaves], smx[kTileWaves];
     __shared__ int sfl[kTileWaves];
     const int n = a.tcand[0];
-    for (int c = (int)blockIdx.x; c < n; c += (int)gridDim.x) tile_rescan(a, a.tcand[1 + c], smn, smx, sfl);
+    for (int c = (int)blockIdx.x; c < n; c += (int)gridDim.x) tile_rescan<NA>(a, a.tcand[1 + c], smn, smx, sfl);
 }
 
 // The tiles' summaries -> the statistics the next step's actor reads (hstat): the
@@ -4080,14 +4089,15 @@ __global__ __launch_bounds__(256) void learn_h_deltas_kernel(LearnTable T, const
             }
 #pragma unroll
             for (int j = 0; j < kApplyJ; j++) {
-                const uint32_t slot = k[j] & 0x0FFFFFFFu;
+                const uint32_t slot = k[j] & kHoutSlot;
                 if (live[j] && (k[j] & kHoutNew)) dense_ensure(T, slot, dense_key(slot, qsh, Q, T.dense_by));
                 live[j] = live[j] && d[j] != 0;
-                if (live[j]) v[j] = tval(T, slot)[(k[j] >> 28) & 7u];
+                if (live[j]) v[j] = tval(T, slot)[(k[j] >> kHoutActShift) & 15u];
             }
 #pragma unroll
             for (int j = 0; j < kApplyJ; j++)
-                if (live[j]) tval(T, k[j] & 0x0FFFFFFFu)[(k[j] >> 28) & 7u] = v[j] + (double)d[j] * (1.0 / kFxOne);
+                if (live[j])
+                    tval(T, k[j] & kHoutSlot)[(k[j] >> kHoutActShift) & 15u] = v[j] + (double)d[j] * (1.0 / kFxOne);
         }
     }
 }
@@ -4878,6 +4888,22 @@ bool learn_batch_raster(int HW, int A, int D) {
     return true;                                     // 1024-lane workgroups, DFF in global memory
 }
 
+// The H passes and the rescan for the table's row width (NA: 5 Neumann, 9 Moore).
+template <bool TM, int NA>
+static void launch_tile_h_na(const LearnArgs& a, unsigned tgrid, unsigned nresc, hipStream_t s) {
+    learn_tile_h_kernel<TM, NA><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
+    learn_tile_h_wide_kernel<TM, NA><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+}
+template <bool TM>
+static void launch_tile_h(const LearnArgs& a, unsigned tgrid, unsigned nresc, hipStream_t s) {
+    if (a.nb == 8) launch_tile_h_na<TM, 9>(a, tgrid, nresc, s);
+    else launch_tile_h_na<TM, 5>(a, tgrid, nresc, s);
+}
+static void launch_tile_rescan(const LearnArgs& a, unsigned nresc, hipStream_t s) {
+    if (a.nb == 8) learn_tile_rescan_kernel<9><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    else learn_tile_rescan_kernel<5><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+}
+
 // One tiled step's table work: V, then (actor modes) H and the statistics.  With
 // init_stats, only the per-tile statistics of the current H (no records).
 hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s) {
@@ -4885,7 +4911,7 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
     const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
     if (init_stats) {
         learn_tile_cand_kernel<<<dim3(1), dim3(kCandThreads), 0, s>>>(a, 1);
-        learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        launch_tile_rescan(a, nresc, s);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
         return hipGetLastError();
     }
@@ -4893,15 +4919,10 @@ hipError_t launch_learn_tiles(const LearnArgs& a, bool init_stats, hipStream_t s
     if (a.thdr) learn_tile_v_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
     else learn_tile_v_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
     if (actor) {
-        if (a.thdr) {
-            learn_tile_h_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-            learn_tile_h_wide_kernel<true><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
-        } else {
-            learn_tile_h_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-            learn_tile_h_wide_kernel<false><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
-        }
+        if (a.thdr) launch_tile_h<true>(a, tgrid, nresc, s);
+        else launch_tile_h<false>(a, tgrid, nresc, s);
         launch_tile_cands(a, s);
-        learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        launch_tile_rescan(a, nresc, s);
         learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     }
     return hipGetLastError();
@@ -4926,10 +4947,9 @@ hipError_t launch_learn_tiles_reset(const LearnArgs& a, const LearnArgs& ra, hip
         if (e != hipSuccess) return e;
     }
     learn_tile_v_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-    learn_tile_h_kernel<false><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-    learn_tile_h_wide_kernel<false><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    launch_tile_h<false>(a, tgrid, nresc, s);
     launch_tile_cands(a, s);
-    learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    launch_tile_rescan(a, nresc, s);
     learn_tile_final_reset_kernel<<<dim3((unsigned)(1 + ra.E)), dim3(kResetBS), smem, s>>>(a, ra);
     return hipGetLastError();
 }
@@ -4963,8 +4983,7 @@ hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStrea
     const unsigned nresc = (unsigned)(a.NTk < 2048 ? (a.NTk > 0 ? a.NTk : 1) : 2048);
     if (a.hout_n) (void)hipMemsetAsync(a.hout_n, 0, 8, s);
     if (a.NTk > 0) {
-        learn_tile_h_kernel<true><<<dim3(tgrid), dim3(kTileThreads), 0, s>>>(a);
-        learn_tile_h_wide_kernel<true><<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+        launch_tile_h<true>(a, tgrid, nresc, s);
         learn_tsum_pack_kernel<<<dim3((unsigned)((a.NTk + 255) / 256)), dim3(256), 0, s>>>(a, tsum);
     }
     return hipGetLastError();
@@ -4973,7 +4992,7 @@ hipError_t launch_learn_tiles_owner_h(const LearnArgs& a, double* tsum, hipStrea
 hipError_t launch_learn_tile_stats(const LearnArgs& a, hipStream_t s) {
     const unsigned nresc = (unsigned)(a.NT < 2048 ? a.NT : 2048);
     launch_tile_cands(a, s);
-    learn_tile_rescan_kernel<<<dim3(nresc), dim3(kTileThreads), 0, s>>>(a);
+    launch_tile_rescan(a, nresc, s);
     learn_tile_final_kernel<<<dim3(1), dim3(256), 0, s>>>(a);
     return hipGetLastError();
 }

@@ -79,6 +79,12 @@ def _tiles_of(shard) -> int:
     return (h * w + 3) // 4
 
 
+def _row_width(shard, which: str) -> int:
+    """Accumulator words per table entry: V 2 (sum of td, visits), H one per action (5 with
+    the Neumann neighbourhood, 9 with Moore's)."""
+    return 2 if which == "V" else int(getattr(shard, "n_actions", 5))
+
+
 class OwnerCaps:
     """Fixed sizes of the owner-sharded exchange (records per destination block, V values and H
     increments per rank and step), so a step's collectives are queued without waiting for the
@@ -93,7 +99,7 @@ class OwnerCaps:
     exact_floor = 1 << 16    # records: 1 MB per destination block
 
     def __init__(self, world: int, e_max: int, agents: int, n_tiles: int, fixed=None, headroom=(1.25, 1.5, 1.5),
-                 adapt_every: int = 8, lag: int = 4, granule: int = 4096):
+                 adapt_every: int = 8, lag: int = 4, granule: int = 4096, actions: int = 5):
         # records per destination move slowly (agents are conserved, the rows dealt round-robin);
         # the V / H output counts follow the crowding of the rooms: more headroom
         self.world, self.granule = int(world), int(granule)
@@ -102,7 +108,8 @@ class OwnerCaps:
         self.e_max = int(e_max)
         ntk = max(owner_tiles(int(n_tiles), self.world, q) for q in range(self.world))
         self.vmax = max(1, ntk * 1024)                       # slots one rank owns
-        self.hmax = 5 * self.vmax
+        self.actions = int(actions)                          # H row values: 5 Neumann, 9 Moore
+        self.hmax = self.actions * self.vmax
         self.adaptive = fixed is None
         if fixed is not None:
             self.rmax = max(1, self.e_max * int(agents))
@@ -124,7 +131,7 @@ class OwnerCaps:
         if self.adaptive:
             r0 = min(self.rmax, max(self.rfloor, self._round(2.0 * self.rmax / self.world)))
             v0 = min(self.vmax, self.world * r0)
-            self.caps = (r0, v0, min(self.hmax, 5 * v0))
+            self.caps = (r0, v0, min(self.hmax, self.actions * v0))
         self.max_seen = [0, 0, 0]
         self.seen = []
         self.n = 0
@@ -267,7 +274,8 @@ class TableSync:
             # the exchange sizes are fixed per step (no host sync inside a step): initial
             # capacities from the shapes, then the counts observed (identical on every rank)
             self.ocaps = OwnerCaps(self.world, -int(v[3].item()), int(getattr(shard, "A", 0)),
-                                   int(getattr(shard, "NT", 0)) or _tiles_of(shard), fixed=owner_caps)
+                                   int(getattr(shard, "NT", 0)) or _tiles_of(shard), fixed=owner_caps,
+                                   actions=_row_width(shard, "H"))
             self.ocaps.apply([shard])
         self.backend = dist.get_backend(group)
         self.received_bytes = 0        # per rank, summed over exchanges (owner mode)
@@ -278,7 +286,7 @@ class TableSync:
     def _record_buffers(self, which: str):
         b = self.bufs.get(which)
         if b is None or b[0].shape[0] != self.caps[which]:
-            width, cap, w, dev = (2 if which == "V" else 5), self.caps[which], self.world, self.device
+            width, cap, w, dev = _row_width(self.shard, which), self.caps[which], self.world, self.device
             b = (torch.zeros(cap, dtype=torch.int64, device=dev),
                  torch.zeros((cap, width), dtype=torch.int64, device=dev),
                  torch.zeros(1, dtype=torch.int64, device=dev),
@@ -614,7 +622,8 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
         if st is None or st[0] != W:
             for q, s in enumerate(shards):
                 s.set_tile_owners(W, q)
-            caps = OwnerCaps(W, max(s.n_envs for s in shards), shards[0].A, _tiles_of(shards[0]), fixed=owner_caps)
+            caps = OwnerCaps(W, max(s.n_envs for s in shards), shards[0].A, _tiles_of(shards[0]), fixed=owner_caps,
+                             actions=_row_width(shards[0], "H"))
             caps.apply(shards)
             st = (W, caps, {})
             _owner_send_buffers(shards, caps, st[2])
@@ -638,7 +647,7 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
         return
 
     def export_async(s, which):
-        width = 2 if which == "V" else 5
+        width = _row_width(s, which)
         k = torch.zeros(capacity, dtype=torch.int64, device=device)
         a = torch.zeros((capacity, width), dtype=torch.int64, device=device)
         c = torch.zeros(1, dtype=torch.int64, device=device)
@@ -646,7 +655,7 @@ def step_coupled(shards, n_steps: int = 1, device=None, capacity: int = 1 << 16,
         return k, a, c
 
     def export(s, which):
-        width = 2 if which == "V" else 5   # accumulator words (V: sum of td, visits)
+        width = _row_width(s, which)   # accumulator words (V: sum of td, visits)
         cap = capacity
         while True:
             k = torch.empty(cap, dtype=torch.int64, device=device)

@@ -133,18 +133,21 @@ def _random_rank_table(H, W, bs, seed=0, frac=0.6, width=5):
 
 
 def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
-                    nthreads=16, sff_dtype=np.float32, log2_cap=22, chunks=1, reset_at=None):
+                    nthreads=16, sff_dtype=np.float32, log2_cap=22, chunks=1, reset_at=None, expect_tiled=None,
+                    exit_pos=None):
     """reset_at = (T1, fraction): after T1 steps a random fraction of the envs is re-placed
     through Learner.reset_envs (the CPU side: reset_philox at step index T1 + 1), then the
-    remaining T - T1 steps run."""
+    remaining T - T1 steps run.  expect_tiled: assert the learner's step path (tiled or not)."""
     from ffm_amd.data import make_room, l1_sff
     from oracle import learn as LO
     from oracle import oracle as O
-    m = make_room(H, W)
+    m = make_room(H, W, exit_pos)
     s = l1_sff(m).astype(sff_dtype)
     A = A or N
     L = _learner(m, s, variant, n_envs=E, n_agents=N, agent_capacity=A, mode=mode, params=params,
                  rng="philox", seed=seed, auto_reset=True, max_steps=max_steps, env_base=env_base)
+    if expect_tiled is not None:
+        assert L.tiled == expect_tiled
     cpu = LO.Learn(m, s, variant, mode, params, log2_cap=log2_cap)
     if variant == "trained":
         hk, hv = _random_rank_table(H, W, int(params.get("block_size", 5)), seed=seed,
@@ -294,6 +297,36 @@ def test_learner_philox_tiled_step_matches_cpu(mode):
                     max_steps=25, seed=6, env_base=77)
 
 
+@pytest.mark.parametrize("mode", ["critic_only", "actor_only", "both"])
+def test_learner_philox_tiled_moore_step_matches_cpu(mode):
+    """The tiled step with the Moore neighbourhood (model/ffm_unified.py:173-185): records
+    carry nine moves and up to eight requesters of a target, the tile passes sum and apply
+    nine-value H rows (and rescan them for the statistics).  Positions, DFF, V and H equal
+    the CPU restatement bit for bit; a square room, then an odd one with spare capacity."""
+    p = {"epsilon": 0.1, "block_size": 1, "neighborhood": "moore"}
+    _philox_compare("unified", mode, p, 64, 64, 600, 16, 30, max_steps=20, seed=4, expect_tiled=True)
+    _philox_compare("unified", mode, dict(p, k_A=3.0, step_penalty=-1.0), 48, 40, 300, 24, 45, A=320,
+                    max_steps=25, seed=6, env_base=77, expect_tiled=True)
+
+
+@pytest.mark.parametrize("nbh,mode", [("neumann", "critic_only"), ("neumann", "actor_only"),
+                                      ("moore", "critic_only"), ("moore", "both")])
+def test_learner_philox_contested_exits_match_cpu(nbh, mode):
+    """Exit-forced agents that lose their exit (model/ffm_unified.py:326-336: every agent next
+    to an exit requests it; one requester enters, the others stay): the reference reads their
+    V(s) at the next step although it never looked their V(s') up (a terminal transition), so
+    the batch kernel inserts every V(s) for such maps instead of trusting the chain of last
+    step's s' (LearnArgs::v_chain).  An exit inside the room (four or eight requesters) and
+    the wall exit under Moore (three), on the tiled and the per-env shapes."""
+    p = {"epsilon": 0.1, "block_size": 1, "neighborhood": nbh}
+    _philox_compare("unified", mode, p, 40, 40, 300, 16, 40, max_steps=30, seed=5, exit_pos=(20, 20),
+                    expect_tiled=True)
+    _philox_compare("unified", mode, p, 24, 24, 60, 64, 40, max_steps=30, seed=6, exit_pos=(11, 13),
+                    expect_tiled=False)
+    if nbh == "moore":
+        _philox_compare("unified", mode, p, 24, 24, 200, 32, 40, max_steps=30, seed=7)
+
+
 @pytest.mark.parametrize("mode", ["actor_only", "both"])
 def test_learner_philox_phase_split_step_matches_cpu(monkeypatch, mode):
     """The phase-split batch step (prep / decide / resolve / learn launches,
@@ -322,17 +355,18 @@ def test_learner_philox_column_stencil_shapes(H, W):
     _philox_compare("unified", "actor_only", p, H, W, 300, 6, 20, max_steps=15, seed=5)
 
 
-@pytest.mark.parametrize("n,N,T", [(520, 600, 8), (300, 3000, 6)])
-def test_learner_tiled_general_tile_pass_equals_accumulators(monkeypatch, n, N, T):
+@pytest.mark.parametrize("n,N,T,nbh", [(520, 600, 8, "neumann"), (300, 3000, 6, "neumann"), (520, 600, 8, "moore"),
+                                       (300, 3000, 6, "moore")])
+def test_learner_tiled_general_tile_pass_equals_accumulators(monkeypatch, n, N, T, nbh):
     """The tile passes' general form (records beyond one window: more than 512 envs, or a
     crowded tile with more than 1,024 records; the fast form holds one window in
     registers) against the accumulator path (FFM_TILED=0) on the same inputs: states,
-    V and H bit for bit."""
+    V and H bit for bit (Neumann's five-value and Moore's nine-value rows)."""
     from ffm_amd.data import make_room, l1_sff
     m = make_room(64, 64)
     s = l1_sff(m)
-    kw = dict(mode="actor_only", params={"epsilon": 0.1, "block_size": 1}, rng="philox", seed=12,
-              auto_reset=True, max_steps=15)
+    kw = dict(mode="actor_only", params={"epsilon": 0.1, "block_size": 1, "neighborhood": nbh}, rng="philox",
+              seed=12, auto_reset=True, max_steps=15)
     tiled = _learner(m, s, "unified", n_envs=n, n_agents=N, **kw)
     monkeypatch.setenv("FFM_TILED", "0")
     acc = _learner(m, s, "unified", n_envs=n, n_agents=N, **kw)
@@ -412,20 +446,23 @@ def test_learner_tiled_shards_equal_one_learner(mode):
         L.close()
 
 
-@pytest.mark.parametrize("mode,world,N", [("actor_only", 3, 600), ("both", 2, 600), ("critic_only", 3, 600),
-                                          ("actor_only", 1, 600), ("both", 3, 1500)])
-def test_learner_owner_shards_equal_one_learner(mode, world, N):
+@pytest.mark.parametrize("mode,world,N,nbh", [("actor_only", 3, 600, "neumann"), ("both", 2, 600, "neumann"),
+                                              ("critic_only", 3, 600, "neumann"), ("actor_only", 1, 600, "neumann"),
+                                              ("both", 3, 1500, "neumann"), ("actor_only", 3, 600, "moore"),
+                                              ("both", 2, 1500, "moore")])
+def test_learner_owner_shards_equal_one_learner(mode, world, N, nbh):
     """The owner-sharded tiled step (TableSync's exchange for tiled learners,
     coupled in one process): the 1,024 tiles of a 64x64 room are dealt to the shards in
     chunks of 64, each shard sums only its own tiles' records from every shard (all-to-all),
     adopts the others' new slots, and takes the others' updated V values, H increments and
     tile summaries.  Shards of unequal size (envs 7 / 5 / 4) end with the tables (values and
-    key sets) and env states of one learner stepping all envs, bit for bit."""
+    key sets) and env states of one learner stepping all envs, bit for bit (Neumann, and
+    Moore's nine-value rows: H increments keyed with actions up to 8)."""
     from ffm_amd.data import make_room, l1_sff
     from ffm_amd.dist import step_coupled
     m = make_room(64, 64)
     s = l1_sff(m)
-    p = {"epsilon": 0.1, "block_size": 1}
+    p = {"epsilon": 0.1, "block_size": 1, "neighborhood": nbh}
     sizes = {1: [16], 2: [9, 7], 3: [7, 5, 4]}[world]
     n, T = sum(sizes), 30
     kw = dict(mode=mode, params=p, rng="philox", seed=8, auto_reset=True, max_steps=20)
@@ -597,20 +634,23 @@ def test_learner_unified_dense_table_rejects_foreign_keys():
     L.close()
 
 
-@pytest.mark.parametrize("variant,mode,sync,dense", [v + (1, False) for v in VARIANTS] + [
-    (("unified", "actor_only") + (1, True)), (("unified", "both") + (4, True)),
-    (("unified", "critic_only") + (4, True)), (("actor_only", None) + (4, False))])
-def test_learner_coupled_shards_equal_one_learner(variant, mode, sync, dense):
+@pytest.mark.parametrize("variant,mode,sync,dense,nbh", [v + (1, False, "neumann") for v in VARIANTS] + [
+    ("unified", "actor_only", 1, True, "neumann"), ("unified", "both", 4, True, "neumann"),
+    ("unified", "critic_only", 4, True, "neumann"), ("actor_only", None, 4, False, "neumann"),
+    ("unified", "actor_only", 1, False, "moore"), ("actor_only", None, 4, False, "moore"),
+    ("unified", "both", 1, True, "moore")])
+def test_learner_coupled_shards_equal_one_learner(variant, mode, sync, dense, nbh):
     """Multi-GPU contract on one device: three Learner shards (env_base offsets) stepped
     through ffm_amd.dist.step_coupled (delta export -> merge of the others' records ->
     apply; dense: summed fixed-point accumulators + presence union) end every sync step
     with the tables of ONE learner holding all envs at the same table sync period, bit
-    for bit, and the same env states."""
+    for bit, and the same env states.  Moore: the H records carry nine increments."""
     from ffm_amd.data import make_room, l1_sff
     from ffm_amd.dist import shard_range, step_coupled
     m = make_room(12, 12)
     s = l1_sff(m)
     p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    p["neighborhood"] = nbh
     n, N, T = 3001, 32, 60
     kw = dict(mode=mode, params=p, rng="philox", seed=21, auto_reset=True, max_steps=40)
     one = _learner(m, s, variant, n_envs=n, n_agents=N, **kw)
