@@ -196,7 +196,8 @@ def main():
         achieved = E * bytes_per_env_step / mean_kernel_s / 1e9
         traffic = traffic_src = None
         tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{H}x{W}_A{A}_E{E}.json")
-        if os.path.exists(tpath):
+        neumann = args.neighborhood == "neumann"      # the committed profiles are the Neumann configs'
+        if os.path.exists(tpath) and (neumann or args.traffic_json):
             with open(tpath) as f:
                 tj = json.load(f)
             if tj.get("config") == f"{H}x{W}_A{A}_E{E}":
@@ -206,7 +207,7 @@ def main():
         # PMC summary (tools/pmc.sh + tools/valu_json.py)
         valu = None
         vpath = os.path.join(ROOT, "profiles", f"valu_{H}x{W}_A{A}_E{E}.json")
-        if os.path.exists(vpath):
+        if os.path.exists(vpath) and neumann:
             with open(vpath) as f:
                 vj = json.load(f)
             if vj.get("config") == f"{H}x{W}_A{A}_E{E}":
@@ -350,20 +351,22 @@ def cpu_share():
                                "omp_num_threads": omp or None, "cpu_model": model}
 
 
-def learner_bytes_per_env_step(H, W, A, D):
+def learner_bytes_per_env_step(H, W, A, D, actions=5):
     """Algorithmic HBM bytes of one learning step of one env at full occupancy
     (DESIGN.md section 9.4): the ffm_core state round trip, 2*(2A + 4HW + 4),
     plus per agent two V reads (key + value, 16 B each) and one fixed-point
     increment (8 B read + 8 B write), and for actor variants the H row (8 B key +
-    40 B values) and its increment (16 B)."""
-    per_agent = 2 * 16 + 16 + (8 + 40 + 16)
+    8 B per action: 40 B Neumann, 72 B Moore) and its increment (16 B)."""
+    per_agent = 2 * 16 + 16 + (8 + 8 * actions + 16)
     return 2 * (2 * A + 4 * H * W + 4) + A * per_agent
 
 
 def bench_learner(args, world, rank, torch, dist):
     from ffm_amd.data import make_room, l1_sff
     from ffm_amd.engine import Learner
-    cfg = LEARN_CONFIGS[args.config]
+    cfg = dict(LEARN_CONFIGS[args.config])
+    if args.neighborhood != "neumann":     # a variant of the workload (the BASELINE configs are Neumann)
+        cfg["params"] = dict(cfg["params"], neighborhood=args.neighborhood)
     H = W = args.size
     A, E = args.agents, args.envs
     m = make_room(H, W)
@@ -408,12 +411,12 @@ def bench_learner(args, world, rank, torch, dist):
     v_size, h_size = L.table_size("V"), L.table_size("H")
     if rank == 0:
         D = 4 if cfg["variant"] == "actor_only" else 1
-        bpe = learner_bytes_per_env_step(H, W, A, D)
+        bpe = learner_bytes_per_env_step(H, W, A, D, 9 if args.neighborhood == "moore" else 5)
         achieved = E * bpe / (step_ms / 1e3) / 1e9
         # PMC HBM bytes of the batch kernel (tools/traffic.sh <out> --config 4|5)
         traffic = traffic_src = None
         tpath = os.path.join(ROOT, "profiles", f"traffic_{H}x{W}_A{A}_E{E}_learn{args.config}.json")
-        if os.path.exists(tpath):
+        if os.path.exists(tpath) and args.neighborhood == "neumann":     # (profiled on the Neumann configs)
             with open(tpath) as f:
                 tj = json.load(f)
             if tj.get("config") == f"{H}x{W}_A{A}_E{E}_learn{args.config}":
@@ -428,7 +431,8 @@ def bench_learner(args, world, rank, torch, dist):
                 "workload": (f"config {args.config}: {cfg['variant']}"
                              f"{'/' + cfg['mode'] if cfg['mode'] else ''} learning step, {H}x{W} room, "
                              f"{A} agents/env, {E} envs/GPU, epsilon {cfg['params']['epsilon']}, "
-                             f"max_steps {cfg['max_steps']}, Philox seed {args.seed}, on-device auto-reset"
+                             + (f"{args.neighborhood} neighbourhood, " if args.neighborhood != "neumann" else "")
+                             + f"max_steps {cfg['max_steps']}, Philox seed {args.seed}, on-device auto-reset"
                              + (f", {args.burn_in}-step untimed burn-in" if args.burn_in else "")
                              + (f"; every {args.steps}-step timed window is one whole episode of every env (the "
                                 f"envs run in lockstep: each episode truncates at max_steps), its start on the "
