@@ -334,7 +334,8 @@ int ffm_learner_step_tiled_apply(ffm_learner* l, const void* d_recs_all, const u
  *     values to v_slot / v_val (out_counts[0] of them, at most v_capacity);
  *   the ranks all-gather v_capacity entries and the count;
  *   step_owner_h: stores the other ranks' V values; actor modes sum this rank's tiles' H
- *     (h_key = slot | action << 28, bit 31 on the first entry of a row another rank's step
+ *     (h_key = slot (bits 0-23) | action << 24 (0-8: Moore's stay is 8), bit 31 on the first
+ *     entry of a row another rank's step
  *     created; h_q = the fixed-point increment; out_counts[1] entries, at most h_capacity)
  *     and write the tiles' H summaries (tsum, tsum_count rows of 5 doubles);
  *   the ranks all-gather h_capacity entries, the count and the summaries;
