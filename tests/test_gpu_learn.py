@@ -327,6 +327,19 @@ def test_learner_philox_contested_exits_match_cpu(nbh, mode):
         _philox_compare("unified", mode, p, 24, 24, 200, 32, 40, max_steps=30, seed=7)
 
 
+@pytest.mark.parametrize("variant,mode", VARIANTS + [("trained", None)])
+@pytest.mark.parametrize("nbh", ["neumann", "moore"])
+def test_learner_philox_interior_exit_all_variants(variant, mode, nbh):
+    """Every learning variant with an exit inside the room (contested exits, terminal
+    transitions of the losers' neighbours), 12x12 at 1,024 envs and a 40x40 room on the
+    256-lane shape; states and tables equal the CPU restatement bit for bit."""
+    p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    p["neighborhood"] = nbh
+    _philox_compare(variant, mode, p, 12, 12, 32, 1024, 80, max_steps=40, seed=23, exit_pos=(6, 5))
+    _philox_compare(variant, mode, dict(p, block_size=5) if variant != "ac" else p, 40, 40, 200, 16, 40,
+                    max_steps=30, seed=24, exit_pos=(20, 21))
+
+
 @pytest.mark.parametrize("mode", ["actor_only", "both"])
 def test_learner_philox_phase_split_step_matches_cpu(monkeypatch, mode):
     """The phase-split batch step (prep / decide / resolve / learn launches,

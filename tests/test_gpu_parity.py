@@ -128,10 +128,11 @@ def test_dropin_model_runs_main_py_config():
 # ---------------------------------------------------------------------------
 # Philox mode: GPU == CPU restatement at scale
 # ---------------------------------------------------------------------------
-def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0, nthreads=16, fused=1):
+def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0, nthreads=16, fused=1,
+                    exit_pos=None):
     from ffm_amd.data import make_room, l1_sff
     from oracle import oracle as O
-    m = make_room(H, W)
+    m = make_room(H, W, exit_pos)
     s = l1_sff(m)
     eng = _engine(map_array=m, sff=s, n_envs=E, n_agents=N, params=params, rng="philox",
                   seed=seed, auto_reset=True, env_base=env_base, envs_per_block=envs_per_block)
@@ -265,6 +266,21 @@ def test_philox_odd_shapes():
     _philox_compare(9, 17, 5, 777, 80, {"k_S": 2, "k_D": 1, "diffuse": 0.25, "decay": 0.3,
                                         "neighborhood": "neumann"}, seed=123)
     _philox_compare(20, 11, 40, 301, 80, {"neighborhood": "moore"}, seed=5, env_base=1 << 20)
+
+
+@pytest.mark.parametrize("epb", [-3, -2, -1, 3])
+@pytest.mark.parametrize("nbh", ["neumann", "moore"])
+def test_philox_interior_exit_all_kernels(nbh, epb):
+    """An exit inside the room (every neighbour of it a free cell: four or eight exit-forced
+    requesters of one cell, so exits are contested and decided by friction draws,
+    model/ffm_core.py:66-72, 90-98) on every step kernel -- group, lane, wave and block --
+    and through K fused steps; positions, counts and DFF equal the CPU restatement."""
+    p = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": nbh}
+    cnt, eps = _philox_compare(12, 12, 32, 2047, 120, p, seed=17, envs_per_block=epb, exit_pos=(6, 5))
+    assert eps.sum() > 0
+    if epb == -3:
+        _philox_compare(12, 12, 32, 1001, 60, p, seed=18, fused=10, exit_pos=(4, 7))
+        _philox_compare(40, 40, 300, 33, 60, p, seed=19, exit_pos=(20, 20))
 
 
 @pytest.mark.parametrize("epb", [-3, -2])
