@@ -134,14 +134,14 @@ def _random_rank_table(H, W, bs, seed=0, frac=0.6, width=5):
 
 def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, seed=42, env_base=0,
                     nthreads=16, sff_dtype=np.float32, log2_cap=22, chunks=1, reset_at=None, expect_tiled=None,
-                    exit_pos=None):
+                    exit_pos=None, room=None):
     """reset_at = (T1, fraction): after T1 steps a random fraction of the envs is re-placed
     through Learner.reset_envs (the CPU side: reset_philox at step index T1 + 1), then the
     remaining T - T1 steps run.  expect_tiled: assert the learner's step path (tiled or not)."""
     from ffm_amd.data import make_room, l1_sff
     from oracle import learn as LO
     from oracle import oracle as O
-    m = make_room(H, W, exit_pos)
+    m = room(H, W) if room is not None else make_room(H, W, exit_pos)
     s = l1_sff(m).astype(sff_dtype)
     A = A or N
     L = _learner(m, s, variant, n_envs=E, n_agents=N, agent_capacity=A, mode=mode, params=params,
@@ -338,6 +338,24 @@ def test_learner_philox_interior_exit_all_variants(variant, mode, nbh):
     _philox_compare(variant, mode, p, 12, 12, 32, 1024, 80, max_steps=40, seed=23, exit_pos=(6, 5))
     _philox_compare(variant, mode, dict(p, block_size=5) if variant != "ac" else p, 40, 40, 200, 16, 40,
                     max_steps=30, seed=24, exit_pos=(20, 21))
+
+
+@pytest.mark.parametrize("variant,mode", VARIANTS + [("trained", None)])
+@pytest.mark.parametrize("nbh", ["neumann", "moore"])
+def test_learner_philox_obstacles_and_two_exits_all_variants(variant, mode, nbh):
+    """Every learning variant on a room with blocked cells inside (an inner wall with a gap,
+    a pillar: the state keys' blocked classes away from the border) and two exits, 12x12 at
+    1,024 envs and 40x40 on the 256-lane shape, then the tiled ffm_unified step on a 64x64
+    room of the same layout."""
+    from test_gpu_parity import obstacle_room
+    p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    p["neighborhood"] = nbh
+    _philox_compare(variant, mode, p, 12, 12, 30, 1024, 80, max_steps=40, seed=33, room=obstacle_room)
+    _philox_compare(variant, mode, dict(p, block_size=5) if variant != "ac" else p, 40, 40, 200, 16, 40,
+                    max_steps=30, seed=34, room=obstacle_room)
+    if variant == "unified":
+        _philox_compare(variant, mode, p, 64, 64, 600, 8, 30, max_steps=20, seed=35, room=obstacle_room,
+                        expect_tiled=True)
 
 
 @pytest.mark.parametrize("mode", ["actor_only", "both"])

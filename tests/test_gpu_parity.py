@@ -128,11 +128,22 @@ def test_dropin_model_runs_main_py_config():
 # ---------------------------------------------------------------------------
 # Philox mode: GPU == CPU restatement at scale
 # ---------------------------------------------------------------------------
+def obstacle_room(H, W):
+    """A room with an inner wall (a gap of two cells), a pillar and two exits (top and left
+    walls): blocked cells inside the room and two exits' SFF basins."""
+    from ffm_amd.data import make_room
+    m = make_room(H, W)
+    m[H // 2, 1:W - 3] = 2                  # inner wall, open at its right end
+    m[H // 4:H // 4 + 2, W // 3:W // 3 + 2] = 2
+    m[H - H // 3, 0] = 3                    # second exit in the left wall
+    return m
+
+
 def _philox_compare(H, W, N, E, T, params, seed=42, env_base=0, envs_per_block=0, nthreads=16, fused=1,
-                    exit_pos=None):
+                    exit_pos=None, room=None):
     from ffm_amd.data import make_room, l1_sff
     from oracle import oracle as O
-    m = make_room(H, W, exit_pos)
+    m = room(H, W) if room is not None else make_room(H, W, exit_pos)
     s = l1_sff(m)
     eng = _engine(map_array=m, sff=s, n_envs=E, n_agents=N, params=params, rng="philox",
                   seed=seed, auto_reset=True, env_base=env_base, envs_per_block=envs_per_block)
@@ -281,6 +292,19 @@ def test_philox_interior_exit_all_kernels(nbh, epb):
     if epb == -3:
         _philox_compare(12, 12, 32, 1001, 60, p, seed=18, fused=10, exit_pos=(4, 7))
         _philox_compare(40, 40, 300, 33, 60, p, seed=19, exit_pos=(20, 20))
+
+
+@pytest.mark.parametrize("epb", [-3, -2, -1, 3])
+@pytest.mark.parametrize("nbh", ["neumann", "moore"])
+def test_philox_obstacles_and_two_exits_all_kernels(nbh, epb):
+    """Blocked cells inside the room (an inner wall with a gap, a pillar) and two exits on
+    every step kernel; a 40x40 room of the same layout on the block kernel."""
+    p = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": nbh}
+    _, eps = _philox_compare(12, 12, 30, 2047, 120, p, seed=27, envs_per_block=epb, room=obstacle_room)
+    assert eps.sum() > 0
+    if epb == -3:
+        _philox_compare(12, 12, 30, 1001, 60, p, seed=28, fused=10, room=obstacle_room)
+        _philox_compare(40, 40, 300, 33, 60, p, seed=29, room=obstacle_room)
 
 
 @pytest.mark.parametrize("epb", [-3, -2])
