@@ -380,6 +380,53 @@ def test_philox_big_maps_global_scratch():
     _philox_compare(110, 110, 12, 64, 400, p, seed=7)
 
 
+@pytest.mark.parametrize("nbh", ["neumann", "moore"])
+@pytest.mark.parametrize("H,N,room", [(12, 30, "obstacles"), (12, 30, "interior"), (40, 200, "obstacles")])
+def test_mt_rooms_match_oracle_stream(H, N, room, nbh):
+    """MT (reference-stream) mode on rooms with inner walls and two exits, and with an exit
+    inside the room (contested exits), against the oracle's MT step: positions, DFF bits and
+    both generators' positions."""
+    import random as pyrandom
+    from ffm_amd.data import make_room, l1_sff
+    from oracle import oracle as O
+    W = H
+    m = obstacle_room(H, W) if room == "obstacles" else make_room(H, W, (H // 2, W // 2 - 1))
+    s = l1_sff(m).astype(np.float64)
+    p = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": nbh}
+    E, T = 3, 60
+    eng = _engine(map_array=m, sff=s, n_envs=E, n_agents=0, agent_capacity=N, params=p, rng="mt",
+                  auto_reset=False)
+    core = O.Core(m, s, p)
+    pos0 = np.full((E, N), 0xFFFF, np.uint16)
+    cpu = []
+    for e in range(E):
+        rs, r = np.random.RandomState(200 + e), pyrandom.Random(200 + e)
+        npr, pyr = O.MT.from_numpy(rs), O.MT.from_python(r)
+        init = core.init_agents_mt(N, npr)
+        pos0[e] = init
+        npr.to_numpy(rs)
+        eng.load_rng_from(e, rs, r)
+        cpu.append([init, np.zeros((H, W), np.float32), npr, pyr])
+    eng.set_state(0, positions=pos0, counts=np.full(E, N, np.int32), dff=np.zeros((E, H, W), np.float32))
+    for _ in range(T):
+        for c in cpu:
+            c[0] = core.step_mt(c[0], c[1], c[2], c[3])
+    eng.step(T)
+    gp, gc, gd = eng.get_state()
+    for e, c in enumerate(cpu):
+        assert gc[e] == len(c[0])
+        assert np.array_equal(gp[e, :gc[e]], c[0]), f"env {e} positions"
+        assert np.array_equal(gd[e].view(np.uint32), c[1].view(np.uint32)), f"env {e} DFF"
+        rs, r = np.random.RandomState(), pyrandom.Random()
+        eng.store_rng_to(e, rs, r)
+        want_np, want_py = np.random.RandomState(), pyrandom.Random()
+        c[2].to_numpy(want_np)
+        c[3].to_python(want_py)
+        assert list(rs._bit_generator.random_raw(4)) == list(want_np._bit_generator.random_raw(4))
+        assert [r.getrandbits(32) for _ in range(4)] == [want_py.getrandbits(32) for _ in range(4)]
+    eng.close()
+
+
 def test_mt_big_map_matches_oracle_stream():
     """MT (reference-stream) mode on a map beyond the LDS: 160x160, 600 agents, f64 SFF
     (main.py's data path), against the oracle's MT step (pinned to the reference by the
