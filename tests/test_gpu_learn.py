@@ -118,6 +118,59 @@ def test_learner_replays_reference_goldens(name):
         L.close()
 
 
+@pytest.mark.parametrize("variant,mode", VARIANTS)
+@pytest.mark.parametrize("nbh", ["neumann", "moore"])
+@pytest.mark.parametrize("room", ["obstacles", "interior"])
+def test_learner_mt_rooms_match_oracle_stream(variant, mode, nbh, room):
+    """MT (reference-stream) learning on rooms the goldens do not hold -- inner walls and two
+    exits, an exit inside the room (contested exits) -- against the oracle's MT learning step
+    (pinned to the reference by the golden replays): positions and DFF after every step,
+    then the V / H tables in insertion (dict) order and both generators' positions."""
+    from oracle import oracle as O
+    from oracle import learn as LO
+    from ffm_amd.data import make_room, l1_sff
+    from test_gpu_parity import obstacle_room
+    H = W = 12
+    m = obstacle_room(H, W) if room == "obstacles" else make_room(H, W, (6, 5))
+    s = l1_sff(m).astype(np.float64)
+    p = {"epsilon": 0.1, "block_size": 1} if variant != "ac" else {}
+    p["neighborhood"] = nbh
+    N, T, seed = 20, 60, 41
+    core = O.Core(m, s, {"neighborhood": "neumann"})
+    L = _learner(m, s, variant, n_envs=1, n_agents=0, agent_capacity=N, mode=mode, params=p, rng="mt",
+                 auto_reset=False)
+    cpu = LO.Learn(m, s, variant, mode, p, log2_cap=20)
+    np_rng, py_rng = O.seeded_np(seed), O.seeded_py(seed)
+    pos = core.init_agents_mt(N, np_rng)
+    cells = np.full((1, N), 0xFFFF, np.uint16)
+    cells[0, :len(pos)] = pos
+    L.set_state(0, positions=cells, counts=np.array([len(pos)], np.int32), dff=np.zeros((1, H, W), np.float32))
+    nk, npos = _mt_words(np_rng)
+    pk, ppos = _mt_words(py_rng)
+    L.set_mt_state(0, nk, npos, pk, ppos)
+    dff = np.zeros((H, W), np.float32)
+    for t in range(T):
+        pos = cpu.step_mt(pos, dff, np_rng, py_rng)
+        L.step(1)
+        gp, gc, gd = L.get_state()
+        assert int(gc[0]) == len(pos), f"step {t}: count"
+        assert np.array_equal(gp[0, :len(pos)], pos), f"step {t}: positions"
+        assert np.array_equal(gd[0].view(np.uint32), dff.view(np.uint32)), f"step {t}: DFF"
+        if len(pos) == 0:
+            break
+    for which, tab in (("V", cpu.V), ("H", cpu.Ht)):
+        ck, cv = tab.export()
+        if which == "H" and len(ck) == 0:     # no actor table (ac, critic_only)
+            continue
+        gk, gv = L.export_table(which)
+        assert np.array_equal(np.asarray(ck, np.uint64), np.asarray(gk, np.uint64)), f"{which} keys / order"
+        assert np.array_equal(np.asarray(cv).view(np.uint64), np.asarray(gv).view(np.uint64)), f"{which} values"
+    nk, npos, pk, ppos = L.get_mt_state(0)
+    assert np.array_equal(nk, np.ctypeslib.as_array(np_rng.mt)) and npos == int(np_rng.pos)
+    assert np.array_equal(pk, np.ctypeslib.as_array(py_rng.mt)) and ppos == int(py_rng.pos)
+    L.close()
+
+
 # ---------------------------------------------------------------------------
 # Philox (batched) mode: GPU == CPU restatement
 # ---------------------------------------------------------------------------
