@@ -270,6 +270,7 @@ def _philox_compare(variant, mode, params, H, W, N, E, T, A=None, max_steps=60, 
     ("actor_only", None, {"epsilon": 0.2}, 12, 32, 4096),
     ("unified", "actor_only", {"block_size": 1}, 12, 32, 2048),
     ("unified", "actor_only", {"block_size": 1}, 64, 512, 16),
+    ("unified", "both", {"block_size": 1, "neighborhood": "moore"}, 64, 512, 16),
 ])
 def test_learner_reset_envs_matches_cpu(variant, mode, params, H, N, E):
     """reset(env_mask) of the batched learner (ffm_learner_reset_envs): a random half of the
@@ -918,8 +919,10 @@ def test_learner_curriculum_schedule_and_episode_log(variant, mode, stride):
     L.close()
 
 
-@pytest.mark.parametrize("variant,mode", [("actor_only", None), ("unified", "actor_only"), ("unified", "critic_only")])
-def test_learner_trajectory_capture_matches_cpu(variant, mode):
+@pytest.mark.parametrize("variant,mode,nbh", [("actor_only", None, "neumann"), ("unified", "actor_only", "neumann"),
+                                              ("unified", "critic_only", "neumann"), ("unified", "critic_only", "moore"),
+                                              ("actor_only", None, "moore")])
+def test_learner_trajectory_capture_matches_cpu(variant, mode, nbh):
     """Batched trajectory capture (run(return_trajectory=True) rows, model/ffm_unified.py:902-931;
     the drivers keep every 100th episode's, run_actor_only_training.py:199-218) against the CPU
     restatement stepped in phases: the positions after every step of every captured episode,
@@ -928,7 +931,7 @@ def test_learner_trajectory_capture_matches_cpu(variant, mode):
     from oracle import learn as LO
     m = make_room(12, 12)
     s = l1_sff(m)
-    p = {"epsilon": 0.1, "block_size": 1}
+    p = {"epsilon": 0.1, "block_size": 1, "neighborhood": nbh}
     E, N, T, seed, maxs = 96, 12, 120, 11, 30
     sel = np.array([0, 5, 17, 42, 95], np.int32)
     ph = np.array([0, 1, 2, 1, 0], np.int32)
