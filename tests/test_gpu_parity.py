@@ -378,6 +378,9 @@ def test_philox_big_maps_global_scratch():
     _philox_compare(256, 256, 8192, 6, 40, p, seed=5)
     _philox_compare(150, 150, 2000, 16, 60, dict(p, neighborhood="moore"), seed=6, env_base=77)
     _philox_compare(110, 110, 12, 64, 400, p, seed=7)
+    # inner walls and two exits beyond the LDS (the global-scratch grid's blocked cells)
+    _philox_compare(150, 150, 2000, 8, 40, dict(p, neighborhood="moore"), seed=8, room=obstacle_room)
+    _philox_compare(256, 256, 4000, 4, 30, p, seed=9, room=obstacle_room)
 
 
 @pytest.mark.parametrize("nbh", ["neumann", "moore"])
