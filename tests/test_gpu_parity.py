@@ -186,8 +186,10 @@ def test_philox_config2_full_size_matches_cpu(epb):
     assert eps.sum() > 0  # auto-reset exercised
 
 
-@pytest.mark.parametrize("H,N,E,epb", [(12, 32, 65536, 0), (12, 32, 4096, -2), (64, 512, 48, 0), (110, 60, 6, 0)])
-def test_engine_reset_envs_matches_cpu(H, N, E, epb):
+@pytest.mark.parametrize("H,N,E,epb,nbh", [(12, 32, 65536, 0, "neumann"), (12, 32, 4096, -2, "neumann"),
+                                          (64, 512, 48, 0, "neumann"), (110, 60, 6, 0, "neumann"),
+                                          (12, 32, 4096, 0, "moore"), (64, 512, 48, 0, "moore")])
+def test_engine_reset_envs_matches_cpu(H, N, E, epb, nbh):
     """reset(env_mask) through the ABI (ffm_engine_reset_envs): mid-run, a random
     third of the envs is re-placed (C2's 65,536 envs on the group kernel, the lane kernel, and
     C3's 64x64 room); the oracle re-places the same envs with reset_philox at the same step
@@ -197,7 +199,7 @@ def test_engine_reset_envs_matches_cpu(H, N, E, epb):
     import torch
     from ffm_amd.data import make_room, l1_sff
     from oracle import oracle as O
-    params = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": "neumann"}
+    params = {"k_S": 3, "k_D": 1, "diffuse": 0.2, "decay": 0.2, "neighborhood": nbh}
     m = make_room(H, H)
     s = l1_sff(m)
     seed, T1, T2 = 11, 25, 25
